@@ -1,0 +1,181 @@
+"""bench.py — Mdisparities/s of the census+CBCA+SGM+WTA hot path on MI355X.
+
+Contract (driver): python bench.py --gpus N --steps K --warmup W ; for N > 1 launched by
+torch.distributed.run, one rank per GPU.  A step = one pass of the whole hot path
+(cost volume -> CBCA x2 -> SolveAll -> 4-path SGM -> WTA) over one batch of synthetic pairs
+already resident in HBM.  Pairs shard across ranks with no data-path collective (weak scaling:
+each rank owns its own batch); RCCL is used only for the barrier and the max-over-ranks time.
+
+Default workload = BASELINE.json configs[1]: Middlebury Teddy size 450x375, D = 64 (maxdisp 63),
+the bit-exact default path.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mdisparities/s (W×H×D/s) + Middlebury bad-2.0 %, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # name: (H, W, max_disp, sgm_paths, pairs per GPU, description)
+    "teddy": (375, 450, 63, 4, 16, "Middlebury Teddy 450x375 D=64, censusGrad+CBCA(2 it)+SolveAll+SGM 4-path+WTA "
+                                   "(BASELINE configs[1], bit-exact path)"),
+    "kitti": (375, 1242, 191, 8, 4, "KITTI-2015 1242x375 D=192, censusGrad+CBCA+SGM 8-path+WTA (configs[2])"),
+    "fullres": (2000, 3000, 255, 4, 1, "Middlebury-2014 full-res 3000x2000 D=256, censusGrad+CBCA+SGM 4-path+WTA (configs[3])"),
+    "hd": (1080, 1920, 255, 4, 8, "1920x1080 D=256 synthetic pairs, censusGrad+CBCA+SGM 4-path+WTA (configs[4] per-GPU shard)"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="teddy", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="pairs per GPU (0 = workload default)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
+    return ap.parse_args()
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus and world > 1:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    return world, rank, local
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args.gpus)
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from mystereomatching_amd import StereoBatch
+    from mystereomatching_amd import synthetic as S
+    from mystereomatching_amd.evaluate import cal_err
+
+    H, W, md, paths, B0, desc = WORKLOADS[args.workload]
+    B = args.batch or B0
+    D = md + 1
+    # this rank's shard of the global batch: pair indices [rank*B, rank*B + B)
+    batch = S.make_batch(B, H, W, D, first_index=rank * B)
+    sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths)
+    sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        sb.run(0.3, download=False)
+    sb.synchronize()
+    profile = not args.no_profile
+    if profile:
+        sb.profile(True)
+        sb.profile_reset()
+
+    barrier()
+    torch.cuda.synchronize()
+    sb.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sb.run(0.3, download=False)
+    sb.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernels = sb.profile_read() if profile else {}
+    sb.profile(False)
+    disp = sb.download()
+    bad2 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 2.0)[0] for i in range(B)]))
+    bad1 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 1.0)[0] for i in range(B)]))
+
+    elems_per_step = world * B * H * W * D
+    value = elems_per_step * args.steps / elapsed / 1e6
+
+    roofline = None
+    kern_out = {}
+    if kernels:
+        tot = sum(k["total_ms"] for k in kernels.values())
+        for name, k in kernels.items():
+            if k["launches"] == 0:
+                continue
+            avg = k["total_ms"] / k["launches"]
+            gbs = k["bytes_per_launch"] / (avg * 1e-3) / 1e9
+            kern_out[name] = {"avg_ms": round(avg, 4), "share": round(k["total_ms"] / tot, 4),
+                              "GB_s": round(gbs, 1), "bytes_per_launch": k["bytes_per_launch"]}
+        dom = max(kern_out, key=lambda n: kernels[n]["total_ms"])
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_b{B}.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        ach = kern_out[dom]["GB_s"]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "bytes_per_launch": kern_out[dom]["bytes_per_launch"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        cfg = O.config(H, W, md, sgm_paths=paths)
+        n, t_cpu = 0, 0.0
+        while n == 0 or (t_cpu < args.cpu_seconds and n < B):
+            pair = {k: batch[k][n] for k in ("lbgr", "rbgr", "lgray", "rgray")}
+            t = time.perf_counter()
+            r = O.run(pair, cfg)
+            t_cpu += time.perf_counter() - t
+            if not np.array_equal(r["disp"], disp[n]):
+                raise SystemExit(f"bench: GPU disparity of pair {n} differs from the CPU restatement")
+            n += 1
+        cpu = {"value": round(n * H * W * D / t_cpu / 1e6, 3), "unit": "Mdisp/s", "cores": 1, "kind": "port",
+               "sample": f"{n} of the {B} bench pairs ({W}x{H} D={D}) through oracle/sm_oracle.c, 1 thread, "
+                         f"{t_cpu:.1f} s; GPU maps checked bit-exact against it"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mdisp/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded piecewise-planar pairs, mystereomatching_amd/synthetic.py)",
+            "config": {"workload": desc, "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": B * world,
+                       "sgm_paths": paths, "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
+            "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kern_out,
+        }
+        if cpu:
+            out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(out))
+    sb.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

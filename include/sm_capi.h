@@ -1,0 +1,142 @@
+/*
+ * sm_capi.h — C-ABI of the MI355X stereo-matching back end (libsm_hip.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: the calls that
+ * main_.cpp makes on class StereoMatching (reference main_.cpp:138-172) map one-to-one onto the
+ * entry points below.  Plain pointers and sizes only; no exceptions, no exit(), no globals:
+ * every call returns an sm_status and sm_last_error(ctx) holds the message.
+ *
+ * Reference interface each entry point replaces (paths relative to the reference root):
+ *   sm_params_default  <- StereoMatching::Parameters::Parameters     stereoMatching.h:204-350
+ *   sm_create          <- StereoMatching::StereoMatching (ctor)      stereoMatching.cpp:2058-2110
+ *   sm_set_images      <- ctor image arguments I1_c,I2_c,I1_g,I2_g   stereoMatching.cpp:2063-2071
+ *   sm_cost_calculate  <- StereoMatching::costCalculate              stereoMatching.cpp:945-1021
+ *   sm_solve_all       <- SolveAll(StereoMatching**&, PY_LVL, REG_LAMBDA)  stereoMatching.cpp:2142-2208
+ *   sm_disp_optimize   <- StereoMatching::dispOptimize + DP[0]       stereoMatching.cpp:1046-1136, h:2724
+ *   sm_get_volume      <- public member vm[view]                     stereoMatching.h:2720
+ *   sm_get_arms        <- public member HVL[view]                    stereoMatching.h:2717
+ *   sm_destroy         <- delete smPsy[p]                            main_.cpp:173-178
+ *   sm_run / sm_run_batch  <- the whole main_.cpp:139-163 sequence for n independent pairs
+ * Threading: one sm_ctx per host thread; each ctx owns one HIP stream on its device.
+ */
+#ifndef SM_CAPI_H
+#define SM_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define SM_API __attribute__((visibility("default")))
+#else
+#define SM_API
+#endif
+
+typedef enum sm_status {
+    SM_OK = 0,
+    SM_EINVAL = 1,   /* bad argument / unsupported parameter combination */
+    SM_ENOMEM = 2,   /* device or host allocation failed */
+    SM_EHIP = 3,     /* HIP runtime error (launch, copy, sync) */
+    SM_ESTATE = 4,   /* call out of order (e.g. optimize before cost) */
+} sm_status;
+
+/* static std::string costcalculation / aggregation / optimization selectors (h:51-53). */
+typedef enum sm_cost_method {
+    SM_COST_CENSUS_GRAD = 0, /* "censusGrad" (main:15; cpp:25-48) — default */
+    SM_COST_CENSUS = 1,      /* "Census"     (cpp:975-976) */
+    SM_COST_AD_CENSUS = 2,   /* "ADCensus"   (cpp:894-915, 5250-5277) */
+    SM_COST_AD = 3,          /* "AD"         (cpp:954-955) */
+} sm_cost_method;
+
+typedef enum sm_aggregation {
+    SM_AGG_NONE = 0,
+    SM_AGG_CBCA = 1,         /* "CBCA" (main:16; cpp:1002-1003) — default */
+} sm_aggregation;
+
+typedef enum sm_optimization {
+    SM_OPT_WTA = 0,          /* "" : WTA only (cpp:1104-1128) */
+    SM_OPT_SGM = 1,          /* "sgm" (main:17; cpp:1051-1060) — default */
+} sm_optimization;
+
+/* The subset of StereoMatching::Parameters (h:85-351) that the hot path reads, plus the
+ * static selectors.  Field defaults come from sm_params_default (= the reference ctor). */
+typedef struct sm_params {
+    int32_t rows, cols;          /* h_, w_ */
+    int32_t num_disparities;     /* numDisparities = maxDisp + 1 (h:209) */
+    int32_t cost_method;         /* sm_cost_method */
+    int32_t aggregation;         /* sm_aggregation */
+    int32_t optimization;        /* sm_optimization */
+    int32_t census_rv, census_ru;/* census window radii {3, 4} (cpp:815) */
+    int32_t census_ring;         /* censusFunc == 3 -> 8 ring bits (h:244) */
+    float lam_cen, lam_g;        /* lamCen = 13, lamG = 1 (main:56-57) */
+    float grad_trunc;            /* 500 (cpp:34) */
+    int32_t grad_adaptive;       /* gradFuse_adpWgt = 1 (h:245) */
+    float lam_ad, lam_cen_adc;   /* ADCensus fusion constants 10, 30 (cpp:5270) */
+    float ad_trunc_adc;          /* 1000 (cpp:905) */
+    float ad_trunc_ad;           /* 20 (cpp:955) */
+    int32_t arm_l, arm_l_out;    /* cbca_crossL[0] = 17, cbca_crossL_out[0] = 34 (h:263, 266) */
+    int32_t arm_c_thresh, arm_c_thresh_out; /* cbca_cTresh[0] = 20, cbca_cTresh_out[0] = 6 */
+    int32_t arm_min_l;           /* cbca_minArmL = 1 (h:259) */
+    int32_t cbca_iterations;     /* cbca_iterationNum = 2 (h:260) */
+    int32_t sgm_paths;           /* 4 (cpp:6214) or 8 (full table cpp:6207-6208) */
+    float sgm_p1, sgm_p2;        /* 1.0, 3.0 (h:2234-2235) */
+    int32_t sgm_cor_dif_thres;   /* 15 (h:239) */
+    int32_t sgm_redu_coeff;      /* 4 (h:240) */
+    int32_t compute_right_view;  /* build vm[1] too (Do_LRConsis, h:72); 0 = skip (unused downstream) */
+    int32_t keep_final_volume;   /* write the SGM path-sum back into vm[0] (reference does); 0 = fuse into WTA */
+    int32_t batch_capacity;      /* max pairs per sm_run call (device buffers sized for it) */
+} sm_params;
+
+typedef struct sm_ctx sm_ctx;
+
+SM_API void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t cols);
+SM_API sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device);
+SM_API sm_status sm_destroy(sm_ctx* ctx);
+SM_API const char* sm_last_error(const sm_ctx* ctx);
+SM_API const char* sm_status_string(sm_status s);
+
+/* Single-pair, reference-ordered API (pair slot 0).  Host buffers: BGR u8 rows of
+ * `cstride` bytes, gray u8 rows of `gstride` bytes; copied to the device. */
+SM_API sm_status sm_set_images(sm_ctx* ctx, const uint8_t* lbgr, const uint8_t* rbgr, size_t cstride,
+                               const uint8_t* lgray, const uint8_t* rgray, size_t gstride);
+SM_API sm_status sm_cost_calculate(sm_ctx* ctx);
+SM_API sm_status sm_solve_all(sm_ctx* ctx, int32_t py_lev, float reg_lambda);
+SM_API sm_status sm_disp_optimize(sm_ctx* ctx, int16_t* disp_out);
+SM_API sm_status sm_get_volume(sm_ctx* ctx, int32_t view, float* dst);   /* H*W*D floats */
+SM_API sm_status sm_get_arms(sm_ctx* ctx, int32_t view, uint16_t* dst);  /* H*W*4 (L,R,U,D) */
+
+/* Batched, device-resident API.  Inputs are packed [n][H][W][3] (BGR) and [n][H][W] (gray). */
+SM_API sm_status sm_upload_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
+                                 const uint8_t* lgray, const uint8_t* rgray);
+/* Run cost -> CBCA -> SolveAll(py_lev=1, reg_lambda) -> SGM -> WTA on the n uploaded pairs.
+ * Asynchronous on the ctx stream.  disp_out: host [n][H][W] int16 (synchronous copy-back) or
+ * NULL to leave the maps on the device (read them with sm_download_disp). */
+SM_API sm_status sm_run(sm_ctx* ctx, int32_t n, float reg_lambda, int16_t* disp_out);
+SM_API sm_status sm_download_disp(sm_ctx* ctx, int32_t n, int16_t* disp_out);
+SM_API sm_status sm_run_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
+                              const uint8_t* lgray, const uint8_t* rgray, float reg_lambda,
+                              int16_t* disp_out);
+SM_API sm_status sm_synchronize(sm_ctx* ctx);
+SM_API void* sm_stream(sm_ctx* ctx);      /* the ctx's hipStream_t */
+
+/* Per-kernel timing with HIP events on the ctx stream. */
+SM_API sm_status sm_profile_enable(sm_ctx* ctx, int32_t on);
+/* Fills up to max entries: name (NUL-terminated, 48 chars max), launches, total ms,
+ * algorithmic bytes per launch.  Returns the number of distinct kernels in *count. */
+SM_API sm_status sm_profile_read(sm_ctx* ctx, int32_t max, char* names /* max*48 */, int64_t* launches,
+                                 double* total_ms, double* bytes_per_launch, int32_t* count);
+SM_API sm_status sm_profile_reset(sm_ctx* ctx);
+
+/* Diagnostics used by the parity tests. */
+SM_API float sm_expf_host(float x);   /* the device expf algorithm, evaluated on the host */
+/* Device expf over the float bit patterns [first_bits, first_bits + n) into host out[n]. */
+SM_API sm_status sm_expf_device_range(sm_ctx* ctx, uint32_t first_bits, uint32_t n, float* out);
+SM_API sm_status sm_get_census(sm_ctx* ctx, int32_t view, uint64_t* dst); /* H*W*2 words */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SM_CAPI_H */

@@ -1,0 +1,118 @@
+// stereo_matching.hpp — header-only C++ facade with the reference's class API over sm_capi.h.
+//
+// A user of the reference replaces `#include "stereoMatching.h"` by this header and keeps the
+// main_.cpp call sequence (main_.cpp:138-172):
+//
+//   smamd::StereoMatching::Parameters param(maxDisp, rows, cols, lamCen, lamG, M, lamc, ts, csv, disSc);
+//   auto* sm = new smamd::StereoMatching(I1_c, I2_c, I1, I2, param);
+//   sm->costCalculate();                       // stereoMatching.cpp:945-1021
+//   smamd::SolveAll(&sm, 1, 0.3f);             // stereoMatching.cpp:2142-2208
+//   sm->dispOptimize();                        // stereoMatching.cpp:1046-1136
+//   const int16_t* disparity = sm->DP[0].data();
+//
+// Images are plain views (smamd::Mat: rows, cols, channels, step, data) instead of cv::Mat so
+// the facade needs no OpenCV; with OpenCV available, wrap a cv::Mat as {m.rows, m.cols,
+// m.channels(), m.step, m.data}.  Non-OK statuses become std::runtime_error (the reference threw
+// cv::Exception from CV_Assert).
+#pragma once
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sm_capi.h"
+
+namespace smamd {
+
+struct Mat {
+    int rows = 0, cols = 0, channels = 1;
+    size_t step = 0;          // bytes per row
+    const uint8_t* data = nullptr;
+};
+
+class StereoMatching {
+   public:
+    // static selectors (stereoMatching.h:51-53)
+    inline static std::string costcalculation = "censusGrad";
+    inline static std::string aggregation = "CBCA";
+    inline static std::string optimization = "sgm";
+    static constexpr bool Do_refine = false;   // h:70
+    static constexpr bool Do_LRConsis = true;  // h:72
+
+    struct Parameters {  // StereoMatching::Parameters (h:85-351), the fields the hot path reads
+        int numDisparities, rows, cols;
+        int lamCen, lamG, disSc;
+        int censusFunc = 3;
+        int cbca_iterationNum = 2, cbca_minArmL = 1;
+        int cbca_crossL0 = 17, cbca_crossL_out0 = 34, cbca_cTresh0 = 20, cbca_cTresh_out0 = 6;
+        int sgm_scanNum = 4, sgm_corDifThres = 15, sgm_reduCoeffi1 = 4;
+        int errorThreshold = 1;
+        Parameters(int maxDisp, int h, int w, int lamCen_ = 13, int lamG_ = 1, int /*M*/ = 2, int /*lamc*/ = 109,
+                   int /*ts*/ = 10, const std::string& /*errCsvName*/ = "", int disSc_ = 1)
+            : numDisparities(maxDisp + 1), rows(h), cols(w), lamCen(lamCen_), lamG(lamG_), disSc(disSc_) {}
+    };
+
+    StereoMatching(const Mat& I1_c, const Mat& I2_c, const Mat& I1_g, const Mat& I2_g, const Parameters& param,
+                   int hip_device = 0)
+        : h_(I1_c.rows), w_(I1_c.cols), d_(param.numDisparities) {
+        if (param.disSc != 1) throw std::invalid_argument("only PY_LEV = 1 (disSc = 1) is supported");
+        sm_params p;
+        sm_params_default(&p, param.numDisparities - 1, I1_c.rows, I1_c.cols);
+        p.cost_method = costcalculation == "censusGrad" ? SM_COST_CENSUS_GRAD
+                        : costcalculation == "Census"   ? SM_COST_CENSUS
+                        : costcalculation == "ADCensus" ? SM_COST_AD_CENSUS
+                        : costcalculation == "AD"       ? SM_COST_AD
+                                                        : -1;
+        if (p.cost_method < 0) throw std::invalid_argument("unsupported costcalculation: " + costcalculation);
+        if (aggregation != "CBCA" && !aggregation.empty()) throw std::invalid_argument("unsupported aggregation: " + aggregation);
+        if (optimization != "sgm" && !optimization.empty()) throw std::invalid_argument("unsupported optimization: " + optimization);
+        p.aggregation = aggregation == "CBCA" ? SM_AGG_CBCA : SM_AGG_NONE;
+        p.optimization = optimization == "sgm" ? SM_OPT_SGM : SM_OPT_WTA;
+        p.census_ring = param.censusFunc == 3;
+        p.lam_cen = (float)param.lamCen;
+        p.lam_g = (float)param.lamG;
+        p.arm_l = param.cbca_crossL0;
+        p.arm_l_out = param.cbca_crossL_out0;
+        p.arm_c_thresh = param.cbca_cTresh0;
+        p.arm_c_thresh_out = param.cbca_cTresh_out0;
+        p.arm_min_l = param.cbca_minArmL;
+        p.cbca_iterations = param.cbca_iterationNum;
+        p.sgm_paths = param.sgm_scanNum;
+        p.sgm_cor_dif_thres = param.sgm_corDifThres;
+        p.sgm_redu_coeff = param.sgm_reduCoeffi1;
+        check(sm_create(&ctx_, &p, hip_device), "sm_create");
+        if (I1_c.channels != 3 || I2_c.channels != 3 || I1_g.channels != 1 || I2_g.channels != 1)
+            throw std::invalid_argument("expected BGR colour and single-channel gray images");
+        check(sm_set_images(ctx_, I1_c.data, I2_c.data, I1_c.step, I1_g.data, I2_g.data, I1_g.step), "sm_set_images");
+    }
+    ~StereoMatching() { sm_destroy(ctx_); }
+    StereoMatching(const StereoMatching&) = delete;
+    StereoMatching& operator=(const StereoMatching&) = delete;
+
+    void costCalculate() { check(sm_cost_calculate(ctx_), "costCalculate"); }
+    void dispOptimize() {
+        DP[0].resize((size_t)h_ * w_);
+        check(sm_disp_optimize(ctx_, DP[0].data()), "dispOptimize");
+    }
+    void refine() { throw std::logic_error("refine(): Do_refine = 0 in the reference (h:70); not built"); }
+    std::vector<float> volume(int view = 0) {
+        std::vector<float> v((size_t)h_ * w_ * d_);
+        check(sm_get_volume(ctx_, view, v.data()), "vm");
+        return v;
+    }
+
+    std::vector<int16_t> DP[2];  // DP[0]: int16 H x W disparity, -1 = invalid (h:2724)
+    int h_, w_, d_;
+    sm_ctx* ctx_ = nullptr;
+
+   private:
+    void check(sm_status s, const char* what) {
+        if (s != SM_OK) throw std::runtime_error(std::string(what) + ": " + sm_last_error(ctx_));
+    }
+    friend void SolveAll(StereoMatching** smPyr, int PY_LVL, float REG_LAMBDA);
+};
+
+inline void SolveAll(StereoMatching** smPyr, int PY_LVL, float REG_LAMBDA) {
+    smPyr[0]->check(sm_solve_all(smPyr[0]->ctx_, PY_LVL, REG_LAMBDA), "SolveAll");
+}
+
+}  // namespace smamd

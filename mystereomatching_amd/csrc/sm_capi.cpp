@@ -1,0 +1,647 @@
+// sm_capi.cpp — C-ABI of libsm_hip.so: context, HBM buffers, stage drivers, profiling.
+// The entry points mirror the reference's StereoMatching call sequence (see include/sm_capi.h
+// for the file:line of each reference interface).  No exceptions cross the ABI.
+#include "../../include/sm_capi.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "sm_kernels.h"
+
+namespace {
+
+struct ProfRec {
+    int kernel;
+    hipEvent_t start, stop;
+};
+
+struct ProfStat {
+    int64_t launches = 0;
+    double total_ms = 0;
+    double bytes = 0;  // algorithmic bytes per launch (last seen)
+};
+
+}  // namespace
+
+struct sm_ctx {
+    sm_params p{};
+    int device = 0;
+    hipStream_t st = nullptr;
+    std::string err;
+    int cap = 1;
+    size_t npix = 0, nvol = 0;
+    uint8_t* bgr = nullptr;     // [cap][2][npix][3]
+    uint8_t* gray = nullptr;    // [cap][2][npix]
+    ulonglong2* code = nullptr; // [cap][2][npix]
+    float* gx = nullptr;        // [cap][2][npix]
+    float* gy = nullptr;
+    uint8_t* arms = nullptr;    // [cap][2][npix][4]
+    float* vm0 = nullptr;       // [cap][npix][D]
+    float* vm1 = nullptr;       // [cap][npix][D] (right view, optional)
+    float* acc = nullptr;       // [cap][npix][D]
+    int16_t* disp = nullptr;    // [cap][npix]
+    int n_loaded = 0;
+    int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized
+    float lut_a[1024], lut_b[1024];
+    float ad_oor_exp = 0;
+    // profiling
+    bool prof = false;
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> free_events;
+    std::vector<std::string> knames;
+    std::map<std::string, int> kidx;
+    std::vector<ProfStat> kstat;
+};
+
+namespace {
+
+sm_status fail(sm_ctx* c, sm_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+sm_status hip_fail(sm_ctx* c, hipError_t e, const char* where) {
+    return fail(c, SM_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(c, expr)                                      \
+    do {                                                      \
+        hipError_t e_ = (expr);                               \
+        if (e_ != hipSuccess) return hip_fail((c), e_, #expr); \
+    } while (0)
+
+hipEvent_t get_event(sm_ctx* c) {
+    if (!c->free_events.empty()) {
+        hipEvent_t e = c->free_events.back();
+        c->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int kernel_id(sm_ctx* c, const char* name, double bytes) {
+    auto it = c->kidx.find(name);
+    int id;
+    if (it == c->kidx.end()) {
+        id = (int)c->knames.size();
+        c->kidx[name] = id;
+        c->knames.push_back(name);
+        c->kstat.emplace_back();
+    } else {
+        id = it->second;
+    }
+    c->kstat[id].bytes = bytes;
+    return id;
+}
+
+// Brackets one launch with events when profiling is on.
+template <typename F>
+sm_status timed(sm_ctx* c, const char* name, double bytes, F&& launch) {
+    ProfRec r{-1, nullptr, nullptr};
+    if (c->prof) {
+        r.kernel = kernel_id(c, name, bytes);
+        r.start = get_event(c);
+        r.stop = get_event(c);
+        if (r.start) hipEventRecord(r.start, c->st);
+    }
+    launch();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(c, e, name);
+    if (c->prof && r.start && r.stop) {
+        hipEventRecord(r.stop, c->st);
+        c->recs.push_back(r);
+    }
+    return SM_OK;
+}
+
+int census_len(const sm_params& p) { return (2 * p.census_rv + 1) * (2 * p.census_ru + 1) + (p.census_ring ? 8 : 0); }
+
+bool needs_census(const sm_params& p) { return p.cost_method != SM_COST_AD; }
+bool needs_arms(const sm_params& p) { return p.cost_method == SM_COST_CENSUS_GRAD || p.aggregation == SM_AGG_CBCA; }
+
+int cbca_lag(const sm_params& p) { return p.arm_l_out > p.arm_min_l ? p.arm_l_out : p.arm_min_l; }
+
+sm_status validate(const sm_params& p, std::string& why) {
+    auto bad = [&](const char* m) { why = m; return SM_EINVAL; };
+    if (p.rows < 2 || p.cols < 2) return bad("rows and cols must be >= 2 (calGrad reads I[1] and I[w-2])");
+    if ((long long)p.rows * p.cols > (1LL << 30)) return bad("rows*cols too large");
+    if (p.num_disparities < 1 || p.num_disparities > 1024) return bad("num_disparities must be in [1, 1024]");
+    if (p.cost_method < 0 || p.cost_method > 3) return bad("unknown cost_method");
+    if (p.aggregation < 0 || p.aggregation > 1) return bad("unknown aggregation");
+    if (p.optimization < 0 || p.optimization > 1) return bad("unknown optimization");
+    if (p.census_rv < 0 || p.census_ru < 0 || census_len(p) > 128) return bad("census code longer than 128 bits");
+    if (p.arm_l_out < 0 || p.arm_l_out > 84 || p.arm_min_l < 0 || p.arm_min_l > 84 || p.arm_l < 0)
+        return bad("arm lengths must be in [0, 84]");
+    if (p.cbca_iterations < 0 || p.cbca_iterations > 64) return bad("cbca_iterations must be in [0, 64]");
+    if (p.sgm_paths < 1 || p.sgm_paths > 8) return bad("sgm_paths must be in [1, 8]");
+    if (p.sgm_redu_coeff == 0) return bad("sgm_redu_coeff must be non-zero");
+    if (p.batch_capacity < 1) return bad("batch_capacity must be >= 1");
+    if (p.lam_cen == 0 || p.lam_g == 0 || p.lam_ad == 0 || p.lam_cen_adc == 0) return bad("fusion lambdas must be non-zero");
+    return SM_OK;
+}
+
+void build_luts(sm_ctx* c) {
+    const sm_params& p = c->p;
+    for (int i = 0; i < 1024; i++) {
+        c->lut_a[i] = 0;
+        c->lut_b[i] = 0;
+    }
+    if (p.cost_method == SM_COST_CENSUS_GRAD) {
+        for (int i = 0; i < 1024; i++) c->lut_a[i] = expf(-(float)i / p.lam_cen);    // cpp:3585, ARU0 = lamCen
+    } else if (p.cost_method == SM_COST_AD_CENSUS) {
+        for (int i = 0; i < 1024; i++) c->lut_a[i] = expf(-(float)i / p.lam_cen_adc); // census term, ARU1 = 30
+        for (int s = 0; s < 1024; s++) {
+            float ad = (float)s / 3;  // sum / channels (cpp:2504)
+            if (p.ad_trunc_adc < ad) ad = p.ad_trunc_adc;
+            c->lut_b[s] = expf(-ad / p.lam_ad);                                        // AD term, ARU0 = 10
+        }
+        c->ad_oor_exp = expf(-p.ad_trunc_adc / p.lam_ad);
+    }
+}
+
+template <typename T>
+sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)ptr, count * sizeof(T));
+    if (e != hipSuccess) {
+        *ptr = nullptr;
+        return fail(c, SM_ENOMEM, std::string("hipMalloc(") + std::to_string(count * sizeof(T)) + " B) failed: " + hipGetErrorString(e));
+    }
+    return SM_OK;
+}
+
+void free_all(sm_ctx* c) {
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms, c->vm0, c->vm1, c->acc, c->disp};
+    for (void* q : ptrs)
+        if (q) hipFree(q);
+    for (auto& r : c->recs) {
+        if (r.start) hipEventDestroy(r.start);
+        if (r.stop) hipEventDestroy(r.stop);
+    }
+    for (auto e : c->free_events) hipEventDestroy(e);
+    c->recs.clear();
+    c->free_events.clear();
+    if (c->st) hipStreamDestroy(c->st);
+}
+
+// ---- stage drivers (all asynchronous on c->st) -------------------------------------------
+
+sm_status run_prep(sm_ctx* c, int n) {
+    const sm_params& p = c->p;
+    const int H = p.rows, W = p.cols;
+    if (needs_census(p) || p.cost_method == SM_COST_CENSUS_GRAD) {
+        sm_status s = timed(c, "census_grad", (double)n * 2 * c->npix * (1 + 16 + 8), [&] {
+            sm::launch_census_grad(c->gray, c->code, c->gx, c->gy, n, H, W, p.census_rv, p.census_ru, p.census_ring, c->st);
+        });
+        if (s) return s;
+    }
+    if (needs_arms(p)) {
+        sm_status s = timed(c, "arms", (double)n * 2 * c->npix * (3 + 4), [&] {
+            sm::launch_arms(c->bgr, c->arms, n, H, W, p.arm_l, p.arm_l_out, p.arm_c_thresh, p.arm_c_thresh_out,
+                            p.arm_min_l, c->st);
+        });
+        if (s) return s;
+    }
+    return SM_OK;
+}
+
+sm_status run_cost(sm_ctx* c, int n, int view) {
+    const sm_params& p = c->p;
+    sm::CostArgs a{};
+    a.vm = view == 0 ? c->vm0 : c->vm1;
+    a.code = c->code;
+    a.gx = c->gx;
+    a.gy = c->gy;
+    a.arms = c->arms;
+    a.bgr = c->bgr;
+    a.H = p.rows;
+    a.W = p.cols;
+    a.D = p.num_disparities;
+    a.view = view;
+    a.nwords = (census_len(p) + 63) / 64;
+    a.census_default = (float)census_len(p) * 1.0f;
+    a.grad_trunc = p.grad_trunc;
+    a.grad_oor = (float)sqrt(pow((double)p.grad_trunc, 2) * 2);
+    a.grad_adaptive = p.grad_adaptive;
+    a.lam2 = p.lam_g;
+    a.ad_trunc = p.ad_trunc_ad;
+    a.ad_oor_exp = c->ad_oor_exp;
+    const int m = p.cost_method == SM_COST_CENSUS_GRAD ? sm::SM_M_CENSUS_GRAD
+                  : p.cost_method == SM_COST_CENSUS    ? sm::SM_M_CENSUS
+                  : p.cost_method == SM_COST_AD_CENSUS ? sm::SM_M_AD_CENSUS
+                                                       : sm::SM_M_AD;
+    return timed(c, view == 0 ? "cost_volume" : "cost_volume_right", (double)n * c->nvol * 4.0,
+                 [&] { sm::launch_cost(a, m, n, c->st); });
+}
+
+sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w) {
+    const sm_params& p = c->p;
+    sm::CbcaArgs a{};
+    a.vm = c->vm0;
+    a.arms = (const uint32_t*)c->arms;
+    a.H = p.rows;
+    a.W = p.cols;
+    a.D = p.num_disparities;
+    a.lag = cbca_lag(p);
+    a.ring = 2 * a.lag + 2;
+    a.scale = w;
+    const double bytes = (double)n * c->nvol * 8.0;
+    for (int it = 0; it < p.cbca_iterations; it++) {
+        const bool first_h = (it % 2 == 0);  // cbca_core: it0 H then V, it1 V then H (cpp:5608-5621)
+        a.apply_scale = 0;
+        sm_status s = timed(c, first_h ? "cbca_h_scan" : "cbca_v_scan", bytes,
+                            [&] { sm::launch_cbca_pass(a, first_h, false, n, c->st); });
+        if (s) return s;
+        a.apply_scale = (fuse_scale && it == p.cbca_iterations - 1) ? 1 : 0;
+        s = timed(c, first_h ? "cbca_v_norm" : "cbca_h_norm", bytes,
+                  [&] { sm::launch_cbca_pass(a, !first_h, true, n, c->st); });
+        if (s) return s;
+    }
+    return SM_OK;
+}
+
+sm_status run_scale(sm_ctx* c, int n, float w) {
+    return timed(c, "solve_all_scale", (double)n * c->nvol * 8.0,
+                 [&] { sm::launch_scale(c->vm0, (size_t)n * c->nvol, w, c->st); });
+}
+
+sm_status run_optimize(sm_ctx* c, int n) {
+    const sm_params& p = c->p;
+    if (p.optimization == SM_OPT_SGM) {
+        static const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};  // cpp:6207
+        static const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};  // cpp:6208
+        static const char* NAMES[8] = {"sgm_path0", "sgm_path1", "sgm_path2", "sgm_path3",
+                                       "sgm_path4", "sgm_path5", "sgm_path6", "sgm_path7"};
+        sm::SgmArgs a{};
+        a.vm = c->vm0;
+        a.acc = c->acc;
+        a.bgr = c->bgr;
+        a.disp = c->disp;
+        a.H = p.rows;
+        a.W = p.cols;
+        a.D = p.num_disparities;
+        a.p1 = p.sgm_p1;
+        a.p2 = p.sgm_p2;
+        a.cor_thres = p.sgm_cor_dif_thres;
+        a.redu = p.sgm_redu_coeff;
+        a.keep_final = p.keep_final_volume;
+        for (int i = 0; i < p.sgm_paths; i++) {
+            a.rv = RV[i];
+            a.ru = RU[i];
+            int mode = (i == 0 ? sm::SGM_FIRST : 0) | (i == p.sgm_paths - 1 ? sm::SGM_LAST : 0);
+            // algorithmic bytes per element: read C (+ read acc) (+ write acc | write final)
+            double per = 4.0 + ((mode & sm::SGM_FIRST) ? 0 : 4.0) + ((mode & sm::SGM_LAST) ? (p.keep_final_volume ? 4.0 : 0) : 4.0);
+            double bytes = (double)n * c->nvol * per + ((mode & sm::SGM_LAST) ? (double)n * c->npix * 2 : 0);
+            sm_status s = timed(c, (mode & sm::SGM_LAST) ? "sgm_last_wta" : NAMES[i], bytes,
+                                [&] { sm::launch_sgm_path(a, mode, n, c->st); });
+            if (s) return s;
+        }
+    } else {
+        sm_status s = timed(c, "wta", (double)n * c->nvol * 4.0 + (double)n * c->npix * 2,
+                            [&] { sm::launch_wta(c->vm0, c->disp, n, p.rows, p.cols, p.num_disparities, c->st); });
+        if (s) return s;
+    }
+    return SM_OK;
+}
+
+sm_status upload(sm_ctx* c, int n, const uint8_t* lbgr, const uint8_t* rbgr, size_t cstride, const uint8_t* lgray,
+                 const uint8_t* rgray, size_t gstride) {
+    const sm_params& p = c->p;
+    const size_t H = p.rows, W = p.cols;
+    // dst rows: pair-major, view-interleaved; src: n stacked images of H rows each
+    const size_t crow = W * 3;
+    for (int view = 0; view < 2; view++) {
+        const uint8_t* src = view == 0 ? lbgr : rbgr;
+        const uint8_t* gsrc = view == 0 ? lgray : rgray;
+        for (int b = 0; b < n; b++) {
+            uint8_t* dst = c->bgr + ((size_t)b * 2 + view) * c->npix * 3;
+            HIP_TRY(c, hipMemcpy2DAsync(dst, crow, src + (size_t)b * H * cstride, cstride, crow, H, hipMemcpyHostToDevice, c->st));
+            uint8_t* gdst = c->gray + ((size_t)b * 2 + view) * c->npix;
+            HIP_TRY(c, hipMemcpy2DAsync(gdst, W, gsrc + (size_t)b * H * gstride, gstride, W, H, hipMemcpyHostToDevice, c->st));
+        }
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    c->n_loaded = n;
+    c->stage = 1;
+    return SM_OK;
+}
+
+sm_status check(sm_ctx* c) {
+    if (!c) return SM_EINVAL;
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return hip_fail(c, e, "hipSetDevice");
+    return SM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t cols) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->rows = rows;
+    p->cols = cols;
+    p->num_disparities = max_disp + 1;  // h:209
+    p->cost_method = SM_COST_CENSUS_GRAD;
+    p->aggregation = SM_AGG_CBCA;
+    p->optimization = SM_OPT_SGM;
+    p->census_rv = 3;   // cpp:815
+    p->census_ru = 4;
+    p->census_ring = 1; // censusFunc = 3 (h:244)
+    p->lam_cen = 13.0f;
+    p->lam_g = 1.0f;
+    p->grad_trunc = 500.0f;
+    p->grad_adaptive = 1;
+    p->lam_ad = 10.0f;
+    p->lam_cen_adc = 30.0f;
+    p->ad_trunc_adc = 1000.0f;
+    p->ad_trunc_ad = 20.0f;
+    p->arm_l = 17;
+    p->arm_l_out = 34;
+    p->arm_c_thresh = 20;
+    p->arm_c_thresh_out = 6;
+    p->arm_min_l = 1;
+    p->cbca_iterations = 2;
+    p->sgm_paths = 4;
+    p->sgm_p1 = 1.0f;
+    p->sgm_p2 = 3.0f;
+    p->sgm_cor_dif_thres = 15;
+    p->sgm_redu_coeff = 4;
+    p->compute_right_view = 0;
+    p->keep_final_volume = 0;
+    p->batch_capacity = 1;
+}
+
+const char* sm_status_string(sm_status s) {
+    switch (s) {
+        case SM_OK: return "ok";
+        case SM_EINVAL: return "invalid argument";
+        case SM_ENOMEM: return "out of memory";
+        case SM_EHIP: return "HIP runtime error";
+        case SM_ESTATE: return "call out of order";
+    }
+    return "unknown status";
+}
+
+sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
+    if (!out || !p) return SM_EINVAL;
+    *out = nullptr;
+    sm_ctx* c = new (std::nothrow) sm_ctx();
+    if (!c) return SM_ENOMEM;
+    *out = c;  // returned even on failure so sm_last_error works; caller must sm_destroy
+    c->p = *p;
+    c->device = hip_device;
+    std::string why;
+    if (validate(c->p, why) != SM_OK) return fail(c, SM_EINVAL, why);
+    int ndev = 0;
+    HIP_TRY(c, hipGetDeviceCount(&ndev));
+    if (hip_device < 0 || hip_device >= ndev) return fail(c, SM_EINVAL, "hip_device out of range");
+    HIP_TRY(c, hipSetDevice(hip_device));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    c->cap = p->batch_capacity;
+    c->npix = (size_t)p->rows * p->cols;
+    c->nvol = c->npix * (size_t)p->num_disparities;
+    const size_t cap = c->cap;
+    sm_status s;
+    if ((s = dalloc(c, &c->bgr, cap * 2 * c->npix * 3))) return s;
+    if ((s = dalloc(c, &c->gray, cap * 2 * c->npix))) return s;
+    if ((s = dalloc(c, &c->code, cap * 2 * c->npix))) return s;
+    if ((s = dalloc(c, &c->gx, cap * 2 * c->npix))) return s;
+    if ((s = dalloc(c, &c->gy, cap * 2 * c->npix))) return s;
+    if ((s = dalloc(c, &c->arms, cap * 2 * c->npix * 4))) return s;
+    if ((s = dalloc(c, &c->vm0, cap * c->nvol))) return s;
+    if (p->compute_right_view)
+        if ((s = dalloc(c, &c->vm1, cap * c->nvol))) return s;
+    if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
+        if ((s = dalloc(c, &c->acc, cap * c->nvol))) return s;
+    if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
+    build_luts(c);
+    HIP_TRY(c, sm::upload_luts(c->lut_a, c->lut_b, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    return SM_OK;
+}
+
+sm_status sm_destroy(sm_ctx* c) {
+    if (!c) return SM_OK;
+    hipSetDevice(c->device);
+    if (c->st) hipStreamSynchronize(c->st);
+    free_all(c);
+    delete c;
+    return SM_OK;
+}
+
+const char* sm_last_error(const sm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+sm_status sm_set_images(sm_ctx* c, const uint8_t* lbgr, const uint8_t* rbgr, size_t cstride, const uint8_t* lgray,
+                        const uint8_t* rgray, size_t gstride) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!lbgr || !rbgr || !lgray || !rgray) return fail(c, SM_EINVAL, "null image pointer");
+    if (cstride < (size_t)c->p.cols * 3 || gstride < (size_t)c->p.cols) return fail(c, SM_EINVAL, "row stride too small");
+    return upload(c, 1, lbgr, rbgr, cstride, lgray, rgray, gstride);
+}
+
+sm_status sm_cost_calculate(sm_ctx* c) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (c->stage < 1) return fail(c, SM_ESTATE, "sm_cost_calculate before sm_set_images");
+    const int n = c->n_loaded;
+    if ((s = run_prep(c, n))) return s;
+    if ((s = run_cost(c, n, 0))) return s;
+    if (c->p.compute_right_view && (s = run_cost(c, n, 1))) return s;
+    if (c->p.aggregation == SM_AGG_CBCA && (s = run_cbca(c, n, false, 1.0f))) return s;
+    c->stage = 2;
+    return SM_OK;
+}
+
+sm_status sm_solve_all(sm_ctx* c, int32_t py_lev, float reg_lambda) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (c->stage != 2) return fail(c, SM_ESTATE, "sm_solve_all must follow sm_cost_calculate");
+    if (py_lev != 1) return fail(c, SM_EINVAL, "only PY_LEV = 1 is supported (main_.cpp:131)");
+    const float m = 1 + reg_lambda;
+    const float w = (float)(1. / (double)m);  // Mat::inv of the 1x1 regMat (cpp:2164)
+    if ((s = run_scale(c, c->n_loaded, w))) return s;
+    c->stage = 3;
+    return SM_OK;
+}
+
+sm_status sm_disp_optimize(sm_ctx* c, int16_t* disp_out) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (c->stage < 2 || c->stage > 3) return fail(c, SM_ESTATE, "sm_disp_optimize must follow sm_cost_calculate / sm_solve_all");
+    if ((s = run_optimize(c, c->n_loaded))) return s;
+    c->stage = 4;
+    if (disp_out) return sm_download_disp(c, 1, disp_out);
+    return SM_OK;
+}
+
+sm_status sm_get_volume(sm_ctx* c, int32_t view, float* dst) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!dst) return fail(c, SM_EINVAL, "null dst");
+    if (c->stage < 2) return fail(c, SM_ESTATE, "no volume yet");
+    float* src = view == 0 ? c->vm0 : (view == 1 ? c->vm1 : nullptr);
+    if (!src) return fail(c, SM_EINVAL, view == 1 ? "right view not computed (compute_right_view = 0)" : "bad view");
+    if (view == 0 && c->stage == 4 && !c->p.keep_final_volume && c->p.optimization == SM_OPT_SGM)
+        return fail(c, SM_ESTATE, "vm[0] after SGM is only kept with keep_final_volume = 1");
+    HIP_TRY(c, hipMemcpyAsync(dst, src, c->nvol * 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    return SM_OK;
+}
+
+sm_status sm_get_arms(sm_ctx* c, int32_t view, uint16_t* dst) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!dst || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
+    if (c->stage < 2 || !needs_arms(c->p)) return fail(c, SM_ESTATE, "arms not computed");
+    std::vector<uint8_t> tmp(c->npix * 4);
+    HIP_TRY(c, hipMemcpyAsync(tmp.data(), c->arms + (size_t)view * c->npix * 4, c->npix * 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    for (size_t i = 0; i < c->npix * 4; i++) dst[i] = tmp[i];
+    return SM_OK;
+}
+
+sm_status sm_get_census(sm_ctx* c, int32_t view, uint64_t* dst) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!dst || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
+    if (c->stage < 2 || !needs_census(c->p)) return fail(c, SM_ESTATE, "census not computed");
+    HIP_TRY(c, hipMemcpyAsync(dst, c->code + (size_t)view * c->npix, c->npix * 16, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    return SM_OK;
+}
+
+sm_status sm_upload_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr, const uint8_t* lgray,
+                          const uint8_t* rgray) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (n < 1 || n > c->cap) return fail(c, SM_EINVAL, "n must be in [1, batch_capacity]");
+    if (!lbgr || !rbgr || !lgray || !rgray) return fail(c, SM_EINVAL, "null image pointer");
+    return upload(c, n, lbgr, rbgr, (size_t)c->p.cols * 3, lgray, rgray, (size_t)c->p.cols);
+}
+
+sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (c->stage < 1) return fail(c, SM_ESTATE, "sm_run before images were uploaded");
+    if (n < 1 || n > c->n_loaded) return fail(c, SM_EINVAL, "n must be in [1, pairs uploaded]");
+    const float m = 1 + reg_lambda;
+    const float w = (float)(1. / (double)m);
+    if ((s = run_prep(c, n))) return s;
+    if ((s = run_cost(c, n, 0))) return s;
+    if (c->p.compute_right_view && (s = run_cost(c, n, 1))) return s;
+    if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0) {
+        if ((s = run_cbca(c, n, true, w))) return s;   // SolveAll fused into the last pass
+    } else {
+        if ((s = run_scale(c, n, w))) return s;
+    }
+    if ((s = run_optimize(c, n))) return s;
+    c->stage = 4;
+    if (disp_out) return sm_download_disp(c, n, disp_out);
+    return SM_OK;
+}
+
+sm_status sm_download_disp(sm_ctx* c, int32_t n, int16_t* disp_out) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!disp_out || n < 1 || n > c->cap) return fail(c, SM_EINVAL, "bad arguments");
+    if (c->stage != 4) return fail(c, SM_ESTATE, "no disparity map yet");
+    HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    return SM_OK;
+}
+
+sm_status sm_run_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr, const uint8_t* lgray,
+                       const uint8_t* rgray, float reg_lambda, int16_t* disp_out) {
+    sm_status s = sm_upload_batch(c, n, lbgr, rbgr, lgray, rgray);
+    if (s) return s;
+    return sm_run(c, n, reg_lambda, disp_out);
+}
+
+sm_status sm_synchronize(sm_ctx* c) {
+    sm_status s = check(c);
+    if (s) return s;
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    return SM_OK;
+}
+
+void* sm_stream(sm_ctx* c) { return c ? (void*)c->st : nullptr; }
+
+sm_status sm_profile_enable(sm_ctx* c, int32_t on) {
+    if (!c) return SM_EINVAL;
+    c->prof = on != 0;
+    return SM_OK;
+}
+
+static sm_status drain_profile(sm_ctx* c) {
+    if (c->recs.empty()) return SM_OK;
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    for (auto& r : c->recs) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess) {
+            c->kstat[r.kernel].launches++;
+            c->kstat[r.kernel].total_ms += ms;
+        }
+        c->free_events.push_back(r.start);
+        c->free_events.push_back(r.stop);
+    }
+    c->recs.clear();
+    return SM_OK;
+}
+
+sm_status sm_profile_read(sm_ctx* c, int32_t max, char* names, int64_t* launches, double* total_ms,
+                          double* bytes_per_launch, int32_t* count) {
+    sm_status s = check(c);
+    if (s) return s;
+    if ((s = drain_profile(c))) return s;
+    const int k = (int)c->knames.size();
+    if (count) *count = k;
+    for (int i = 0; i < k && i < max; i++) {
+        if (names) {
+            strncpy(names + (size_t)i * 48, c->knames[i].c_str(), 47);
+            names[(size_t)i * 48 + 47] = 0;
+        }
+        if (launches) launches[i] = c->kstat[i].launches;
+        if (total_ms) total_ms[i] = c->kstat[i].total_ms;
+        if (bytes_per_launch) bytes_per_launch[i] = c->kstat[i].bytes;
+    }
+    return SM_OK;
+}
+
+sm_status sm_profile_reset(sm_ctx* c) {
+    sm_status s = check(c);
+    if (s) return s;
+    if ((s = drain_profile(c))) return s;
+    for (auto& st : c->kstat) st = ProfStat();
+    return SM_OK;
+}
+
+float sm_expf_host(float x) { return sm::expf_host(x); }
+
+sm_status sm_expf_device_range(sm_ctx* c, uint32_t first_bits, uint32_t n, float* out) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!out) return fail(c, SM_EINVAL, "null out");
+    float* dbuf = nullptr;
+    if ((s = dalloc(c, &dbuf, n))) return s;
+    sm::launch_expf_range(first_bits, n, dbuf, c->st);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dbuf, (size_t)n * 4, hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    hipFree(dbuf);
+    if (e != hipSuccess) return hip_fail(c, e, "sm_expf_device_range");
+    return SM_OK;
+}
+
+}  // extern "C"

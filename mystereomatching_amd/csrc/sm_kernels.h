@@ -1,0 +1,61 @@
+// sm_kernels.h — internal launch interface between the C-ABI layer and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sm {
+
+enum { SM_M_CENSUS_GRAD = 0, SM_M_CENSUS = 1, SM_M_AD_CENSUS = 2, SM_M_AD = 3 };
+enum { SGM_FIRST = 1, SGM_LAST = 2 };
+
+struct CostArgs {
+    float* vm;                  // [n][H][W][D] destination (view's volume)
+    const ulonglong2* code;     // [n][2][H][W]
+    const float* gx;            // [n][2][H][W]
+    const float* gy;
+    const uint8_t* arms;        // [n][2][H][W][4]
+    const uint8_t* bgr;         // [n][2][H][W][3]
+    int H, W, D, view, nwords;
+    float census_default;       // codeLength * truncRat (h:938)
+    float grad_trunc, grad_oor; // 500, sqrt(2*500^2) (cpp:440)
+    int grad_adaptive;
+    float lam2;                 // lamG
+    float ad_trunc;             // "AD" method truncation
+    float ad_oor_exp;           // ADCensus: expf(-(trunc)/lamAD) for out-of-range pairs
+};
+
+struct CbcaArgs {
+    float* vm;                  // [n][H][W][D], in place
+    const uint32_t* arms;       // [n][2][H][W] packed L|R<<8|U<<16|D<<24
+    int H, W, D;
+    int lag, ring;              // lag = max arm length, ring = 2*lag + 2
+    int apply_scale;
+    float scale;                // SolveAll weight (fused into the last normalising pass)
+};
+
+struct SgmArgs {
+    float* vm;                  // [n][H][W][D] aggregated costs (also the final volume if keep_final)
+    float* acc;                 // [n][H][W][D] running path sum
+    const uint8_t* bgr;         // [n][2][H][W][3] (left colour used for P1/P2 adaptivity)
+    int16_t* disp;              // [n][H][W]
+    int H, W, D, rv, ru;
+    float p1, p2;
+    int cor_thres, redu, keep_final;
+};
+
+hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st);
+void launch_census_grad(const uint8_t* gray, ulonglong2* code, float* gx, float* gy, int n, int H, int W, int rv,
+                        int ru, int ring, hipStream_t st);
+void launch_arms(const uint8_t* bgr, uint8_t* arms, int n, int H, int W, int L, int L_out, int C_D, int C_D_out,
+                 int minL, hipStream_t st);
+void launch_cost(const CostArgs& a, int method, int n, hipStream_t st);
+void launch_cbca_pass(const CbcaArgs& a, bool horiz, bool norm, int n, hipStream_t st);
+void launch_scale(float* vm, size_t n, float w, hipStream_t st);
+void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st);
+void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
+void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);
+float expf_host(float x);
+int sgm_k_for(int D);
+
+}  // namespace sm

@@ -1,0 +1,599 @@
+// sm_kernels.hip — hand-written gfx950 kernels for the census / CBCA / SGM / WTA hot path.
+//
+// Layout in HBM (per pair b, all packed):
+//   bgr   [b][view][H][W][3] u8  gray [b][view][H][W] u8   (view 0 = left, 1 = right)
+//   code  [b][view][H][W] ulonglong2   (census words 0,1; genCensusCode_NC_Sur h:867-934)
+//   gx,gy [b][view][H][W] f32    (calGrad / calGrad_y cpp:271-386)
+//   arms  [b][view][H][W] u8x4   (L,R,U,D; calHorVerDis cpp:2959-3050)
+//   vm    [b][H][W][D] f32       (d innermost, as the reference's CV_32FC(D), cpp:2080)
+//   acc   [b][H][W][D] f32       (SGM path sum in path order, gen_sgm_vm cpp:2031-2056)
+//   disp  [b][H][W] i16          (DP[0], gen_dispFromVm cpp:3928-3967)
+// Every float op below is written in the reference's evaluation order and the file is compiled
+// with -ffp-contract=off, so results are bit-identical to the scalar CPU path.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_device.h"
+#include "sm_kernels.h"
+
+namespace sm {
+
+__constant__ uint64_t c_exp_tab[32] = SM_EXPF_TABLE;
+__constant__ float c_lut_a[1024];   // expf(-x/lam) for integer-valued costs (census / AD)
+__constant__ float c_lut_b[1024];
+
+__device__ inline float dev_expf(float x) { return expf_glibc(x, c_exp_tab); }
+
+// ---------------------------------------------------------------------------------------
+// K0a: census codes + x/y gradients for both views of every pair; one thread per pixel.
+// genCensusCode_NC_Sur (h:867-934): MSB-first bit stream, flush when step > 63.
+// calGrad / calGrad_y single-channel branches (cpp:271-287, 320-350).
+// ---------------------------------------------------------------------------------------
+__global__ void k_census_grad(const uint8_t* __restrict__ gray, ulonglong2* __restrict__ code,
+                              float* __restrict__ gx, float* __restrict__ gy, int H, int W, int rv,
+                              int ru, int ring, int views_per_pair) {
+    const int npix = H * W;
+    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= npix) return;
+    const int view = blockIdx.y;  // 0 left, 1 right
+    const int b = blockIdx.z;
+    const uint8_t* I = gray + ((size_t)b * 2 + view) * npix;
+    const int v = pix / W, u = pix - v * W;
+    const int c = I[pix];
+    uint64_t w[2] = {0, 0};
+    uint64_t cs = 0;
+    int step = 0, dep = 0;
+    for (int dv = -rv; dv <= rv; dv++) {
+        const uint8_t* row = I + (size_t)reflect101(v + dv, H) * W;
+        for (int du = -ru; du <= ru; du++) {
+            if (step > 63) {
+                w[dep & 1] = cs;
+                cs = 0;
+                step = 0;
+                dep++;
+            }
+            cs <<= 1;
+            if (c - (int)row[reflect101(u + du, W)] < 0) cs++;
+            step++;
+        }
+    }
+    if (ring) {
+        const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
+        const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
+        for (int i = 0; i < 8; i++) {
+            int pre = I[(size_t)reflect101(v + dvs[i], H) * W + reflect101(u + dus[i], W)];
+            int aft = I[(size_t)reflect101(v + dvs[i + 1], H) * W + reflect101(u + dus[i + 1], W)];
+            if (step > 63) {
+                w[dep & 1] = cs;
+                cs = 0;
+                step = 0;
+                dep++;
+            }
+            cs <<= 1;
+            if (pre - aft < 0) cs++;
+            step++;
+        }
+    }
+    if (step > 0) w[dep & 1] = cs;
+    const size_t o = ((size_t)b * views_per_pair + view) * npix + pix;
+    code[o] = make_ulonglong2(w[0], w[1]);
+    // gradients (edges: full difference; interior: 0.5 * central difference, exact in f32)
+    const uint8_t* r = I + (size_t)v * W;
+    float g;
+    if (u == 0)
+        g = (float)(r[1] - r[0]);
+    else if (u == W - 1)
+        g = (float)(r[W - 1] - r[W - 2]);
+    else
+        g = 0.5f * (float)(r[u + 1] - r[u - 1]);
+    gx[o] = g;
+    if (v == 0)
+        g = (float)(I[W + u] - I[u]);
+    else if (v == H - 1)
+        g = (float)(I[(size_t)(H - 1) * W + u] - I[(size_t)(H - 2) * W + u]);
+    else
+        g = 0.5f * (float)(I[(size_t)(v + 1) * W + u] - I[(size_t)(v - 1) * W + u]);
+    gy[o] = g;
+}
+
+// ---------------------------------------------------------------------------------------
+// K0b: cross arms (calHorVerDis 7-arg, cpp:2959-3050); one thread per (pixel, direction).
+// ---------------------------------------------------------------------------------------
+__device__ inline bool color_ok(const uint8_t* a, const uint8_t* b, int t) {
+    return abs((int)a[0] - (int)b[0]) <= t && abs((int)a[1] - (int)b[1]) <= t && abs((int)a[2] - (int)b[2]) <= t;
+}
+
+__global__ void k_arms(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ arms, int H, int W, int L,
+                       int L_out, int C_D, int C_D_out, int minL) {
+    const int npix = H * W;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= npix * 4) return;
+    const int pix = t >> 2, direc = t & 3;
+    const int view = blockIdx.y, b = blockIdx.z;
+    const uint8_t* I = bgr + ((size_t)b * 2 + view) * npix * 3;
+    const int v = pix / W, u = pix - v * W;
+    const int du = direc == 0 ? -1 : (direc == 1 ? 1 : 0);
+    const int dv = direc == 2 ? -1 : (direc == 3 ? 1 : 0);
+    const uint8_t* IPtr = I + (size_t)pix * 3;
+    int arm = 1;
+    for (; arm <= L_out; arm++) {
+        int va = v + arm * dv, ua = u + arm * du;
+        if (va < 0 || va >= H || ua < 0 || ua >= W) break;
+        const uint8_t* ap = I + ((size_t)va * W + ua) * 3;
+        const uint8_t* pp = ap - (dv * W + du) * 3;
+        bool nb = color_ok(ap, pp, C_D);
+        bool ip = color_ok(IPtr, ap, arm <= L ? C_D : C_D_out);
+        if (!nb || !ip) break;
+    }
+    int out = 0;
+    if (--arm >= minL)
+        out = arm;
+    else {
+        for (int len = minL; len >= 0; len--)
+            if (u + len * du >= 0 && u + len * du <= W - 1 && v + len * dv >= 0 && v + len * dv <= H - 1) {
+                out = len;
+                break;
+            }
+    }
+    arms[(((size_t)b * 2 + view) * npix + pix) * 4 + direc] = (uint8_t)out;
+}
+
+// ---------------------------------------------------------------------------------------
+// K1: cost volume.  One thread per (pixel, d) element; consecutive threads = consecutive d, so
+// the f32 volume write is fully coalesced.  view 0: pairs (u, u-d); view 1: (u+d, u).
+//   census  gen_cenVM_XOR (h:936-981); grad calgradvm (cpp:388-455);
+//   AD      gen_ad_sd_vm (cpp:2468-2509);   fusion gen_vm_from2vm_exp (cpp:3566-3590).
+// The census term exp(-C/lam) (C integer 0..71) and the AD term exp(-AD/lam) (AD = s/3,
+// s integer 0..765) come from host-built LUTs of libm expf; only the gradient term needs
+// sm::dev_expf.
+// ---------------------------------------------------------------------------------------
+template <int METHOD>
+__global__ void k_cost(const CostArgs a) {
+    const size_t nvol = (size_t)a.H * a.W * a.D;
+    const int b = blockIdx.y;
+    const size_t npix = (size_t)a.H * a.W;
+    float* out = a.vm + (size_t)b * nvol;
+    const int lc = a.view == 1 ? 1 : 0, rc = a.view == 1 ? 0 : 1;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < nvol; e += (size_t)gridDim.x * blockDim.x) {
+        const int pix = (int)(e / a.D);
+        const int d = (int)(e - (size_t)pix * a.D);
+        const int v = pix / a.W, u = pix - v * a.W;
+        const int lp = u + d * lc, rp = u - d * rc;
+        const bool oor = lp >= a.W || rp < 0;
+        const size_t rowb = (size_t)v * a.W;
+        float cen = 0.f;
+        if (METHOD != SM_M_AD) {
+            if (oor)
+                cen = a.census_default;
+            else {
+                const ulonglong2 cl = a.code[((size_t)b * 2 + 0) * npix + rowb + lp];
+                const ulonglong2 cr = a.code[((size_t)b * 2 + 1) * npix + rowb + rp];
+                float cost = 0;
+                cost += (float)__popcll(cl.x ^ cr.x);
+                if (a.nwords > 1) cost += (float)__popcll(cl.y ^ cr.y);
+                cen = fminf(cost, a.census_default);
+            }
+        }
+        float res;
+        if (METHOD == SM_M_CENSUS) {
+            res = cen;
+        } else if (METHOD == SM_M_CENSUS_GRAD) {
+            float g;
+            if (oor)
+                g = a.grad_oor;
+            else {
+                const uint8_t* arm = a.arms + (((size_t)b * 2 + a.view) * npix + pix) * 4;
+                float sH = (float)min(arm[0], arm[1]);
+                float sV = (float)min(arm[2], arm[3]);
+                if (sH == 0) sH = 1;
+                if (sV == 0) sV = 1;
+                const float wa = sH / (sH + sV);
+                const size_t o0 = ((size_t)b * 2 + 0) * npix + rowb + lp;
+                const size_t o1 = ((size_t)b * 2 + 1) * npix + rowb + rp;
+                const float dx = fminf(fabsf(a.gx[o0] - a.gx[o1]), a.grad_trunc);
+                const float dy = fminf(fabsf(a.gy[o0] - a.gy[o1]), a.grad_trunc);
+                if (a.grad_adaptive) {
+                    const float t1 = wa * dx;
+                    const float t2 = (1.0f - wa) * dy;
+                    g = t1 + t2;
+                } else {
+                    g = dx + dy;
+                }
+            }
+            const float e0 = c_lut_a[(int)cen];                 // expf(-C / lamCen)
+            const float e1 = dev_expf(-g / a.lam2);             // expf(-G / lamG)
+            const float t = 2.0f - e0;
+            res = t - e1;
+        } else {  // AD-based: AD = min(s/3, trunc), s = sum_c |L_c - R_c| (integer)
+            int s = 0;
+            if (!oor) {
+                const uint8_t* L = a.bgr + (((size_t)b * 2 + 0) * npix + rowb + lp) * 3;
+                const uint8_t* R = a.bgr + (((size_t)b * 2 + 1) * npix + rowb + rp) * 3;
+                s = abs((int)L[0] - (int)R[0]) + abs((int)L[1] - (int)R[1]) + abs((int)L[2] - (int)R[2]);
+            }
+            if (METHOD == SM_M_AD) {
+                res = oor ? a.ad_trunc : fminf((float)s / 3.0f, a.ad_trunc);
+            } else {  // ADCensus: 2 - exp(-AD/lamAD) - exp(-C/lamC); AD trunc 1000 > 255 never binds
+                const float e0 = oor ? a.ad_oor_exp : c_lut_b[s];
+                const float e1 = c_lut_a[(int)cen];
+                const float t = 2.0f - e0;
+                res = t - e1;
+            }
+        }
+        out[e] = res;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// K2: one CBCA 1-D pass along lines (rows for H, columns for V), in place on vm.
+// Fuses gen1DCumu (cpp:3896-3926) + cal1DCost (h:1643-1715) [+ genfinalVm_cbca (cpp:3969-3992)
+// and the SolveAll scale (cpp:2189-2201) on the second pass of an iteration].
+// One wave = one (line, 64-disparity chunk); the sequential prefix sum S runs along the line in
+// the reference's order; S values live in an LDS ring of 2*lag+2 slots (lag = max arm) so the
+// head/tail differences S[i+head] - S[i-tail-1] are read back without a second HBM pass.
+// Areas (int) are recomputed from the arms instead of being stored: after the first pass of an
+// iteration the area of (p,d) is tail+head+1 of that pass's intersection arms, so the second
+// pass prefix-sums that value (mod 2^16 — the true window area is < 2^16) next to S.
+// Intersection arms (genTrueHorVerArms, cpp:2794-2845): min(A0(v,u), A1(v,u-d)) per arm, 0 if
+// u-d < 0.
+// ---------------------------------------------------------------------------------------
+__device__ inline uint32_t isect_arms(uint32_t a0, const uint32_t* __restrict__ a1row, int u, int d) {
+    if (u - d < 0) return 0u;
+    const uint32_t b = a1row[u - d];
+    uint32_t r = min(a0 & 0xffu, b & 0xffu);
+    r |= min(a0 & 0xff00u, b & 0xff00u);
+    r |= min(a0 & 0xff0000u, b & 0xff0000u);
+    r |= min(a0 & 0xff000000u, b & 0xff000000u);
+    return r;
+}
+
+template <bool HORIZ, bool NORM>
+__global__ __launch_bounds__(64) void k_cbca_pass(const CbcaArgs a) {
+    extern __shared__ float smem[];
+    const int lane = threadIdx.x;
+    const int nchunks = (a.D + 63) >> 6;
+    const int line = blockIdx.x / nchunks, chunk = blockIdx.x - line * nchunks;
+    const int b = blockIdx.y;
+    const int d = chunk * 64 + lane;
+    const bool valid = d < a.D;
+    const int dd = valid ? d : a.D - 1;
+    const int H = a.H, W = a.W, D = a.D;
+    const size_t npix = (size_t)H * W;
+    float* vm = a.vm + (size_t)b * npix * D;
+    const uint32_t* A0 = a.arms + (size_t)b * 2 * npix;
+    const uint32_t* A1 = A0 + npix;
+    const int len = HORIZ ? W : H;
+    const int ring = a.ring, lag = a.lag;
+    float* sring = smem;                                   // [ring][64]
+    uint16_t* aring = (uint16_t*)(smem + ring * 64);       // [ring][64] (NORM only)
+    // arm byte positions: H pass tail=L(0) head=R(1); V pass tail=U(2) head=D(3).
+    const int tsh = HORIZ ? 0 : 16, hsh = HORIZ ? 8 : 24;
+    const int psh_t = HORIZ ? 16 : 0, psh_h = HORIZ ? 24 : 8;  // perpendicular arms for areas
+    float S = 0.f;
+    uint32_t Acc = 0;
+    int wslot = 0;           // ring slot of j
+    for (int j = 0; j < len + lag; j++) {
+        if (j < len) {
+            const int v = HORIZ ? line : j, u = HORIZ ? j : line;
+            const size_t p = (size_t)v * W + u;
+            const float x = vm[p * D + dd];
+            S = (j == 0) ? x : S + x;
+            sring[wslot * 64 + lane] = S;
+            if (NORM) {
+                const uint32_t is = isect_arms(A0[p], A1 + (size_t)v * W, u, d);
+                const uint32_t ain = ((is >> psh_t) & 0xffu) + ((is >> psh_h) & 0xffu) + 1u;
+                Acc = (j == 0) ? ain : Acc + ain;
+                aring[wslot * 64 + lane] = (uint16_t)Acc;
+            }
+        }
+        const int i = j - lag;
+        if (i >= 0) {
+            const int v = HORIZ ? line : i, u = HORIZ ? i : line;
+            const size_t p = (size_t)v * W + u;
+            const uint32_t is = isect_arms(A0[p], A1 + (size_t)v * W, u, d);
+            const int tail = (is >> tsh) & 0xff, head = (is >> hsh) & 0xff;
+            // slot of index k: slot(j) - (j - k), wrapped
+            int hs = wslot - (j - (i + head));
+            if (hs < 0) hs += ring;
+            float out = sring[hs * 64 + lane];
+            uint32_t area = 0;
+            if (NORM) area = aring[hs * 64 + lane];
+            if (i - tail - 1 >= 0) {
+                int ts = wslot - (j - (i - tail - 1));
+                if (ts < 0) ts += ring;
+                out = out - sring[ts * 64 + lane];
+                if (NORM) area = (area - aring[ts * 64 + lane]) & 0xffffu;
+            }
+            if (NORM) {
+                out = out / (float)area;
+                if (a.apply_scale) {
+                    float sum = 0.f;
+                    sum += a.scale * out;
+                    out = sum;
+                }
+            }
+            if (valid) vm[p * D + d] = out;
+        }
+        wslot = (wslot + 1 == ring) ? 0 : wslot + 1;
+    }
+}
+
+// SolveAll with PY_LVL = 1 as a standalone pass (used by the reference-ordered API):
+// vm = 0 + invWgt * vm (cpp:2189-2201).
+__global__ void k_scale(float* __restrict__ vm, size_t n, float w) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        float sum = 0.f;
+        sum += w * vm[i];
+        vm[i] = sum;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// K3: SGM path walker.  One wave walks one scan line of direction r = (rv, ru) (the previous
+// pixel of p is p + r, costScan cpp:1983-2029); lane l holds disparities [l*K, l*K+K).
+// updateCost<float> (h:2206-2280):  m = min_d Lprev;  P1' = P1 - m;
+//   L(d) = C(d) + min(min(Lp(d) - m, Lp(d-1) + P1'), min(Lp(d+1) + P1', P2))
+// FIRST: acc = 0 + L; middle: acc = acc + L; LAST: f = acc + L then WTA (first strict minimum,
+// gen_dispFromVm cpp:3928-3967) and optionally vm = f.  Path order = the reference's sum order.
+// ---------------------------------------------------------------------------------------
+template <int K, int MODE>
+__global__ __launch_bounds__(256) void k_sgm_path(const SgmArgs a) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int H = a.H, W = a.W, D = a.D;
+    const int b = blockIdx.y;
+    const int rv = a.rv, ru = a.ru;
+    // enumerate the lines: start pixels are those whose predecessor p + r lies outside.
+    int nlines, v0, u0;
+    if (rv == 0) {            // horizontal: one line per row
+        nlines = H;
+        if (wave >= nlines) return;
+        v0 = wave;
+        u0 = ru > 0 ? W - 1 : 0;
+    } else if (ru == 0) {     // vertical: one line per column
+        nlines = W;
+        if (wave >= nlines) return;
+        u0 = wave;
+        v0 = rv > 0 ? H - 1 : 0;
+    } else {                  // diagonal: starts on the entry row, then on the entry column
+        nlines = W + H - 1;
+        if (wave >= nlines) return;
+        const int vedge = rv > 0 ? H - 1 : 0, uedge = ru > 0 ? W - 1 : 0;
+        if (wave < W) {
+            v0 = vedge;
+            u0 = wave;
+        } else {
+            const int k = wave - W;           // rows other than vedge
+            v0 = rv > 0 ? k : k + 1;
+            u0 = uedge;
+        }
+    }
+    const int sv = -rv, su = -ru;             // walk direction
+    int steps;
+    {
+        const int nv = rv > 0 ? v0 + 1 : (rv < 0 ? H - v0 : 1 << 30);
+        const int nu = ru > 0 ? u0 + 1 : (ru < 0 ? W - u0 : 1 << 30);
+        steps = min(nv, nu);
+    }
+    const size_t npix = (size_t)H * W;
+    const float* C = a.vm + (size_t)b * npix * D;
+    float* acc = a.acc + (size_t)b * npix * D;
+    float* fin = a.vm + (size_t)b * npix * D;
+    const uint8_t* Ic = a.bgr + (size_t)b * 2 * npix * 3;   // left colour image of pair b
+    const int d0 = lane * K;
+    float Lp[K];
+    int v = v0, u = u0;
+    for (int s = 0; s < steps; s++, v += sv, u += su) {
+        const size_t p = (size_t)v * W + u;
+        const float* cp = C + p * D;
+        float c[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) c[k] = (d0 + k < D) ? cp[d0 + k] : FLT_MAX;
+        float L[K];
+        if (s == 0) {
+#pragma unroll
+            for (int k = 0; k < K; k++) L[k] = c[k];
+        } else {
+            const uint8_t* q0 = Ic + p * 3;
+            const uint8_t* q1 = Ic + ((size_t)(v - sv) * W + (u - su)) * 3;
+            int D1 = max(max(abs((int)q0[0] - (int)q1[0]), abs((int)q0[1] - (int)q1[1])), abs((int)q0[2] - (int)q1[2]));
+            float P1 = a.p1, P2 = a.p2;
+            if (D1 > a.cor_thres) {
+                P1 /= (float)a.redu;
+                P2 /= (float)a.redu;
+            }
+            float lm = Lp[0];
+#pragma unroll
+            for (int k = 1; k < K; k++) lm = fminf(lm, Lp[k]);
+            const float m = wave_min(lm);
+            P1 -= m;
+            const float left_nb = __shfl_up(Lp[K - 1], 1);
+            const float right_nb = __shfl_down(Lp[0], 1);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int d = d0 + k;
+                const float prev = (k == 0) ? left_nb : Lp[k - 1];
+                const float next = (k == K - 1) ? right_nb : Lp[k + 1];
+                const float S1 = Lp[k] - m;
+                const float S2 = d - 1 >= 0 ? prev + P1 : FLT_MAX;
+                const float S3 = d + 1 < D ? next + P1 : FLT_MAX;
+                const float S4 = P2;
+                const float mm = fminf(fminf(S1, S2), fminf(S3, S4));
+                L[k] = (d < D) ? c[k] + mm : FLT_MAX;
+            }
+        }
+        float* ap = acc + p * D;
+        float f[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const float prev = (MODE & SGM_FIRST) ? 0.f : ((d0 + k < D) ? ap[d0 + k] : 0.f);
+            f[k] = (d0 + k < D) ? prev + L[k] : FLT_MAX;   // sum += Lr[num] (cpp:2046-2049)
+        }
+        if (MODE & SGM_LAST) {
+            if (a.keep_final) {
+#pragma unroll
+                for (int k = 0; k < K; k++)
+                    if (d0 + k < D) fin[p * D + d0 + k] = f[k];
+            }
+            // WTA: local first minimum, then wave min value, then lowest index holding it.
+            float bm = f[0];
+            int bi = d0;
+#pragma unroll
+            for (int k = 1; k < K; k++)
+                if (bm > f[k]) {
+                    bm = f[k];
+                    bi = d0 + k;
+                }
+            const float wm = wave_min(bm);
+            const int cand = (bm == wm && d0 < D) ? bi : 0x7fffffff;
+            const int widx = wave_min_i(cand);
+            if (lane == 0) a.disp[(size_t)b * npix + p] = (int16_t)((wm < FLT_MAX) ? widx : -1);
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                if (d0 + k < D) ap[d0 + k] = f[k];
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) Lp[k] = L[k];
+    }
+}
+
+// WTA alone (optimization == "" / aggregation-only runs): one wave per pixel.
+template <int K>
+__global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vm, int16_t* __restrict__ disp, int H, int W, int D) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const size_t npix = (size_t)H * W;
+    const int b = blockIdx.y;
+    if ((size_t)wave >= npix) return;
+    const float* f = vm + ((size_t)b * npix + wave) * D;
+    const int d0 = lane * K;
+    float bm = FLT_MAX;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        if (d0 + k < D && bm > f[d0 + k]) {
+            bm = f[d0 + k];
+            bi = d0 + k;
+        }
+    const float wm = wave_min(bm);
+    const int widx = wave_min_i(bm == wm ? bi : 0x7fffffff);
+    if (lane == 0) disp[(size_t)b * npix + wave] = (int16_t)((wm < FLT_MAX) ? widx : -1);
+}
+
+__global__ void k_expf_range(uint32_t first, uint32_t n, float* __restrict__ out) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        out[i] = dev_expf(__builtin_bit_cast(float, first + i));
+}
+
+// ---------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------
+hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st) {
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut_a), lut_a, sizeof(float) * 1024, 0, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut_b), lut_b, sizeof(float) * 1024, 0, hipMemcpyHostToDevice, st);
+}
+
+void launch_census_grad(const uint8_t* gray, ulonglong2* code, float* gx, float* gy, int n, int H, int W, int rv,
+                        int ru, int ring, hipStream_t st) {
+    dim3 grid((H * W + 255) / 256, 2, n);
+    hipLaunchKernelGGL(k_census_grad, grid, dim3(256), 0, st, gray, code, gx, gy, H, W, rv, ru, ring, 2);
+}
+
+void launch_arms(const uint8_t* bgr, uint8_t* arms, int n, int H, int W, int L, int L_out, int C_D, int C_D_out,
+                 int minL, hipStream_t st) {
+    dim3 grid((H * W * 4 + 255) / 256, 2, n);
+    hipLaunchKernelGGL(k_arms, grid, dim3(256), 0, st, bgr, arms, H, W, L, L_out, C_D, C_D_out, minL);
+}
+
+void launch_cost(const CostArgs& a, int method, int n, hipStream_t st) {
+    const size_t nvol = (size_t)a.H * a.W * a.D;
+    size_t blocks = (nvol + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    dim3 grid((unsigned)blocks, n);
+    switch (method) {
+        case SM_M_CENSUS_GRAD: hipLaunchKernelGGL(k_cost<SM_M_CENSUS_GRAD>, grid, dim3(256), 0, st, a); break;
+        case SM_M_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_CENSUS>, grid, dim3(256), 0, st, a); break;
+        case SM_M_AD_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_AD_CENSUS>, grid, dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL(k_cost<SM_M_AD>, grid, dim3(256), 0, st, a); break;
+    }
+}
+
+void launch_cbca_pass(const CbcaArgs& a, bool horiz, bool norm, int n, hipStream_t st) {
+    const int nchunks = (a.D + 63) / 64;
+    const int lines = horiz ? a.H : a.W;
+    dim3 grid(lines * nchunks, n);
+    const size_t shm = (size_t)a.ring * 64 * (4 + (norm ? 2 : 0));
+    if (horiz && norm) hipLaunchKernelGGL((k_cbca_pass<true, true>), grid, dim3(64), shm, st, a);
+    else if (horiz) hipLaunchKernelGGL((k_cbca_pass<true, false>), grid, dim3(64), shm, st, a);
+    else if (norm) hipLaunchKernelGGL((k_cbca_pass<false, true>), grid, dim3(64), shm, st, a);
+    else hipLaunchKernelGGL((k_cbca_pass<false, false>), grid, dim3(64), shm, st, a);
+}
+
+void launch_scale(float* vm, size_t n, float w, hipStream_t st) {
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, st, vm, n, w);
+}
+
+template <int K>
+static void launch_sgm_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
+    dim3 grid((nlines + 3) / 4, n);
+    switch (mode) {
+        case SGM_FIRST: hipLaunchKernelGGL((k_sgm_path<K, SGM_FIRST>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST: hipLaunchKernelGGL((k_sgm_path<K, SGM_LAST>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm_path<K, SGM_FIRST | SGM_LAST>), grid, dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_sgm_path<K, 0>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
+int sgm_k_for(int D) {
+    const int k = (D + 63) / 64;
+    if (k <= 4) return k;
+    if (k <= 6) return 6;
+    if (k <= 8) return 8;
+    if (k <= 12) return 12;
+    return 16;
+}
+
+void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    switch (sgm_k_for(a.D)) {
+        case 1: launch_sgm_k<1>(a, mode, n, st); break;
+        case 2: launch_sgm_k<2>(a, mode, n, st); break;
+        case 3: launch_sgm_k<3>(a, mode, n, st); break;
+        case 4: launch_sgm_k<4>(a, mode, n, st); break;
+        case 6: launch_sgm_k<6>(a, mode, n, st); break;
+        case 8: launch_sgm_k<8>(a, mode, n, st); break;
+        case 12: launch_sgm_k<12>(a, mode, n, st); break;
+        default: launch_sgm_k<16>(a, mode, n, st); break;
+    }
+}
+
+void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st) {
+    const size_t npix = (size_t)H * W;
+    dim3 grid((unsigned)((npix + 3) / 4), n);
+    switch (sgm_k_for(D)) {
+        case 1: hipLaunchKernelGGL(k_wta<1>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+        case 2: hipLaunchKernelGGL(k_wta<2>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+        case 3: hipLaunchKernelGGL(k_wta<3>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+        case 4: hipLaunchKernelGGL(k_wta<4>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+        case 6: hipLaunchKernelGGL(k_wta<6>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+        case 8: hipLaunchKernelGGL(k_wta<8>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+        case 12: hipLaunchKernelGGL(k_wta<12>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+        default: hipLaunchKernelGGL(k_wta<16>, grid, dim3(256), 0, st, vm, disp, H, W, D); break;
+    }
+}
+
+void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_expf_range, dim3(4096), dim3(256), 0, st, first, n, out);
+}
+
+float expf_host(float x) {
+    static const uint64_t tab[32] = SM_EXPF_TABLE;
+    return expf_glibc(x, tab);
+}
+
+}  // namespace sm

@@ -1,0 +1,258 @@
+"""Host-side mirror of the reference's ``class StereoMatching`` interface (stereoMatching.h:46-2738).
+
+Same names, argument meaning and call order as ``main_.cpp`` uses them (main_.cpp:138-172):
+
+    StereoMatching.costcalculation = "censusGrad"      # static selectors (h:51-53, main:15-17)
+    param = StereoMatching.Parameters(maxDisp, h, w, lamCen, lamG, M, lamc, ts, csvName, disSc)
+    sm = StereoMatching(I1_c, I2_c, I1, I2, DT, all_mask, nonocc_mask, disc_mask, param)
+    sm.costCalculate()                                  # cost + CBCA (cpp:945-1021)
+    SolveAll([sm], 1, 0.3)                              # cpp:2142-2208
+    sm.dispOptimize()                                   # SGM + WTA (cpp:1046-1136)
+    disparity = sm.DP[0]                                # int16 H x W, -1 = invalid
+
+All compute runs in libsm_hip.so on the GPU (no CPU fallback).  Errors are raised as
+``SMError`` (the reference threw cv::Exception / called exit()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _capi
+from .evaluate import cal_err
+
+
+class StereoMatching:
+    # static std::string selectors (h:51-54); process-global in the reference, read at ctor time here
+    costcalculation: str = "censusGrad"
+    aggregation: str = "CBCA"
+    optimization: str = "sgm"
+    object: str = ""
+
+    # compile-time switches the hot path reads (h:57-83)
+    Do_refine = False
+    Do_LRConsis = True
+
+    class Parameters:
+        """StereoMatching::Parameters (h:85-351): the fields the hot path reads."""
+
+        def __init__(self, maxDisp: int, h: int, w: int, lamCen: int = 13, lamG: int = 1, M: int = 2,
+                     lamc: int = 109, ts: int = 10, errCsvName: str = "", disSc: int = 1):
+            self.numDisparities = maxDisp + 1          # h:209
+            self.W_U, self.W_V = 4, 3                  # h:206-207
+            self.errorThreshold = 1                    # h:225
+            self.census_channel = 1                    # h:229
+            self.censusFunc = 3                        # h:244
+            self.gradFuse_adpWgt = True                # h:245
+            self.grad_use2direc = True                 # h:246
+            self.cbca_minArmL = 1                      # h:259
+            self.cbca_iterationNum = 2                 # h:260
+            self.cbca_intersect = True                 # h:262
+            self.cbca_crossL = [17, 23, 34]            # h:263-265
+            self.cbca_crossL_out = [34, 23, 34]        # h:266-268
+            self.cbca_cTresh = [20, 30, 30]            # h:269-271
+            self.cbca_cTresh_out = [6, 0, 0]           # h:272-274
+            self.sgm_scanNum = 4                       # h:236 (the reference hard-codes 4, cpp:6214)
+            self.sgm_P1, self.sgm_P2 = 1.0, 3.0        # ctor override for CBCA (cpp:2089-2091)
+            self.sgm_corDifThres = 15                  # h:239
+            self.sgm_reduCoeffi1 = 4                   # h:240
+            self.lamCen, self.lamG = lamCen, lamG      # h:340-341
+            self.ts, self.disSc = ts, disSc
+            self.errCsvName = errCsvName
+            self.vmTop_Num = M
+            self.vmTop_thres = lamc * 0.01
+            self.rows, self.cols = h, w
+            if disSc != 1:
+                raise ValueError("pyramid levels > 0 (disSc > 1) are not supported; PY_LEV = 1")
+
+        def to_c(self, cost: str, aggregation: str, optimization: str, batch: int = 1,
+                 compute_right_view: bool = False, keep_final_volume: bool = False) -> _capi.sm_params:
+            if self.censusFunc not in (0, 3):
+                raise ValueError("censusFunc must be 0 (plain census) or 3 (census + ring bits)")
+            p = _capi.default_params(self.numDisparities - 1, self.rows, self.cols)
+            p.cost_method = _capi.COST_METHODS[cost]
+            p.aggregation = _capi.AGGREGATIONS[aggregation]
+            p.optimization = _capi.OPTIMIZATIONS[optimization]
+            p.census_ring = 1 if self.censusFunc == 3 else 0
+            p.lam_cen, p.lam_g = float(self.lamCen), float(self.lamG)
+            p.grad_adaptive = int(self.gradFuse_adpWgt)
+            p.arm_l, p.arm_l_out = self.cbca_crossL[0], self.cbca_crossL_out[0]
+            p.arm_c_thresh, p.arm_c_thresh_out = self.cbca_cTresh[0], self.cbca_cTresh_out[0]
+            p.arm_min_l = self.cbca_minArmL
+            p.cbca_iterations = self.cbca_iterationNum
+            p.sgm_paths = self.sgm_scanNum
+            p.sgm_cor_dif_thres = self.sgm_corDifThres
+            p.sgm_redu_coeff = self.sgm_reduCoeffi1
+            p.batch_capacity = batch
+            p.compute_right_view = int(compute_right_view)
+            p.keep_final_volume = int(keep_final_volume)
+            return p
+
+    def __init__(self, I1_c, I2_c, I1_g, I2_g, DT=None, all_mask=None, nonocc_mask=None, disc_mask=None,
+                 param: Optional["StereoMatching.Parameters"] = None, device: int = 0,
+                 keep_final_volume: bool = False):
+        """StereoMatching::StereoMatching (cpp:2058-2110).  Images: BGR u8 HxWx3, gray u8 HxW."""
+        I1_c, I2_c = np.ascontiguousarray(I1_c, np.uint8), np.ascontiguousarray(I2_c, np.uint8)
+        I1_g, I2_g = np.ascontiguousarray(I1_g, np.uint8), np.ascontiguousarray(I2_g, np.uint8)
+        h, w = I1_c.shape[:2]
+        for im, nd in ((I1_c, 3), (I2_c, 3), (I1_g, 2), (I2_g, 2)):
+            if im.ndim != nd or im.shape[:2] != (h, w) or (nd == 3 and im.shape[2] != 3):
+                raise ValueError("images must be HxWx3 (colour) and HxW (gray) of one size")
+        if param is None:
+            raise ValueError("param is required")
+        self.h_, self.w_ = h, w
+        self.d_ = param.numDisparities
+        self.param_ = param
+        self.DT = DT
+        self.I_mask = [nonocc_mask, all_mask, disc_mask]   # cpp:2073-2075
+        self.I_c, self.I_g = [I1_c, I2_c], [I1_g, I2_g]
+        self.DP: List[Optional[np.ndarray]] = [None, None]
+        self._lib = _capi.load()
+        p = param.to_c(self.costcalculation, self.aggregation, self.optimization,
+                       compute_right_view=self.Do_LRConsis and self.Do_refine,
+                       keep_final_volume=keep_final_volume)
+        p.rows, p.cols = h, w
+        ctx = C.c_void_p()
+        st = self._lib.sm_create(C.byref(ctx), C.byref(p), device)
+        self._ctx = ctx
+        _capi.check(self._lib, ctx, st, "sm_create")
+        st = self._lib.sm_set_images(ctx, _capi.ptr(I1_c), _capi.ptr(I2_c), w * 3,
+                                     _capi.ptr(I1_g), _capi.ptr(I2_g), w)
+        _capi.check(self._lib, ctx, st, "sm_set_images")
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.value:
+            self._lib.sm_destroy(ctx)
+            self._ctx = None
+
+    # -- pipeline stages ---------------------------------------------------------------
+    def costCalculate(self):
+        """Cost volume + aggregation (cpp:945-1021)."""
+        _capi.check(self._lib, self._ctx, self._lib.sm_cost_calculate(self._ctx), "costCalculate")
+
+    def dispOptimize(self):
+        """SGM (or WTA only) -> DP[0] (cpp:1046-1136)."""
+        dp = np.empty((self.h_, self.w_), np.int16)
+        _capi.check(self._lib, self._ctx, self._lib.sm_disp_optimize(self._ctx, _capi.ptr(dp)), "dispOptimize")
+        self.DP[0] = dp
+        return dp
+
+    def refine(self):
+        raise NotImplementedError("refine() is off in the reference default (Do_refine = 0, h:70); "
+                                  "it is the next row of SURVEY.md §8f")
+
+    def pipeline(self):
+        """pipeline() (cpp:1950-1981): costCalculate -> dispOptimize (no SolveAll)."""
+        self.costCalculate()
+        return self.dispOptimize()
+
+    # -- state readback ------------------------------------------------------------------
+    @property
+    def vm(self) -> List[np.ndarray]:
+        out = []
+        for view in (0, 1):
+            a = np.empty((self.h_, self.w_, self.d_), np.float32)
+            st = self._lib.sm_get_volume(self._ctx, view, _capi.ptr(a))
+            if st == _capi.SM_OK:
+                out.append(a)
+            elif view == 0:
+                _capi.check(self._lib, self._ctx, st, "vm[0]")
+        return out
+
+    @property
+    def HVL(self) -> List[np.ndarray]:
+        out = []
+        for view in (0, 1):
+            a = np.empty((self.h_, self.w_, 4), np.uint16)
+            _capi.check(self._lib, self._ctx, self._lib.sm_get_arms(self._ctx, view, _capi.ptr(a)), "HVL")
+            out.append(a)
+        return out
+
+    def census_codes(self, view: int) -> np.ndarray:
+        a = np.empty((self.h_, self.w_, 2), np.uint64)
+        _capi.check(self._lib, self._ctx, self._lib.sm_get_census(self._ctx, view, _capi.ptr(a)), "census")
+        return a
+
+    def calErr(self, DP=None, thres: Optional[float] = None):
+        """bad-t ratio / RMS per mask region (h:1748-1825) -> {region: (PBM, RMS)}."""
+        DP = self.DP[0] if DP is None else DP
+        t = self.param_.errorThreshold if thres is None else thres
+        res = {}
+        for name, m in zip(("nonocc", "all", "disc"), self.I_mask):
+            if m is not None and self.DT is not None:
+                res[name] = cal_err(DP, self.DT, m, t)
+        return res
+
+
+def SolveAll(smPyr: Sequence[StereoMatching], PY_LVL: int, REG_LAMBDA: float):
+    """SolveAll (cpp:2142-2208); PY_LVL must be 1 (main_.cpp:131)."""
+    sm = smPyr[0]
+    _capi.check(sm._lib, sm._ctx, sm._lib.sm_solve_all(sm._ctx, int(PY_LVL), float(REG_LAMBDA)), "SolveAll")
+
+
+class StereoBatch:
+    """n independent pairs of one size through the whole main_.cpp sequence in one set of launches."""
+
+    def __init__(self, max_disp: int, rows: int, cols: int, batch: int, device: int = 0, **overrides):
+        self._lib = _capi.load()
+        overrides.setdefault("batch_capacity", batch)
+        p = _capi.default_params(max_disp, rows, cols, **overrides)
+        self.params = p
+        self.shape = (rows, cols, p.num_disparities)
+        ctx = C.c_void_p()
+        st = self._lib.sm_create(C.byref(ctx), C.byref(p), device)
+        self._ctx = ctx
+        _capi.check(self._lib, ctx, st, "sm_create")
+        self.n = 0
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self._lib.sm_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def upload(self, lbgr, rbgr, lgray, rgray):
+        arrs = [np.ascontiguousarray(a, np.uint8) for a in (lbgr, rbgr, lgray, rgray)]
+        n = arrs[0].shape[0]
+        st = self._lib.sm_upload_batch(self._ctx, n, *[_capi.ptr(a) for a in arrs])
+        _capi.check(self._lib, self._ctx, st, "sm_upload_batch")
+        self.n = n
+
+    def run(self, reg_lambda: float = 0.3, download: bool = True) -> Optional[np.ndarray]:
+        out = np.empty((self.n, self.shape[0], self.shape[1]), np.int16) if download else None
+        st = self._lib.sm_run(self._ctx, self.n, float(reg_lambda), _capi.ptr(out) if download else None)
+        _capi.check(self._lib, self._ctx, st, "sm_run")
+        return out
+
+    def download(self) -> np.ndarray:
+        out = np.empty((self.n, self.shape[0], self.shape[1]), np.int16)
+        _capi.check(self._lib, self._ctx, self._lib.sm_download_disp(self._ctx, self.n, _capi.ptr(out)), "download")
+        return out
+
+    def synchronize(self):
+        _capi.check(self._lib, self._ctx, self._lib.sm_synchronize(self._ctx), "sync")
+
+    def profile(self, on: bool = True):
+        self._lib.sm_profile_enable(self._ctx, int(on))
+
+    def profile_reset(self):
+        self._lib.sm_profile_reset(self._ctx)
+
+    def profile_read(self):
+        names = C.create_string_buffer(64 * 48)
+        launches = (C.c_int64 * 64)()
+        total = (C.c_double * 64)()
+        byts = (C.c_double * 64)()
+        cnt = C.c_int32()
+        st = self._lib.sm_profile_read(self._ctx, 64, names, launches, total, byts, C.byref(cnt))
+        _capi.check(self._lib, self._ctx, st, "profile_read")
+        out = {}
+        for i in range(min(cnt.value, 64)):
+            nm = names.raw[i * 48:(i + 1) * 48].split(b"\0", 1)[0].decode()
+            out[nm] = {"launches": launches[i], "total_ms": total[i], "bytes_per_launch": byts[i]}
+        return out

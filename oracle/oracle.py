@@ -1,0 +1,144 @@
+"""ctypes wrapper of the CPU restatement (oracle/sm_oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+PARITY UNPINNED (see sm_oracle.h): the reference cannot be built here and ships no fixtures.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libsm_oracle.so")
+
+COST = {"censusGrad": 0, "Census": 1, "ADCensus": 2, "AD": 3}
+
+
+class Config(C.Structure):
+    """struct smo_config (oracle/sm_oracle.h)."""
+
+    _fields_ = [
+        ("H", C.c_int), ("W", C.c_int), ("D", C.c_int), ("cost_method", C.c_int),
+        ("census_rv", C.c_int), ("census_ru", C.c_int), ("census_ring", C.c_int),
+        ("lam_cen", C.c_float), ("lam_g", C.c_float), ("grad_trunc", C.c_float),
+        ("grad_adaptive", C.c_int), ("lam_ad", C.c_float), ("lam_cen_adc", C.c_float),
+        ("ad_trunc_adc", C.c_float), ("ad_trunc_ad", C.c_float),
+        ("arm_L", C.c_int), ("arm_L_out", C.c_int), ("arm_cT", C.c_int), ("arm_cT_out", C.c_int),
+        ("arm_minL", C.c_int), ("aggregation", C.c_int), ("cbca_iters", C.c_int),
+        ("solve_all", C.c_int), ("reg_lambda", C.c_float), ("optimization", C.c_int),
+        ("sgm_paths", C.c_int), ("sgm_p1", C.c_float), ("sgm_p2", C.c_float),
+        ("sgm_cor_thres", C.c_int), ("sgm_redu", C.c_int),
+    ]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = C.CDLL(LIB)
+        P = C.c_void_p
+        lib.smo_default_config.argtypes = [C.POINTER(Config), C.c_int, C.c_int, C.c_int]
+        lib.smo_run.argtypes = [C.POINTER(Config), P, P, P, P, P, P, P, P, P, P]
+        lib.smo_run.restype = C.c_int
+        lib.smo_census.argtypes = [C.POINTER(Config), P, P]
+        lib.smo_arms.argtypes = [C.POINTER(Config), P, P]
+        lib.smo_cost_volume.argtypes = [C.POINTER(Config), P, P, P, P, C.c_int, P]
+        lib.smo_census_nwords.argtypes = [C.POINTER(Config)]
+        lib.smo_solve_all_weight.argtypes = [C.c_float]
+        lib.smo_solve_all_weight.restype = C.c_float
+        lib.smo_bad_ratio.argtypes = [C.c_int, C.c_int, P, P, P, C.c_float, C.POINTER(C.c_float)]
+        lib.smo_bad_ratio.restype = C.c_float
+        lib.smo_expf_range.argtypes = [C.c_uint32, C.c_uint32, P]
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def config(H, W, max_disp, cost="censusGrad", **kw) -> Config:
+    lib = load()
+    c = Config()
+    lib.smo_default_config(C.byref(c), max_disp, H, W)
+    c.cost_method = COST[cost] if isinstance(cost, str) else cost
+    for k, v in kw.items():
+        if not hasattr(c, k):
+            raise AttributeError(k)
+        setattr(c, k, v)
+    return c
+
+
+def run(pair: dict, cfg: Config, dumps: bool = False, right: bool = False):
+    """Run the pipeline; returns dict(disp, [cost, agg, final], [right], stage_ms)."""
+    lib = load()
+    H, W, D = cfg.H, cfg.W, cfg.D
+    arr = {k: np.ascontiguousarray(pair[k], np.uint8) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+    disp = np.empty((H, W), np.int16)
+    vols = {k: (np.empty((H, W, D), np.float32) if dumps else None) for k in ("cost", "agg", "final")}
+    vr = np.empty((H, W, D), np.float32) if right else None
+    ms = (C.c_double * 6)()
+    st = lib.smo_run(C.byref(cfg), _p(arr["lbgr"]), _p(arr["rbgr"]), _p(arr["lgray"]), _p(arr["rgray"]),
+                     _p(disp), _p(vols["cost"]), _p(vols["agg"]), _p(vols["final"]), _p(vr), ms)
+    if st != 0:
+        raise ValueError("oracle rejected the configuration")
+    out = {"disp": disp, "stage_ms": list(ms)}
+    if dumps:
+        out.update(vols)
+    if right:
+        out["right"] = vr
+    return out
+
+
+def census(gray: np.ndarray, cfg: Config) -> np.ndarray:
+    lib = load()
+    nw = lib.smo_census_nwords(C.byref(cfg))
+    g = np.ascontiguousarray(gray, np.uint8)
+    out = np.zeros((cfg.H, cfg.W, nw), np.uint64)
+    lib.smo_census(C.byref(cfg), _p(g), _p(out))
+    return out
+
+
+def arms(bgr: np.ndarray, cfg: Config) -> np.ndarray:
+    lib = load()
+    b = np.ascontiguousarray(bgr, np.uint8)
+    out = np.zeros((cfg.H, cfg.W, 4), np.uint16)
+    lib.smo_arms(C.byref(cfg), _p(b), _p(out))
+    return out
+
+
+def cost_volume(pair: dict, cfg: Config, view: int = 0) -> np.ndarray:
+    lib = load()
+    arr = {k: np.ascontiguousarray(pair[k], np.uint8) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+    out = np.empty((cfg.H, cfg.W, cfg.D), np.float32)
+    lib.smo_cost_volume(C.byref(cfg), _p(arr["lbgr"]), _p(arr["rbgr"]), _p(arr["lgray"]), _p(arr["rgray"]), view, _p(out))
+    return out
+
+
+def solve_all_weight(reg_lambda: float = 0.3) -> float:
+    return load().smo_solve_all_weight(reg_lambda)
+
+
+def expf_range(first_bits: int, n: int) -> np.ndarray:
+    out = np.empty(n, np.float32)
+    load().smo_expf_range(first_bits, n, _p(out))
+    return out
+
+
+def expf_libm(x: np.ndarray) -> np.ndarray:
+    """Host libm expf on each element (via ctypes to libm; numpy's exp is not libm's)."""
+    libm = C.CDLL("libm.so.6")
+    libm.expf.restype = C.c_float
+    libm.expf.argtypes = [C.c_float]
+    return np.array([libm.expf(float(v)) for v in np.asarray(x, np.float32).ravel()], np.float32)

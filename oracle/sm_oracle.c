@@ -1,0 +1,589 @@
+/*
+ * sm_oracle.c — CPU restatement of the reference hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * PARITY UNPINNED — see sm_oracle.h.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library; the product never does.
+ *
+ * Each function cites the reference lines (relative to /root/reference/) it restates.
+ * "h" = stereoMatching.h, "cpp" = stereoMatching.cpp, "main" = main_.cpp.
+ * Memory-lean but op-order-identical: the h×w×D×5 arm-intersection tensor of
+ * genTrueHorVerArms (cpp:2794-2845) is evaluated on the fly (it is a pure min of two
+ * arm records), and SGM path volumes are accumulated in path order as gen_sgm_vm does.
+ */
+#include "sm_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+/* std::min(a, b) == (b < a) ? b : a */
+static inline float fminstd(float a, float b) { return (b < a) ? b : a; }
+static inline int imin(int a, int b) { return b < a ? b : a; }
+static inline int imax(int a, int b) { return a < b ? b : a; }
+
+void smo_default_config(smo_config* c, int maxdisp, int H, int W) {
+    memset(c, 0, sizeof(*c));
+    c->H = H;
+    c->W = W;
+    c->D = maxdisp + 1;          /* Parameters: numDisparities = maxDisp + 1 (h:209) */
+    c->cost_method = SMO_COST_CENSUS_GRAD;
+    c->census_rv = 3;            /* census_W[0] = {3, 4} (cpp:815) */
+    c->census_ru = 4;
+    c->census_ring = 1;          /* censusFunc = 3 (h:244) */
+    c->lam_cen = 13.0f;          /* lamCen (main:57) */
+    c->lam_g = 1.0f;             /* lamG (main:56) */
+    c->grad_trunc = 500.0f;      /* grad(gradVm, 500) (cpp:34) */
+    c->grad_adaptive = 1;        /* gradFuse_adpWgt (h:245) */
+    c->lam_ad = 10.0f;           /* gen_vm_from2vm_exp(..., 10, 30) (cpp:5270) */
+    c->lam_cen_adc = 30.0f;
+    c->ad_trunc_adc = 1000.0f;   /* asdCal(vm_asd, "AD", imgNum, 1000) (cpp:905) */
+    c->ad_trunc_ad = 20.0f;      /* asdCal(vm, costcalculation, imgNum, 20) (cpp:955) */
+    c->arm_L = 17;               /* cbca_crossL[0] (h:263) */
+    c->arm_L_out = 34;           /* cbca_crossL_out[0] (h:266) */
+    c->arm_cT = 20;              /* cbca_cTresh[0] (h:269) */
+    c->arm_cT_out = 6;           /* cbca_cTresh_out[0] (h:272) */
+    c->arm_minL = 1;             /* cbca_minArmL (h:259) */
+    c->aggregation = 1;          /* "CBCA" (main:16) */
+    c->cbca_iters = 2;           /* cbca_iterationNum (h:260) */
+    c->solve_all = 1;            /* SolveAll(smPsy, 1, 0.3f) (main:157-158) */
+    c->reg_lambda = 0.3f;
+    c->optimization = 1;         /* "sgm" (main:17) */
+    c->sgm_paths = 4;            /* numOfDirec = 4 (cpp:6214) */
+    c->sgm_p1 = 1.0f;            /* updateCost P1 (h:2234) */
+    c->sgm_p2 = 3.0f;            /* updateCost P2 (h:2235) */
+    c->sgm_cor_thres = 15;       /* sgm_corDifThres (h:239) */
+    c->sgm_redu = 4;             /* sgm_reduCoeffi1 (h:240) */
+}
+
+/* OpenCV borderInterpolate, BORDER_REFLECT_101 (used by copyMakeBorder, h:870-871). */
+int smo_reflect101(int p, int len) {
+    if (len == 1) return 0;
+    do {
+        if (p < 0)
+            p = -p;
+        else
+            p = 2 * len - p - 2;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+int smo_census_nwords(const smo_config* c) {
+    /* codeLength (cpp:829-831), varNum = ceil(codeLength / 64.) (cpp:832) */
+    int len = (2 * c->census_rv + 1) * (2 * c->census_ru + 1) + (c->census_ring ? 8 : 0);
+    return (len + 63) / 64;
+}
+
+static int census_length(const smo_config* c) {
+    return (2 * c->census_rv + 1) * (2 * c->census_ru + 1) + (c->census_ring ? 8 : 0);
+}
+
+/* genCensusCode_NC_Sur (h:867-934) on one gray image; censusFunc == 0 (genCensusCode,
+ * h:634-688) is the same loop without the ring bits.  Bits are shifted in MSB-first; a word
+ * is flushed when `step > 63` before the next bit (h:895-901, 916-922). */
+void smo_census(const smo_config* c, const uint8_t* I, uint64_t* codes) {
+    const int H = c->H, W = c->W, RV = c->census_rv, RU = c->census_ru;
+    const int nw = smo_census_nwords(c);
+    static const int dv_sur[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};  /* h:873 */
+    static const int du_sur[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};  /* h:874 */
+    for (int v = 0; v < H; v++) {
+        for (int u = 0; u < W; u++) {
+            uint64_t* censP = codes + ((size_t)v * W + u) * nw;
+            for (int k = 0; k < nw; k++) censP[k] = 0;
+            int center = I[(size_t)v * W + u];
+            uint64_t cs = 0;
+            int step = 0, dep = 0;
+            for (int dv = -RV; dv <= RV; dv++) {
+                int vv = smo_reflect101(v + dv, H);
+                for (int du = -RU; du <= RU; du++) {
+                    int uu = smo_reflect101(u + du, W);
+                    if (step > 63) {
+                        censP[dep] = cs;
+                        cs = 0;
+                        step = 0;
+                        dep++;
+                    }
+                    cs <<= 1;
+                    if (center - (int)I[(size_t)vv * W + uu] < 0) cs++;  /* h:903 */
+                    step++;
+                }
+            }
+            if (c->census_ring) {
+                for (int i = 0; i < 8; i++) {
+                    int pv = smo_reflect101(v + dv_sur[i], H), pu = smo_reflect101(u + du_sur[i], W);
+                    int av = smo_reflect101(v + dv_sur[i + 1], H), au = smo_reflect101(u + du_sur[i + 1], W);
+                    if (step > 63) {
+                        censP[dep] = cs;
+                        cs = 0;
+                        step = 0;
+                        dep++;
+                    }
+                    cs <<= 1;
+                    if ((int)I[(size_t)pv * W + pu] - (int)I[(size_t)av * W + au] < 0) cs++;  /* h:924 */
+                    step++;
+                }
+            }
+            if (step > 0) censP[dep] = cs;
+        }
+    }
+}
+
+/* calGrad, single-channel branch (cpp:271-287): gx = 0.5*(I[u+1]-I[u-1]); edges full diff. */
+void smo_grad_x(int H, int W, const uint8_t* I, float* g) {
+    for (int v = 0; v < H; v++) {
+        const uint8_t* iP = I + (size_t)v * W;
+        float* gP = g + (size_t)v * W;
+        for (int u = 1; u < W - 1; u++) gP[u] = (float)(0.5 * (iP[u + 1] - iP[u - 1]));
+        gP[0] = (float)(iP[1] - iP[0]);
+        gP[W - 1] = (float)(iP[W - 1] - iP[W - 2]);
+    }
+}
+
+/* calGrad_y, single-channel branch (cpp:320-350). */
+void smo_grad_y(int H, int W, const uint8_t* I, float* g) {
+    for (int v = 1; v < H - 1; v++)
+        for (int u = 0; u < W; u++)
+            g[(size_t)v * W + u] = (float)(0.5 * (I[(size_t)(v + 1) * W + u] - I[(size_t)(v - 1) * W + u]));
+    for (int u = 0; u < W; u++) g[u] = (float)(I[(size_t)W + u] - I[u]);
+    for (int u = 0; u < W; u++)
+        g[(size_t)(H - 1) * W + u] = (float)(I[(size_t)(H - 1) * W + u] - I[(size_t)(H - 2) * W + u]);
+}
+
+/* judgeColorDif (cpp:2847-2856) on 3-channel u8 pixels. */
+static inline int color_ok(const uint8_t* a, const uint8_t* b, int thres) {
+    for (int ch = 0; ch < 3; ch++)
+        if (abs((int)a[ch] - (int)b[ch]) > thres) return 0;
+    return 1;
+}
+
+/* calHorVerDis, 7-argument overload (cpp:2959-3050) with the arguments calArms passes
+ * (cpp:5371: L, L_out, cTresh, cTresh_out, minL).  Direction order L, R, U, D (cpp:2978-2998). */
+void smo_arms(const smo_config* c, const uint8_t* I, uint16_t* arms) {
+    const int h = c->H, w = c->W;
+    const int L = c->arm_L, L_out = c->arm_L_out, C_D = c->arm_cT, C_D_out = c->arm_cT_out;
+    const int minL = c->arm_minL;
+    const int dus[4] = {-1, 1, 0, 0}, dvs[4] = {0, 0, -1, 1};
+    for (int direc = 0; direc < 4; direc++) {
+        const int du = dus[direc], dv = dvs[direc];
+        for (int v = 0; v < h; v++) {
+            for (int u = 0; u < w; u++) {
+                const uint8_t* IPtr = I + ((size_t)v * w + u) * 3;
+                int arm = 1;
+                for (; arm <= L_out; arm++) {
+                    int v_arm = v + arm * dv, u_arm = u + arm * du;
+                    if (v_arm < 0 || v_arm >= h || u_arm < 0 || u_arm >= w) break;
+                    const uint8_t* armPtr = I + ((size_t)v_arm * w + u_arm) * 3;
+                    const uint8_t* armPrePtr = I + ((size_t)(v + (arm - 1) * dv) * w + (u + (arm - 1) * du)) * 3;
+                    int nb = color_ok(armPtr, armPrePtr, C_D);
+                    int ip = arm <= L ? color_ok(IPtr, armPtr, C_D) : color_ok(IPtr, armPtr, C_D_out);
+                    if (!nb || !ip) break;
+                }
+                uint16_t out = 0;
+                if (--arm >= minL)
+                    out = (uint16_t)arm;
+                else {
+                    for (int len = minL; len >= 0; len--) {
+                        if (u + len * du >= 0 && u + len * du <= w - 1 && v + len * dv >= 0 && v + len * dv <= h - 1) {
+                            out = (uint16_t)len;
+                            break;
+                        }
+                    }
+                }
+                arms[((size_t)v * w + u) * 4 + direc] = out;
+            }
+        }
+    }
+}
+
+/* gen_cenVM_XOR (h:936-981) for one view: lp = u + d*left, rp = u - d*right. */
+static void census_volume(const smo_config* c, const uint64_t* codeL, const uint64_t* codeR, int view, float* vm) {
+    const int H = c->H, W = c->W, D = c->D, nw = smo_census_nwords(c);
+    const float DEFAULT = (float)census_length(c) * 1.0f;  /* codeLength * truncRat (h:938) */
+    const int lc = view == 1 ? 1 : 0, rc = view == 1 ? 0 : 1;
+    for (int v = 0; v < H; v++)
+        for (int u = 0; u < W; u++) {
+            float* cP = vm + ((size_t)v * W + u) * D;
+            for (int d = 0; d < D; d++) {
+                int lp = u + d * lc, rp = u - d * rc;
+                if (lp >= W || rp < 0)
+                    cP[d] = DEFAULT;
+                else {
+                    float cost = 0;
+                    for (int k = 0; k < nw; k++)
+                        cost += (float)__builtin_popcountll(codeL[((size_t)v * W + lp) * nw + k] ^ codeR[((size_t)v * W + rp) * nw + k]);
+                    cP[d] = fminstd(cost, DEFAULT);
+                }
+            }
+        }
+}
+
+/* calgradvm (cpp:388-455) for one view, arms = HVL[view]. */
+static void grad_volume(const smo_config* c, const float* gx0, const float* gx1, const float* gy0, const float* gy1,
+                        const uint16_t* arms, int view, float* vm) {
+    const int H = c->H, W = c->W, n = c->D;
+    const float Trunc = c->grad_trunc;
+    const int leftCoe = view == 1 ? 1 : 0, rightCoe = view == 1 ? 0 : -1;
+    const float oor = (float)sqrt(pow((double)Trunc, 2) * 2);  /* sqrt(pow(Trunc, 2) * 2) (cpp:440) */
+    for (int v = 0; v < H; v++)
+        for (int u = 0; u < W; u++) {
+            const uint16_t* arm = arms + ((size_t)v * W + u) * 4;
+            float shortestH = 10000, shortestV = 10000;
+            for (int dir = 0; dir < 2; dir++)
+                if (arm[dir] < shortestH) shortestH = arm[dir];
+            for (int dir = 2; dir < 4; dir++)
+                if (arm[dir] < shortestV) shortestV = arm[dir];
+            if (shortestH == 0) shortestH++;
+            if (shortestV == 0) shortestV++;
+            float a = shortestH / (shortestH + shortestV);
+            float* vP = vm + ((size_t)v * W + u) * n;
+            const float* g0 = gx0 + (size_t)v * W;
+            const float* g1 = gx1 + (size_t)v * W;
+            const float* y0 = gy0 + (size_t)v * W;
+            const float* y1 = gy1 + (size_t)v * W;
+            for (int d = 0; d < n; d++) {
+                int u0 = u + leftCoe * d, u1 = u + rightCoe * d;
+                if (u0 >= W || u1 < 0)
+                    vP[d] = oor;
+                else if (c->grad_adaptive) {
+                    float t1 = a * fminstd(fabsf(g0[u0] - g1[u1]), Trunc);
+                    float t2 = (1 - a) * fminstd(fabsf(y0[u0] - y1[u1]), Trunc);
+                    vP[d] = t1 + t2;
+                } else {
+                    vP[d] = fminstd(fabsf(g0[u0] - g1[u1]), Trunc) + fminstd(fabsf(y0[u0] - y1[u1]), Trunc);
+                }
+            }
+        }
+}
+
+/* gen_ad_sd_vm, AD branch with 3 colour channels (cpp:2468-2509). */
+static void ad_volume(const smo_config* c, const uint8_t* I0, const uint8_t* I1, int view, float trunc, float* vm) {
+    const int H = c->H, W = c->W, n = c->D;
+    const int lc = view == 1 ? 1 : 0, rc = view == 1 ? 0 : -1;
+    for (int v = 0; v < H; v++)
+        for (int u = 0; u < W; u++) {
+            float* vP = vm + ((size_t)v * W + u) * n;
+            for (int d = 0; d < n; d++) {
+                int uL = u + d * lc, uR = u + d * rc;
+                if (uL >= W || uR < 0)
+                    vP[d] = trunc;
+                else {
+                    const uint8_t* l = I0 + ((size_t)v * W + uL) * 3;
+                    const uint8_t* r = I1 + ((size_t)v * W + uR) * 3;
+                    float sum = 0;
+                    for (int ch = 0; ch < 3; ch++) sum = (float)((double)sum + pow(fabsf((float)l[ch] - (float)r[ch]), 1));
+                    vP[d] = fminstd(sum / 3, trunc);
+                }
+            }
+        }
+}
+
+/* gen_vm_from2vm_exp (cpp:3566-3590): out = 2 - exp(-vm0/ARU0) - exp(-vm1/ARU1). */
+static void fuse_exp(size_t n, const float* vm0, const float* vm1, float aru0, float aru1, float* out) {
+    for (size_t i = 0; i < n; i++) out[i] = 2 - expf(-vm0[i] / aru0) - expf(-vm1[i] / aru1);
+}
+
+void smo_cost_volume(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
+                     const uint8_t* grayL, const uint8_t* grayR, int view, float* vm) {
+    const int H = c->H, W = c->W;
+    const size_t npix = (size_t)H * W, nvol = npix * c->D;
+    if (c->cost_method == SMO_COST_AD) {           /* asdCal "AD" (cpp:954-955) */
+        ad_volume(c, bgrL, bgrR, view, c->ad_trunc_ad, vm);
+        return;
+    }
+    const int nw = smo_census_nwords(c);
+    uint64_t* cL = (uint64_t*)malloc(npix * nw * 8);
+    uint64_t* cR = (uint64_t*)malloc(npix * nw * 8);
+    smo_census(c, grayL, cL);                      /* censusCal (cpp:856-872) */
+    smo_census(c, grayR, cR);
+    if (c->cost_method == SMO_COST_CENSUS) {       /* costcalculation "Census" (cpp:975-976) */
+        census_volume(c, cL, cR, view, vm);
+    } else if (c->cost_method == SMO_COST_AD_CENSUS) {  /* ADCensusCal (cpp:894-915) */
+        float* ad = (float*)malloc(nvol * 4);
+        float* cen = (float*)malloc(nvol * 4);
+        ad_volume(c, bgrL, bgrR, view, c->ad_trunc_adc, ad);
+        census_volume(c, cL, cR, view, cen);
+        fuse_exp(nvol, ad, cen, c->lam_ad, c->lam_cen_adc, vm);   /* adCensus (cpp:5270) */
+        free(ad);
+        free(cen);
+    } else {                                       /* censusGrad (cpp:25-48) */
+        float* gx0 = (float*)malloc(npix * 4);
+        float* gx1 = (float*)malloc(npix * 4);
+        float* gy0 = (float*)malloc(npix * 4);
+        float* gy1 = (float*)malloc(npix * 4);
+        uint16_t* arms = (uint16_t*)malloc(npix * 8);
+        smo_grad_x(H, W, grayL, gx0);
+        smo_grad_x(H, W, grayR, gx1);
+        smo_grad_y(H, W, grayL, gy0);
+        smo_grad_y(H, W, grayR, gy1);
+        smo_arms(c, view == 1 ? bgrR : bgrL, arms);  /* HVL[num] of that view (cpp:403) */
+        float* gv = (float*)malloc(nvol * 4);
+        float* cv = (float*)malloc(nvol * 4);
+        grad_volume(c, gx0, gx1, gy0, gy1, arms, view, gv);
+        census_volume(c, cL, cR, view, cv);
+        fuse_exp(nvol, cv, gv, c->lam_cen, c->lam_g, vm);        /* cpp:40-43 */
+        free(gv);
+        free(cv);
+        free(gx0);
+        free(gx1);
+        free(gy0);
+        free(gy1);
+        free(arms);
+    }
+    free(cL);
+    free(cR);
+}
+
+/* HVL_INTERSECTION[0] element k at (v,u,d) — genTrueHorVerArms (cpp:2794-2845), left view:
+ * min(HVL[0](v,u)[k], HVL[1](v,u-d)[k]); zero (memset, cpp:2799-2800) once u-d < 0. */
+static inline int isect(const uint16_t* aL, const uint16_t* aR, int W, int v, int u, int d, int k) {
+    if (u - d < 0) return 0;
+    int a = aL[((size_t)v * W + u) * 4 + k], b = aR[((size_t)v * W + (u - d)) * 4 + k];
+    return imin(a, b);
+}
+
+/* gen1DCumu (cpp:3896-3926) with cbca_intersect = 1. */
+static void cumu(const smo_config* c, float* vm, int32_t* area, int dv, int du) {
+    const int H = c->H, W = c->W, n = c->D;
+    for (int v = 0; v < H; v++)
+        for (int u = 0; u < W; u++) {
+            int vPre = v + dv, uPre = u + du;
+            int inner = (vPre >= 0 && vPre < H && uPre >= 0 && uPre < W);
+            if (!inner) continue;
+            float* p = vm + ((size_t)v * W + u) * n;
+            const float* q = vm + ((size_t)vPre * W + uPre) * n;
+            int32_t* a = area + ((size_t)v * W + u) * n;
+            const int32_t* b = area + ((size_t)vPre * W + uPre) * n;
+            for (int d = 0; d < n; d++) {
+                p[d] += q[d];
+                a[d] += b[d];
+            }
+        }
+}
+
+/* cal1DCost (h:1643-1715) with cbca_intersect = 1; writes temps then copies back. */
+static void cost1d(const smo_config* c, float* vm, int32_t* area, float* vmT, int32_t* areaT,
+                   const uint16_t* aL, const uint16_t* aR, int dv, int du, int direc) {
+    const int H = c->H, W = c->W, n = c->D;
+    const int head_num = direc * 2 + 1, tail_num = direc * 2;
+    for (int v = 0; v < H; v++)
+        for (int u = 0; u < W; u++) {
+            float* vT = vmT + ((size_t)v * W + u) * n;
+            int32_t* aT = areaT + ((size_t)v * W + u) * n;
+            for (int d = 0; d < n; d++) {
+                int tailL = isect(aL, aR, W, v, u, d, tail_num), headL = isect(aL, aR, W, v, u, d, head_num);
+                int tail_u = u + du * tailL, tail_v = v + dv * tailL;
+                int head_u = u - du * headL, head_v = v - dv * headL;
+                int pre_tailU = tail_u + du, pre_tailV = tail_v + dv;
+                int inner = (pre_tailU >= 0 && pre_tailU < W && pre_tailV >= 0 && pre_tailV < H);
+                size_t hi = ((size_t)head_v * W + head_u) * n + d;
+                size_t ti = ((size_t)pre_tailV * W + pre_tailU) * n + d;
+                if (inner) {
+                    aT[d] = area[hi] - area[ti];
+                    vT[d] = vm[hi] - vm[ti];
+                } else {
+                    aT[d] = area[hi];
+                    vT[d] = vm[hi];
+                }
+            }
+        }
+    memcpy(vm, vmT, (size_t)H * W * n * 4);
+    memcpy(area, areaT, (size_t)H * W * n * 4);
+}
+
+/* cbca_core (cpp:5585-5666) for LOR = 0 only (imgNum = Do_refine && Do_LRConsis ? 2 : 1). */
+void smo_cbca(const smo_config* c, float* vm, const uint16_t* aL, const uint16_t* aR) {
+    const size_t nvol = (size_t)c->H * c->W * c->D;
+    const int du[2] = {-1, 0}, dv[2] = {0, -1};
+    int32_t* area = (int32_t*)malloc(nvol * 4);
+    int32_t* areaT = (int32_t*)malloc(nvol * 4);
+    float* vmT = (float*)malloc(nvol * 4);
+    for (int it = 0; it < c->cbca_iters; it++) {
+        for (size_t i = 0; i < nvol; i++) area[i] = 1;  /* Scalar::all(1) (cpp:5604) */
+        if (it % 2 == 0) {
+            cumu(c, vm, area, dv[0], du[0]);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[0], du[0], 0);
+            cumu(c, vm, area, dv[1], du[1]);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[1], du[1], 1);
+        } else {
+            cumu(c, vm, area, dv[1], du[1]);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[1], du[1], 1);
+            cumu(c, vm, area, dv[0], du[0]);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[0], du[0], 0);
+        }
+        for (size_t i = 0; i < nvol; i++) vm[i] /= area[i];  /* genfinalVm_cbca (cpp:3969-3992) */
+    }
+    free(area);
+    free(areaT);
+    free(vmT);
+}
+
+/* SolveAll (cpp:2142-2208) with PY_LVL = 1: regMat = [1 + REG_LAMBDA]; OpenCV's 1×1 float
+ * invert computes (float)(1. / (double)m). */
+float smo_solve_all_weight(float reg_lambda) {
+    float m = 1 + reg_lambda;
+    return (float)(1. / (double)m);
+}
+
+void smo_solve_all(const smo_config* c, float* vm) {
+    const size_t nvol = (size_t)c->H * c->W * c->D;
+    const float w = smo_solve_all_weight(c->reg_lambda);
+    for (size_t i = 0; i < nvol; i++) {
+        float sum = 0;
+        sum += w * vm[i];
+        vm[i] = sum;
+    }
+}
+
+/* updateCost<float> (h:2206-2280) for one pixel, leftFirst = true (D2 is computed there
+ * but never used, so it is omitted). */
+static void update_cost(const smo_config* c, float* Lr, const float* vm, const uint8_t* Ic, int v, int u,
+                        int rv, int ru, int preIsInner) {
+    const int W = c->W, n = c->D;
+    const float* vmPtr = vm + ((size_t)v * W + u) * n;
+    float* out = Lr + ((size_t)v * W + u) * n;
+    if (!preIsInner) {
+        for (int d = 0; d < n; d++) out[d] = vmPtr[d];
+        return;
+    }
+    int D1 = 0;
+    for (int ch = 0; ch < 3; ch++)
+        D1 = imax(D1, abs((int)Ic[((size_t)v * W + u) * 3 + ch] - (int)Ic[((size_t)(v + rv) * W + (u + ru)) * 3 + ch]));
+    const float* fore = Lr + ((size_t)(v + rv) * W + (u + ru)) * n;
+    float minC = FLT_MAX;
+    for (int d = 0; d < n; d++) minC = fminstd(fore[d], minC);
+    for (int d = 0; d < n; d++) {
+        float P1 = c->sgm_p1, P2 = c->sgm_p2;
+        if (D1 > c->sgm_cor_thres) {
+            P1 /= c->sgm_redu;
+            P2 /= c->sgm_redu;
+        }
+        P1 -= minC;
+        float cost = vmPtr[d];
+        float S1 = fore[d] - minC;
+        float S2 = d - 1 >= 0 ? fore[d - 1] + P1 : FLT_MAX;
+        float S3 = d + 1 < n ? fore[d + 1] + P1 : FLT_MAX;
+        float S4 = P2;
+        out[d] = cost + fminstd(fminstd(S1, S2), fminstd(S3, S4));  /* min4 (h:2200-2203) */
+    }
+}
+
+/* sgm (cpp:6204-6224) + costScan (cpp:1983-2029) + gen_sgm_vm (cpp:2031-2056). */
+void smo_sgm(const smo_config* c, float* vm, const uint8_t* Ic) {
+    static const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};  /* cpp:6207 */
+    static const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};  /* cpp:6208 */
+    const int h = c->H, w = c->W;
+    const size_t nvol = (size_t)h * w * c->D;
+    float* Lr = (float*)malloc(nvol * 4);
+    float* acc = (float*)malloc(nvol * 4);
+    for (size_t i = 0; i < nvol; i++) acc[i] = 0;
+    for (int i = 0; i < c->sgm_paths; i++) {
+        int rv = RV[i], ru = RU[i];
+        int v0 = 0, v1 = h, u0 = 0, u1 = w, dv = +1, du = +1;
+        if ((rv > 0) || (rv == 0 && ru > 0)) {
+            v0 = h - 1; v1 = -1; u0 = w - 1; u1 = -1; dv = -1; du = -1;
+        }
+        for (int v = v0; v != v1; v += dv)
+            for (int u = u0; u != u1; u += du) {
+                int pre = !(v + rv > h - 1 || v + rv < 0 || u + ru > w - 1 || u + ru < 0);
+                update_cost(c, Lr, vm, Ic, v, u, rv, ru, pre);
+            }
+        for (size_t k = 0; k < nvol; k++) acc[k] += Lr[k];  /* sum += Lr[num] in path order */
+    }
+    memcpy(vm, acc, nvol * 4);
+    free(Lr);
+    free(acc);
+}
+
+/* gen_dispFromVm (cpp:3928-3967), ChooseSmall = true. */
+void smo_wta(const smo_config* c, const float* vm, int16_t* disp) {
+    const int n = c->D;
+    for (size_t p = 0; p < (size_t)c->H * c->W; p++) {
+        float minC = FLT_MAX;
+        int d_best = -1;
+        const float* vP = vm + p * n;
+        for (int d = 0; d < n; d++)
+            if (minC > vP[d]) {
+                minC = vP[d];
+                d_best = d;
+            }
+        disp[p] = (int16_t)d_best;
+    }
+}
+
+int smo_run(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
+            const uint8_t* grayL, const uint8_t* grayR, int16_t* disp,
+            float* vol_cost, float* vol_agg, float* vol_final, float* vol_right, double* stage_ms) {
+    if (c->H < 2 || c->W < 2 || c->D < 1) return -1;
+    const size_t npix = (size_t)c->H * c->W, nvol = npix * c->D;
+    double t0 = now_ms(), t;
+    float* vm = (float*)malloc(nvol * 4);
+    if (!vm) return -1;
+    double ms[6] = {0, 0, 0, 0, 0, 0};
+    smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 0, vm);
+    if (vol_right) smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 1, vol_right);
+    if (vol_cost) memcpy(vol_cost, vm, nvol * 4);
+    t = now_ms(); ms[0] = t - t0; t0 = t;
+    if (c->aggregation == 1) {
+        uint16_t* aL = (uint16_t*)malloc(npix * 8);
+        uint16_t* aR = (uint16_t*)malloc(npix * 8);
+        smo_arms(c, bgrL, aL);                   /* calArms for both images (cpp:5358-5385) */
+        smo_arms(c, bgrR, aR);
+        smo_cbca(c, vm, aL, aR);
+        free(aL);
+        free(aR);
+    }
+    if (vol_agg) memcpy(vol_agg, vm, nvol * 4);
+    t = now_ms(); ms[1] = t - t0; t0 = t;
+    if (c->solve_all) smo_solve_all(c, vm);
+    t = now_ms(); ms[2] = t - t0; t0 = t;
+    if (c->optimization == 1) smo_sgm(c, vm, bgrL);
+    if (vol_final) memcpy(vol_final, vm, nvol * 4);
+    t = now_ms(); ms[3] = t - t0; t0 = t;
+    smo_wta(c, vm, disp);
+    t = now_ms(); ms[4] = t - t0;
+    ms[5] = ms[0] + ms[1] + ms[2] + ms[3] + ms[4];
+    if (stage_ms) memcpy(stage_ms, ms, sizeof(ms));
+    free(vm);
+    return 0;
+}
+
+/* calErr (h:1748-1825): bad pixel ratio over mask == 255 with threshold `thres`. */
+float smo_bad_ratio(int H, int W, const int16_t* DP, const float* DT, const uint8_t* mask, float thres, float* rms_out) {
+    int sumNum = 0, errorNumer = 0;
+    float errorValueSum = 0;
+    for (size_t p = 0; p < (size_t)H * W; p++) {
+        if (mask[p] != 255) continue;
+        sumNum++;
+        if (DP[p] >= 0) {
+            float dif = fabsf(DT[p] - DP[p]);
+            errorValueSum = (float)(errorValueSum + pow(dif, 2));
+            if (dif > thres) errorNumer++;
+        } else {
+            errorNumer++;
+            errorValueSum += 2;
+        }
+    }
+    if (sumNum == 0) {
+        if (rms_out) *rms_out = 0;
+        return 0;
+    }
+    if (rms_out) *rms_out = sqrtf(errorValueSum / sumNum);
+    return (float)errorNumer / sumNum;
+}
+
+/* libm expf over the float bit patterns [first, first + n) — the checker for the device expf. */
+void smo_expf_range(uint32_t first, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t b = first + i;
+        float x;
+        memcpy(&x, &b, 4);
+        out[i] = expf(x);
+    }
+}

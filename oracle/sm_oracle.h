@@ -1,0 +1,92 @@
+/*
+ * sm_oracle.h — CPU restatement of the reference's census/CBCA/SGM/WTA hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (mystereomatching_amd/, include/)
+ * links, loads or calls this code; only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg do, and only as the checker / the CPU baseline.
+ *
+ * PARITY UNPINNED: the reference (xinge456/myStereoMatching, mounted at /root/reference)
+ * cannot be built here (needs OpenCV + opencv_contrib/ximgproc + a missing util.h + MSVC-only
+ * constructs) and it ships no tests, fixtures or golden vectors.
+ * This restatement follows the reference source line by line (citations per function in
+ * sm_oracle.c) and is cross-checked against an independent pure-Python restatement
+ * (tests/pyref.py) on small inputs; it is not pinned to outputs of the reference binary.
+ *
+ * Every function is single-threaded, compiled -O2 -ffp-contract=off -fno-fast-math so that
+ * each float operation rounds exactly as the reference's scalar C++ does.
+ */
+#ifndef SM_ORACLE_H
+#define SM_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { SMO_COST_CENSUS_GRAD = 0, SMO_COST_CENSUS = 1, SMO_COST_AD_CENSUS = 2, SMO_COST_AD = 3 };
+
+typedef struct smo_config {
+    int H, W, D;                 /* D = numDisparities = maxdisp + 1 (h:209) */
+    int cost_method;             /* SMO_COST_*; default censusGrad (main:15) */
+    int census_rv, census_ru;    /* census window radii {3,4} (cpp:815) */
+    int census_ring;             /* censusFunc == 3: 8 ring bits (h:244, h:910-928) */
+    float lam_cen, lam_g;        /* 13, 1 (main:56-57, cpp:38-39) */
+    float grad_trunc;            /* 500 (cpp:34) */
+    int grad_adaptive;           /* gradFuse_adpWgt = 1 (h:245) */
+    float lam_ad, lam_cen_adc;   /* ADCensus fusion 10, 30 (cpp:5270) */
+    float ad_trunc_adc;          /* ADCensus AD trunc 1000 (cpp:905) */
+    float ad_trunc_ad;           /* "AD" cost trunc 20 (cpp:955) */
+    int arm_L, arm_L_out;        /* cbca_crossL[0]=17, cbca_crossL_out[0]=34 (h:263,266) */
+    int arm_cT, arm_cT_out;      /* cbca_cTresh[0]=20, cbca_cTresh_out[0]=6 (h:269,272) */
+    int arm_minL;                /* cbca_minArmL = 1 (h:259) */
+    int aggregation;             /* 0 none, 1 CBCA (main:16) */
+    int cbca_iters;              /* cbca_iterationNum = 2 (h:260) */
+    int solve_all;               /* apply SolveAll(PY_LEV=1) (main:158) */
+    float reg_lambda;            /* REG_LAMBDA = 0.3 (main:157) */
+    int optimization;            /* 0 WTA only, 1 SGM (main:17) */
+    int sgm_paths;               /* 4 (cpp:6214); 8 = full direction table (cpp:6207-6208) */
+    float sgm_p1, sgm_p2;        /* 1.0, 3.0 hard-coded in updateCost (h:2234-2235) */
+    int sgm_cor_thres;           /* sgm_corDifThres = 15 (h:239) */
+    int sgm_redu;                /* sgm_reduCoeffi1 = 4 (h:240) */
+} smo_config;
+
+void smo_default_config(smo_config* c, int maxdisp, int H, int W);
+
+/* OpenCV borderInterpolate(BORDER_REFLECT_101). */
+int smo_reflect101(int p, int len);
+
+int smo_census_nwords(const smo_config* c);
+void smo_census(const smo_config* c, const uint8_t* gray, uint64_t* codes);
+void smo_grad_x(int H, int W, const uint8_t* gray, float* g);
+void smo_grad_y(int H, int W, const uint8_t* gray, float* g);
+void smo_arms(const smo_config* c, const uint8_t* bgr, uint16_t* arms /* H*W*4 */);
+
+/* Cost volume for one view (0 = left reference, 1 = right), H*W*D floats. */
+void smo_cost_volume(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
+                     const uint8_t* grayL, const uint8_t* grayR, int view, float* vm);
+void smo_cbca(const smo_config* c, float* vm, const uint16_t* armsL, const uint16_t* armsR);
+float smo_solve_all_weight(float reg_lambda);
+void smo_solve_all(const smo_config* c, float* vm);
+void smo_sgm(const smo_config* c, float* vm, const uint8_t* bgrL);
+void smo_wta(const smo_config* c, const float* vm, int16_t* disp);
+
+/* Whole default pipeline for one pair (main:138-163 call order).  Optional dumps may be NULL:
+ * vol_cost = vm[0] after the cost stage, vol_agg = after CBCA, vol_final = after SGM sum,
+ * vol_right = vm[1] cost volume.  stage_ms[6] (optional): cost, cbca, solveall, sgm, wta, total.
+ * Returns 0 on success, -1 on bad config / allocation failure. */
+int smo_run(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
+            const uint8_t* grayL, const uint8_t* grayR, int16_t* disp,
+            float* vol_cost, float* vol_agg, float* vol_final, float* vol_right,
+            double* stage_ms);
+
+/* bad-t evaluator (h:1748-1825): returns PBM; rms_out optional. */
+float smo_bad_ratio(int H, int W, const int16_t* disp, const float* gt, const uint8_t* mask,
+                    float thres, float* rms_out);
+
+/* libm expf over float bit patterns [first, first+n). */
+void smo_expf_range(uint32_t first, uint32_t n, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,302 @@
+"""Independent numpy restatement of the reference hot path, for SMALL inputs only.
+
+Written directly from the reference text (stereoMatching.cpp / .h), separately from the C
+oracle, and used to cross-check it (tests/test_oracle.py).  float32 numpy ufuncs round every
+operation individually (no FMA contraction), and np.add.accumulate is a strictly sequential
+float32 prefix sum, so this reproduces the reference's arithmetic.  expf is the host libm's.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+f32 = np.float32
+_libm = ctypes.CDLL("libm.so.6")
+_libm.expf.restype = ctypes.c_float
+_libm.expf.argtypes = [ctypes.c_float]
+_expf_vec = np.frompyfunc(lambda x: _libm.expf(float(x)), 1, 1)
+
+
+def expf(a):
+    return np.asarray(_expf_vec(np.asarray(a, f32)), dtype=f32)
+
+
+def reflect101(p, n):
+    if n == 1:
+        return 0
+    while p < 0 or p >= n:
+        p = -p if p < 0 else 2 * n - p - 2
+    return p
+
+
+def census(gray, rv=3, ru=4, ring=True):
+    """genCensusCode_NC_Sur (h:867-934) -> list of per-pixel bit strings (as python ints + length)."""
+    H, W = gray.shape
+    bits = np.zeros((H, W), dtype=object)
+    ring_v = [-1, -1, -1, 0, 1, 1, 1, 0, -1]
+    ring_u = [-1, 0, 1, 1, 1, 0, -1, -1, -1]
+    for v in range(H):
+        for u in range(W):
+            c = int(gray[v, u])
+            s = []
+            for dv in range(-rv, rv + 1):
+                for du in range(-ru, ru + 1):
+                    s.append(1 if c < int(gray[reflect101(v + dv, H), reflect101(u + du, W)]) else 0)
+            if ring:
+                for i in range(8):
+                    a = int(gray[reflect101(v + ring_v[i], H), reflect101(u + ring_u[i], W)])
+                    b = int(gray[reflect101(v + ring_v[i + 1], H), reflect101(u + ring_u[i + 1], W)])
+                    s.append(1 if a < b else 0)
+            bits[v, u] = s
+    return bits
+
+
+def census_words(bits):
+    """Pack a bit list the way h:886-930 does: 64-bit words, MSB first, last word right-aligned."""
+    H, W = bits.shape
+    L = len(bits[0, 0])
+    nw = (L + 63) // 64
+    out = np.zeros((H, W, nw), np.uint64)
+    for v in range(H):
+        for u in range(W):
+            s = bits[v, u]
+            for k in range(nw):
+                chunk = s[64 * k:64 * (k + 1)]
+                val = 0
+                for bit in chunk:
+                    val = (val << 1) | bit
+                out[v, u, k] = val
+    return out
+
+
+def census_cost(bitsL, bitsR, D, view=0):
+    H, W = bitsL.shape
+    L = len(bitsL[0, 0])
+    out = np.empty((H, W, D), f32)
+    for v in range(H):
+        for u in range(W):
+            for d in range(D):
+                lp, rp = (u + d, u) if view == 1 else (u, u - d)
+                if lp >= W or rp < 0:
+                    out[v, u, d] = f32(L)
+                else:
+                    out[v, u, d] = f32(sum(a != b for a, b in zip(bitsL[v, lp], bitsR[v, rp])))
+    return out
+
+
+def grads(gray):
+    g = gray.astype(np.int32)
+    gx = np.empty(g.shape, f32)
+    gx[:, 1:-1] = (0.5 * (g[:, 2:] - g[:, :-2])).astype(f32)
+    gx[:, 0] = g[:, 1] - g[:, 0]
+    gx[:, -1] = g[:, -1] - g[:, -2]
+    gy = np.empty(g.shape, f32)
+    gy[1:-1] = (0.5 * (g[2:] - g[:-2])).astype(f32)
+    gy[0] = g[1] - g[0]
+    gy[-1] = g[-1] - g[-2]
+    return gx, gy
+
+
+def arms(bgr, L=17, L_out=34, cT=20, cT_out=6, minL=1):
+    H, W, _ = bgr.shape
+    I = bgr.astype(np.int32)
+    out = np.zeros((H, W, 4), np.uint16)
+    dirs = [(0, -1), (0, 1), (-1, 0), (1, 0)]
+    for k, (dv, du) in enumerate(dirs):
+        for v in range(H):
+            for u in range(W):
+                n = 0
+                for arm in range(1, L_out + 1):
+                    va, ua = v + arm * dv, u + arm * du
+                    if not (0 <= va < H and 0 <= ua < W):
+                        break
+                    prev = I[v + (arm - 1) * dv, u + (arm - 1) * du]
+                    cur = I[va, ua]
+                    thr = cT if arm <= L else cT_out
+                    if np.any(np.abs(cur - prev) > cT) or np.any(np.abs(I[v, u] - cur) > thr):
+                        break
+                    n = arm
+                if n < minL:
+                    n = 0
+                    for ln in range(minL, -1, -1):
+                        if 0 <= u + ln * du < W and 0 <= v + ln * dv < H:
+                            n = ln
+                            break
+                out[v, u, k] = n
+    return out
+
+
+def grad_cost(gx0, gx1, gy0, gy1, arm, D, view=0, trunc=f32(500)):
+    H, W = gx0.shape
+    oor = f32(np.sqrt(2.0 * float(trunc) ** 2))
+    out = np.empty((H, W, D), f32)
+    sH = np.minimum(arm[..., 0], arm[..., 1]).astype(f32)
+    sV = np.minimum(arm[..., 2], arm[..., 3]).astype(f32)
+    sH[sH == 0] = 1
+    sV[sV == 0] = 1
+    a = (sH / (sH + sV)).astype(f32)
+    one_m_a = (f32(1) - a).astype(f32)
+    for d in range(D):
+        for u in range(W):
+            u0, u1 = (u + d, u) if view == 1 else (u, u - d)
+            if u0 >= W or u1 < 0:
+                out[:, u, d] = oor
+                continue
+            dx = np.minimum(np.abs(gx0[:, u0] - gx1[:, u1]), trunc).astype(f32)
+            dy = np.minimum(np.abs(gy0[:, u0] - gy1[:, u1]), trunc).astype(f32)
+            out[:, u, d] = (a[:, u] * dx).astype(f32) + (one_m_a[:, u] * dy).astype(f32)
+    return out
+
+
+def ad_cost(bgrL, bgrR, D, trunc, view=0):
+    H, W, _ = bgrL.shape
+    out = np.empty((H, W, D), f32)
+    L = bgrL.astype(f32)
+    R = bgrR.astype(f32)
+    for d in range(D):
+        for u in range(W):
+            uL, uR = (u + d, u) if view == 1 else (u, u - d)
+            if uL >= W or uR < 0:
+                out[:, u, d] = f32(trunc)
+                continue
+            s = np.abs(L[:, uL] - R[:, uR]).sum(axis=1, dtype=f32)
+            out[:, u, d] = np.minimum((s / f32(3)).astype(f32), f32(trunc))
+    return out
+
+
+def fuse(vm0, vm1, lam0, lam1):
+    e0 = expf((-vm0 / f32(lam0)).astype(f32))
+    e1 = expf((-vm1 / f32(lam1)).astype(f32))
+    return ((f32(2) - e0).astype(f32) - e1).astype(f32)
+
+
+def isect(aL, aR, D):
+    H, W, _ = aL.shape
+    out = np.zeros((H, W, D, 4), np.int32)
+    for d in range(D):
+        if d < W:
+            out[:, d:, d, :] = np.minimum(aL[:, d:, :], aR[:, :W - d, :])
+    return out
+
+
+def cbca(vm, aL, aR, iters=2):
+    H, W, D = vm.shape
+    A = isect(aL, aR, D)
+    vm = vm.copy()
+    vv, uu, dd = np.meshgrid(np.arange(H), np.arange(W), np.arange(D), indexing="ij")
+
+    def pass1d(vm, area, horiz):
+        axis = 1 if horiz else 0
+        S = np.add.accumulate(vm, axis=axis, dtype=f32)
+        Ar = np.add.accumulate(area, axis=axis)
+        tail = A[..., 0] if horiz else A[..., 2]
+        head = A[..., 1] if horiz else A[..., 3]
+        if horiz:
+            hi = (vv, uu + head, dd)
+            pt = uu - tail - 1
+            ti = (vv, np.maximum(pt, 0), dd)
+        else:
+            hi = (vv + head, uu, dd)
+            pt = vv - tail - 1
+            ti = (np.maximum(pt, 0), uu, dd)
+        inner = pt >= 0
+        out = np.where(inner, (S[hi] - S[ti]).astype(f32), S[hi]).astype(f32)
+        ao = np.where(inner, Ar[hi] - Ar[ti], Ar[hi])
+        return out, ao
+
+    for it in range(iters):
+        area = np.ones((H, W, D), np.int64)
+        order = (True, False) if it % 2 == 0 else (False, True)
+        for horiz in order:
+            vm, area = pass1d(vm, area, horiz)
+        vm = (vm / area.astype(f32)).astype(f32)
+    return vm
+
+
+def solve_all(vm, lam=f32(0.3)):
+    m = f32(f32(1) + f32(lam))
+    w = f32(1.0 / float(m))
+    return (f32(0) + (w * vm).astype(f32)).astype(f32)
+
+
+def sgm(vm, bgrL, paths=4, P1=f32(1), P2=f32(3), thres=15, redu=4):
+    H, W, D = vm.shape
+    RV = [+1, -1, 0, 0, +1, +1, -1, -1]
+    RU = [0, 0, +1, -1, -1, +1, +1, -1]
+    I = bgrL.astype(np.int32)
+    BIG = np.finfo(f32).max
+    acc = np.zeros_like(vm)
+    for i in range(paths):
+        rv, ru = RV[i], RU[i]
+        Lr = np.empty_like(vm)
+        vs = range(H - 1, -1, -1) if (rv > 0 or (rv == 0 and ru > 0)) else range(H)
+        us = list(range(W - 1, -1, -1)) if (rv > 0 or (rv == 0 and ru > 0)) else list(range(W))
+        for v in vs:
+            for u in us:
+                pv, pu = v + rv, u + ru
+                if not (0 <= pv < H and 0 <= pu < W):
+                    Lr[v, u] = vm[v, u]
+                    continue
+                D1 = int(np.max(np.abs(I[v, u] - I[pv, pu])))
+                p1, p2 = f32(P1), f32(P2)
+                if D1 > thres:
+                    p1, p2 = f32(p1 / f32(redu)), f32(p2 / f32(redu))
+                fore = Lr[pv, pu]
+                m = fore.min()
+                p1 = f32(p1 - m)
+                S1 = (fore - m).astype(f32)
+                S2 = np.full(D, BIG, f32)
+                S2[1:] = (fore[:-1] + p1).astype(f32)
+                S3 = np.full(D, BIG, f32)
+                S3[:-1] = (fore[1:] + p1).astype(f32)
+                mm = np.minimum(np.minimum(S1, S2), np.minimum(S3, np.full(D, p2, f32)))
+                Lr[v, u] = (vm[v, u] + mm).astype(f32)
+        acc = (acc + Lr).astype(f32)
+    return acc
+
+
+def wta(vm):
+    H, W, D = vm.shape
+    out = np.full((H, W), -1, np.int16)
+    BIG = np.finfo(f32).max
+    for v in range(H):
+        for u in range(W):
+            best = BIG
+            for d in range(D):
+                if best > vm[v, u, d]:
+                    best = vm[v, u, d]
+                    out[v, u] = d
+    return out
+
+
+def pipeline(pair, max_disp, cost="censusGrad", aggregate=True, solve=True, optimize=True, paths=4):
+    """Default main_.cpp sequence; returns dict of stage volumes and the disparity map."""
+    D = max_disp + 1
+    lb, rb, lg, rg = pair["lbgr"], pair["rbgr"], pair["lgray"], pair["rgray"]
+    out = {}
+    if cost == "AD":
+        vm = ad_cost(lb, rb, D, 20)
+    else:
+        bl, br = census(lg), census(rg)
+        cen = census_cost(bl, br, D)
+        if cost == "Census":
+            vm = cen
+        elif cost == "ADCensus":
+            vm = fuse(ad_cost(lb, rb, D, 1000), cen, 10, 30)
+        else:
+            gx0, gy0 = grads(lg)
+            gx1, gy1 = grads(rg)
+            aL = arms(lb)
+            vm = fuse(cen, grad_cost(gx0, gx1, gy0, gy1, aL, D), 13, 1)
+    out["cost"] = vm
+    if aggregate:
+        vm = cbca(vm, arms(lb), arms(rb))
+    out["agg"] = vm
+    if solve:
+        vm = solve_all(vm)
+    if optimize:
+        vm = sgm(vm, lb, paths=paths)
+    out["final"] = vm
+    out["disp"] = wta(vm)
+    return out

@@ -1,0 +1,210 @@
+"""GPU parity: libsm_hip.so (through the C-ABI) against the CPU oracle, bit-exact.
+
+Every comparison is on float bit patterns (volumes) or int16 (disparity): the whole path is
+IEEE-deterministic, so the bar is bit-exactness, not a tolerance (north_star allows 1e-4 for
+the float CBCA; we do not need it).
+"""
+import ctypes as C
+import glob
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from mystereomatching_amd import StereoBatch, StereoMatching, SolveAll, _capi
+from mystereomatching_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def make_sm(pair, max_disp, cost="censusGrad", agg="CBCA", opt="sgm", paths=4, keep=True, **kw):
+    StereoMatching.costcalculation, StereoMatching.aggregation, StereoMatching.optimization = cost, agg, opt
+    H, W = pair["lgray"].shape
+    prm = StereoMatching.Parameters(max_disp, H, W)
+    prm.sgm_scanNum = paths
+    for k, v in kw.items():
+        setattr(prm, k, v)
+    return StereoMatching(pair["lbgr"], pair["rbgr"], pair["lgray"], pair["rgray"], pair.get("gt"),
+                          None, pair.get("nonocc"), None, prm, keep_final_volume=keep)
+
+
+def run_reference_order(pair, max_disp, **kw):
+    """main_.cpp:139-163 order through the mirror API; returns stage volumes + DP[0]."""
+    sm = make_sm(pair, max_disp, **kw)
+    sm.costCalculate()
+    agg = sm.vm[0]
+    SolveAll([sm], 1, 0.3)
+    dp = sm.dispOptimize()
+    final = sm.vm[0]
+    return sm, agg, final, dp
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_golden(path):
+    g = np.load(path)
+    pair = {k: g[k] for k in ("lbgr", "rbgr", "lgray", "rgray")}
+    sm, agg, final, dp = run_reference_order(pair, int(g["max_disp"]), cost=str(g["cost"]), paths=int(g["paths"]))
+    np.testing.assert_array_equal(dp, g["disp"])
+    assert sha(agg) == str(g["sha_agg"])
+    assert sha(final) == str(g["sha_final"])
+    if "agg_vol" in g.files:
+        np.testing.assert_array_equal(bits(agg), bits(g["agg_vol"]))
+
+
+@pytest.mark.parametrize("cost", ["censusGrad", "Census", "ADCensus", "AD"])
+def test_cost_volume_and_stages(oracle, cost):
+    H, W, md = 41, 67, 23
+    pair = S.make_pair(H, W, md + 1, 11)
+    cfg = oracle.config(H, W, md, cost=cost)
+    ref = oracle.run(pair, cfg, dumps=True, right=True)
+    # raw cost volume: aggregation off, WTA only
+    sm = make_sm(pair, md, cost=cost, agg="", opt="")
+    sm.costCalculate()
+    np.testing.assert_array_equal(bits(sm.vm[0]), bits(ref["cost"]))
+    _, agg, final, dp = run_reference_order(pair, md, cost=cost)
+    np.testing.assert_array_equal(bits(agg), bits(ref["agg"]))
+    np.testing.assert_array_equal(bits(final), bits(ref["final"]))
+    np.testing.assert_array_equal(dp, ref["disp"])
+
+
+def test_right_view_volume(oracle):
+    H, W, md = 33, 52, 19
+    pair = S.make_pair(H, W, md + 1, 12)
+    cfg = oracle.config(H, W, md)
+    ref = oracle.cost_volume(pair, cfg, view=1)
+    StereoMatching.costcalculation, StereoMatching.aggregation, StereoMatching.optimization = "censusGrad", "", ""
+    lib = _capi.load()
+    p = _capi.default_params(md, H, W, aggregation=0, optimization=0, compute_right_view=1)
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        a = {k: np.ascontiguousarray(pair[k]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        _capi.check(lib, ctx, lib.sm_set_images(ctx, _capi.ptr(a["lbgr"]), _capi.ptr(a["rbgr"]), W * 3,
+                                                _capi.ptr(a["lgray"]), _capi.ptr(a["rgray"]), W))
+        _capi.check(lib, ctx, lib.sm_cost_calculate(ctx))
+        got = np.empty((H, W, md + 1), np.float32)
+        _capi.check(lib, ctx, lib.sm_get_volume(ctx, 1, _capi.ptr(got)))
+    finally:
+        lib.sm_destroy(ctx)
+    np.testing.assert_array_equal(bits(got), bits(ref))
+
+
+def test_census_and_arms(oracle):
+    H, W, md = 29, 45, 15
+    pair = S.make_pair(H, W, md + 1, 13)
+    cfg = oracle.config(H, W, md)
+    sm = make_sm(pair, md)
+    sm.costCalculate()
+    for view, g, c in ((0, "lgray", "lbgr"), (1, "rgray", "rbgr")):
+        codes = sm.census_codes(view)
+        np.testing.assert_array_equal(codes, oracle.census(pair[g], cfg))
+        np.testing.assert_array_equal(sm.HVL[view], oracle.arms(pair[c], cfg))
+
+
+@pytest.mark.parametrize("H,W,md,paths", [(2, 2, 0, 4), (3, 70, 63, 4), (70, 3, 5, 8), (17, 23, 64, 8),
+                                          (25, 31, 127, 4), (13, 90, 191, 8), (9, 40, 255, 4)])
+def test_shapes_and_edge_cases(oracle, H, W, md, paths):
+    """Tiny/ragged images, D not a multiple of 64, D > W, D = 1, 8 paths."""
+    pair = S.make_pair(H, W, md + 1, 14 + H)
+    cfg = oracle.config(H, W, md, sgm_paths=paths)
+    ref = oracle.run(pair, cfg, dumps=True)
+    _, agg, final, dp = run_reference_order(pair, md, paths=paths)
+    np.testing.assert_array_equal(bits(agg), bits(ref["agg"]))
+    np.testing.assert_array_equal(bits(final), bits(ref["final"]))
+    np.testing.assert_array_equal(dp, ref["disp"])
+
+
+def test_flat_images_long_arms(oracle):
+    """Uniform regions: arms saturate at L_out = 34, prefix sums run long."""
+    H, W, md = 60, 90, 31
+    pair = S.make_pair(H, W, md + 1, 20)
+    for k in ("lbgr", "rbgr"):
+        pair[k] = (pair[k] // 128 * 128).astype(np.uint8)
+    pair["lgray"], pair["rgray"] = S.bgr_to_gray(pair["lbgr"]), S.bgr_to_gray(pair["rbgr"])
+    cfg = oracle.config(H, W, md)
+    ref = oracle.run(pair, cfg, dumps=True)
+    _, agg, final, dp = run_reference_order(pair, md)
+    np.testing.assert_array_equal(bits(agg), bits(ref["agg"]))
+    np.testing.assert_array_equal(dp, ref["disp"])
+
+
+def test_batch_matches_single_and_oracle(oracle):
+    H, W, md, n = 48, 64, 31, 5
+    b = S.make_batch(n, H, W, md + 1, first_index=30)
+    sb = StereoBatch(md, H, W, n)
+    sb.upload(b["lbgr"], b["rbgr"], b["lgray"], b["rgray"])
+    disp = sb.run(0.3)
+    disp2 = sb.run(0.3)
+    np.testing.assert_array_equal(disp, disp2)  # deterministic
+    cfg = oracle.config(H, W, md)
+    for i in range(n):
+        pair = {k: b[k][i] for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        np.testing.assert_array_equal(disp[i], oracle.run(pair, cfg)["disp"])
+    sb.close()
+
+
+def test_kitti_size_8path(oracle):
+    """KITTI-2015 shape (configs[2]): 375x1242, D=192, 8-path SGM, bit-exact map."""
+    H, W, md = 375, 1242, 191
+    pair = S.make_pair(H, W, md + 1, 40)
+    cfg = oracle.config(H, W, md, sgm_paths=8)
+    ref = oracle.run(pair, cfg)
+    sb = StereoBatch(md, H, W, 1, sgm_paths=8)
+    sb.upload(pair["lbgr"][None], pair["rbgr"][None], pair["lgray"][None], pair["rgray"][None])
+    disp = sb.run(0.3)[0]
+    np.testing.assert_array_equal(disp, ref["disp"])
+    sb.close()
+
+
+def test_device_expf_exhaustive(oracle):
+    """Device expf == host libm expf on every negative float down to the underflow bound."""
+    lib = _capi.load()
+    p = _capi.default_params(15, 8, 8)
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        first, last = 0x80000000, 0xC2D00000
+        chunk = 1 << 25
+        out = np.empty(chunk, np.float32)
+        b = first
+        bad = 0
+        while b <= last:
+            n = min(chunk, last - b + 1)
+            _capi.check(lib, ctx, lib.sm_expf_device_range(ctx, b, n, _capi.ptr(out)))
+            ref = oracle.expf_range(b, n)
+            bad += int(np.count_nonzero(out[:n].view(np.uint32) != ref.view(np.uint32)))
+            b += n
+        assert bad == 0
+    finally:
+        lib.sm_destroy(ctx)
+
+
+def test_state_errors():
+    lib = _capi.load()
+    p = _capi.default_params(15, 16, 16)
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        assert lib.sm_cost_calculate(ctx) == _capi.SM_ESTATE
+        assert lib.sm_disp_optimize(ctx, None) == _capi.SM_ESTATE
+        assert b"must follow" in lib.sm_last_error(ctx)
+        a = np.zeros((16, 16, 3), np.uint8)
+        g = np.zeros((16, 16), np.uint8)
+        assert lib.sm_set_images(ctx, _capi.ptr(a), _capi.ptr(a), 16, _capi.ptr(g), _capi.ptr(g), 16) == _capi.SM_EINVAL
+        assert lib.sm_set_images(ctx, _capi.ptr(a), _capi.ptr(a), 48, _capi.ptr(g), _capi.ptr(g), 16) == _capi.SM_OK
+        assert lib.sm_solve_all(ctx, 1, 0.3) == _capi.SM_ESTATE
+        assert lib.sm_cost_calculate(ctx) == _capi.SM_OK
+        assert lib.sm_solve_all(ctx, 2, 0.3) == _capi.SM_EINVAL
+    finally:
+        lib.sm_destroy(ctx)

@@ -47,6 +47,8 @@ struct sm_ctx {
     float* vm1 = nullptr;       // [cap][npix][D] (right view, optional)
     float* acc = nullptr;       // [cap][npix][D]
     int16_t* disp = nullptr;    // [cap][npix]
+    float* dummy = nullptr;     // 64 floats written by lanes past D
+    uint8_t* flags = nullptr;   // [cap][npix] SGM colour-difference penalty bits
     int n_loaded = 0;
     int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized
     float lut_a[1024], lut_b[1024];
@@ -180,7 +182,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 }
 
 void free_all(sm_ctx* c) {
-    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms, c->vm0, c->vm1, c->acc, c->disp};
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms, c->vm0, c->vm1, c->acc, c->disp, c->dummy, c->flags};
     for (void* q : ptrs)
         if (q) hipFree(q);
     for (auto& r : c->recs) {
@@ -244,9 +246,15 @@ sm_status run_cost(sm_ctx* c, int n, int view) {
 }
 
 sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w) {
+    // cbca_core (cpp:5585-5666): iteration k runs H then V for even k, V then H for odd k.
+    // The last pass of iteration k and the first pass of iteration k+1 share a direction and
+    // are fused into one CB_NORM_SCAN sweep, so N iterations take N + 1 sweeps.
     const sm_params& p = c->p;
+    const int N = p.cbca_iterations;
+    if (N <= 0) return SM_OK;
     sm::CbcaArgs a{};
     a.vm = c->vm0;
+    a.dummy = c->dummy;
     a.arms = (const uint32_t*)c->arms;
     a.H = p.rows;
     a.W = p.cols;
@@ -254,16 +262,20 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w) {
     a.lag = cbca_lag(p);
     a.ring = 2 * a.lag + 2;
     a.scale = w;
+    a.apply_scale = 0;
     const double bytes = (double)n * c->nvol * 8.0;
-    for (int it = 0; it < p.cbca_iterations; it++) {
-        const bool first_h = (it % 2 == 0);  // cbca_core: it0 H then V, it1 V then H (cpp:5608-5621)
-        a.apply_scale = 0;
-        sm_status s = timed(c, first_h ? "cbca_h_scan" : "cbca_v_scan", bytes,
-                            [&] { sm::launch_cbca_pass(a, first_h, false, n, c->st); });
-        if (s) return s;
-        a.apply_scale = (fuse_scale && it == p.cbca_iterations - 1) ? 1 : 0;
-        s = timed(c, first_h ? "cbca_v_norm" : "cbca_h_norm", bytes,
-                  [&] { sm::launch_cbca_pass(a, !first_h, true, n, c->st); });
+    sm_status s = timed(c, "cbca_h_scan", bytes, [&] { sm::launch_cbca(a, true, sm::CB_SCAN, n, c->st); });
+    if (s) return s;
+    for (int k = 0; k < N; k++) {
+        const bool dir_h = (k % 2 == 1);  // direction of iteration k's second pass
+        if (k + 1 < N) {
+            s = timed(c, dir_h ? "cbca_h_norm_scan" : "cbca_v_norm_scan", bytes,
+                      [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM_SCAN, n, c->st); });
+        } else {
+            a.apply_scale = fuse_scale ? 1 : 0;
+            s = timed(c, dir_h ? "cbca_h_norm" : "cbca_v_norm", bytes,
+                      [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM, n, c->st); });
+        }
         if (s) return s;
     }
     return SM_OK;
@@ -281,7 +293,13 @@ sm_status run_optimize(sm_ctx* c, int n) {
         static const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};  // cpp:6208
         static const char* NAMES[8] = {"sgm_path0", "sgm_path1", "sgm_path2", "sgm_path3",
                                        "sgm_path4", "sgm_path5", "sgm_path6", "sgm_path7"};
+        sm_status s0 = timed(c, "penalty_flags", (double)n * c->npix * 4, [&] {
+            sm::launch_penalty_flags(c->bgr, c->flags, n, p.rows, p.cols, p.sgm_cor_dif_thres, c->st);
+        });
+        if (s0) return s0;
         sm::SgmArgs a{};
+        a.flags = c->flags;
+        a.dummy = c->dummy;
         a.vm = c->vm0;
         a.acc = c->acc;
         a.bgr = c->bgr;
@@ -297,6 +315,7 @@ sm_status run_optimize(sm_ctx* c, int n) {
         for (int i = 0; i < p.sgm_paths; i++) {
             a.rv = RV[i];
             a.ru = RU[i];
+            a.dir = i;
             int mode = (i == 0 ? sm::SGM_FIRST : 0) | (i == p.sgm_paths - 1 ? sm::SGM_LAST : 0);
             // algorithmic bytes per element: read C (+ read acc) (+ write acc | write final)
             double per = 4.0 + ((mode & sm::SGM_FIRST) ? 0 : 4.0) + ((mode & sm::SGM_LAST) ? (p.keep_final_volume ? 4.0 : 0) : 4.0);
@@ -425,6 +444,8 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
         if ((s = dalloc(c, &c->acc, cap * c->nvol))) return s;
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
+    if ((s = dalloc(c, &c->dummy, 64))) return s;
+    if ((s = dalloc(c, &c->flags, cap * c->npix))) return s;
     build_luts(c);
     HIP_TRY(c, sm::upload_luts(c->lut_a, c->lut_b, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));

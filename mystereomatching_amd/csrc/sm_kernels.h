@@ -8,6 +8,8 @@ namespace sm {
 
 enum { SM_M_CENSUS_GRAD = 0, SM_M_CENSUS = 1, SM_M_AD_CENSUS = 2, SM_M_AD = 3 };
 enum { SGM_FIRST = 1, SGM_LAST = 2 };
+enum { CB_SCAN = 0, CB_NORM = 1, CB_NORM_SCAN = 2 };
+constexpr int CBCA_TILE = 16;  // steps of lookahead per wave in the CBCA line sweeps
 
 struct CostArgs {
     float* vm;                  // [n][H][W][D] destination (view's volume)
@@ -27,6 +29,7 @@ struct CostArgs {
 
 struct CbcaArgs {
     float* vm;                  // [n][H][W][D], in place
+    float* dummy;               // 64 floats: private slots for lanes past D
     const uint32_t* arms;       // [n][2][H][W] packed L|R<<8|U<<16|D<<24
     int H, W, D;
     int lag, ring;              // lag = max arm length, ring = 2*lag + 2
@@ -37,9 +40,11 @@ struct CbcaArgs {
 struct SgmArgs {
     float* vm;                  // [n][H][W][D] aggregated costs (also the final volume if keep_final)
     float* acc;                 // [n][H][W][D] running path sum
+    float* dummy;               // 64 floats: store target of elements past D
     const uint8_t* bgr;         // [n][2][H][W][3] (left colour used for P1/P2 adaptivity)
     int16_t* disp;              // [n][H][W]
-    int H, W, D, rv, ru;
+    const uint8_t* flags;       // [n][H][W] bit i: colour-difference penalty towards direction i
+    int H, W, D, rv, ru, dir;
     float p1, p2;
     int cor_thres, redu, keep_final;
 };
@@ -50,9 +55,10 @@ void launch_census_grad(const uint8_t* gray, ulonglong2* code, float* gx, float*
 void launch_arms(const uint8_t* bgr, uint8_t* arms, int n, int H, int W, int L, int L_out, int C_D, int C_D_out,
                  int minL, hipStream_t st);
 void launch_cost(const CostArgs& a, int method, int n, hipStream_t st);
-void launch_cbca_pass(const CbcaArgs& a, bool horiz, bool norm, int n, hipStream_t st);
+void launch_cbca(const CbcaArgs& a, bool horiz, int mode, int n, hipStream_t st);
 void launch_scale(float* vm, size_t n, float w, hipStream_t st);
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st);
+void launch_penalty_flags(const uint8_t* bgr, uint8_t* flags, int n, int H, int W, int thres, hipStream_t st);
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);
 float expf_host(float x);

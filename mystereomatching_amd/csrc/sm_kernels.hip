@@ -225,100 +225,6 @@ __global__ void k_cost(const CostArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// K2: one CBCA 1-D pass along lines (rows for H, columns for V), in place on vm.
-// Fuses gen1DCumu (cpp:3896-3926) + cal1DCost (h:1643-1715) [+ genfinalVm_cbca (cpp:3969-3992)
-// and the SolveAll scale (cpp:2189-2201) on the second pass of an iteration].
-// One wave = one (line, 64-disparity chunk); the sequential prefix sum S runs along the line in
-// the reference's order; S values live in an LDS ring of 2*lag+2 slots (lag = max arm) so the
-// head/tail differences S[i+head] - S[i-tail-1] are read back without a second HBM pass.
-// Areas (int) are recomputed from the arms instead of being stored: after the first pass of an
-// iteration the area of (p,d) is tail+head+1 of that pass's intersection arms, so the second
-// pass prefix-sums that value (mod 2^16 — the true window area is < 2^16) next to S.
-// Intersection arms (genTrueHorVerArms, cpp:2794-2845): min(A0(v,u), A1(v,u-d)) per arm, 0 if
-// u-d < 0.
-// ---------------------------------------------------------------------------------------
-__device__ inline uint32_t isect_arms(uint32_t a0, const uint32_t* __restrict__ a1row, int u, int d) {
-    if (u - d < 0) return 0u;
-    const uint32_t b = a1row[u - d];
-    uint32_t r = min(a0 & 0xffu, b & 0xffu);
-    r |= min(a0 & 0xff00u, b & 0xff00u);
-    r |= min(a0 & 0xff0000u, b & 0xff0000u);
-    r |= min(a0 & 0xff000000u, b & 0xff000000u);
-    return r;
-}
-
-template <bool HORIZ, bool NORM>
-__global__ __launch_bounds__(64) void k_cbca_pass(const CbcaArgs a) {
-    extern __shared__ float smem[];
-    const int lane = threadIdx.x;
-    const int nchunks = (a.D + 63) >> 6;
-    const int line = blockIdx.x / nchunks, chunk = blockIdx.x - line * nchunks;
-    const int b = blockIdx.y;
-    const int d = chunk * 64 + lane;
-    const bool valid = d < a.D;
-    const int dd = valid ? d : a.D - 1;
-    const int H = a.H, W = a.W, D = a.D;
-    const size_t npix = (size_t)H * W;
-    float* vm = a.vm + (size_t)b * npix * D;
-    const uint32_t* A0 = a.arms + (size_t)b * 2 * npix;
-    const uint32_t* A1 = A0 + npix;
-    const int len = HORIZ ? W : H;
-    const int ring = a.ring, lag = a.lag;
-    float* sring = smem;                                   // [ring][64]
-    uint16_t* aring = (uint16_t*)(smem + ring * 64);       // [ring][64] (NORM only)
-    // arm byte positions: H pass tail=L(0) head=R(1); V pass tail=U(2) head=D(3).
-    const int tsh = HORIZ ? 0 : 16, hsh = HORIZ ? 8 : 24;
-    const int psh_t = HORIZ ? 16 : 0, psh_h = HORIZ ? 24 : 8;  // perpendicular arms for areas
-    float S = 0.f;
-    uint32_t Acc = 0;
-    int wslot = 0;           // ring slot of j
-    for (int j = 0; j < len + lag; j++) {
-        if (j < len) {
-            const int v = HORIZ ? line : j, u = HORIZ ? j : line;
-            const size_t p = (size_t)v * W + u;
-            const float x = vm[p * D + dd];
-            S = (j == 0) ? x : S + x;
-            sring[wslot * 64 + lane] = S;
-            if (NORM) {
-                const uint32_t is = isect_arms(A0[p], A1 + (size_t)v * W, u, d);
-                const uint32_t ain = ((is >> psh_t) & 0xffu) + ((is >> psh_h) & 0xffu) + 1u;
-                Acc = (j == 0) ? ain : Acc + ain;
-                aring[wslot * 64 + lane] = (uint16_t)Acc;
-            }
-        }
-        const int i = j - lag;
-        if (i >= 0) {
-            const int v = HORIZ ? line : i, u = HORIZ ? i : line;
-            const size_t p = (size_t)v * W + u;
-            const uint32_t is = isect_arms(A0[p], A1 + (size_t)v * W, u, d);
-            const int tail = (is >> tsh) & 0xff, head = (is >> hsh) & 0xff;
-            // slot of index k: slot(j) - (j - k), wrapped
-            int hs = wslot - (j - (i + head));
-            if (hs < 0) hs += ring;
-            float out = sring[hs * 64 + lane];
-            uint32_t area = 0;
-            if (NORM) area = aring[hs * 64 + lane];
-            if (i - tail - 1 >= 0) {
-                int ts = wslot - (j - (i - tail - 1));
-                if (ts < 0) ts += ring;
-                out = out - sring[ts * 64 + lane];
-                if (NORM) area = (area - aring[ts * 64 + lane]) & 0xffffu;
-            }
-            if (NORM) {
-                out = out / (float)area;
-                if (a.apply_scale) {
-                    float sum = 0.f;
-                    sum += a.scale * out;
-                    out = sum;
-                }
-            }
-            if (valid) vm[p * D + d] = out;
-        }
-        wslot = (wslot + 1 == ring) ? 0 : wslot + 1;
-    }
-}
-
 // SolveAll with PY_LVL = 1 as a standalone pass (used by the reference-ordered API):
 // vm = 0 + invWgt * vm (cpp:2189-2201).
 __global__ void k_scale(float* __restrict__ vm, size_t n, float w) {
@@ -326,136 +232,6 @@ __global__ void k_scale(float* __restrict__ vm, size_t n, float w) {
         float sum = 0.f;
         sum += w * vm[i];
         vm[i] = sum;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// K3: SGM path walker.  One wave walks one scan line of direction r = (rv, ru) (the previous
-// pixel of p is p + r, costScan cpp:1983-2029); lane l holds disparities [l*K, l*K+K).
-// updateCost<float> (h:2206-2280):  m = min_d Lprev;  P1' = P1 - m;
-//   L(d) = C(d) + min(min(Lp(d) - m, Lp(d-1) + P1'), min(Lp(d+1) + P1', P2))
-// FIRST: acc = 0 + L; middle: acc = acc + L; LAST: f = acc + L then WTA (first strict minimum,
-// gen_dispFromVm cpp:3928-3967) and optionally vm = f.  Path order = the reference's sum order.
-// ---------------------------------------------------------------------------------------
-template <int K, int MODE>
-__global__ __launch_bounds__(256) void k_sgm_path(const SgmArgs a) {
-    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    const int H = a.H, W = a.W, D = a.D;
-    const int b = blockIdx.y;
-    const int rv = a.rv, ru = a.ru;
-    // enumerate the lines: start pixels are those whose predecessor p + r lies outside.
-    int nlines, v0, u0;
-    if (rv == 0) {            // horizontal: one line per row
-        nlines = H;
-        if (wave >= nlines) return;
-        v0 = wave;
-        u0 = ru > 0 ? W - 1 : 0;
-    } else if (ru == 0) {     // vertical: one line per column
-        nlines = W;
-        if (wave >= nlines) return;
-        u0 = wave;
-        v0 = rv > 0 ? H - 1 : 0;
-    } else {                  // diagonal: starts on the entry row, then on the entry column
-        nlines = W + H - 1;
-        if (wave >= nlines) return;
-        const int vedge = rv > 0 ? H - 1 : 0, uedge = ru > 0 ? W - 1 : 0;
-        if (wave < W) {
-            v0 = vedge;
-            u0 = wave;
-        } else {
-            const int k = wave - W;           // rows other than vedge
-            v0 = rv > 0 ? k : k + 1;
-            u0 = uedge;
-        }
-    }
-    const int sv = -rv, su = -ru;             // walk direction
-    int steps;
-    {
-        const int nv = rv > 0 ? v0 + 1 : (rv < 0 ? H - v0 : 1 << 30);
-        const int nu = ru > 0 ? u0 + 1 : (ru < 0 ? W - u0 : 1 << 30);
-        steps = min(nv, nu);
-    }
-    const size_t npix = (size_t)H * W;
-    const float* C = a.vm + (size_t)b * npix * D;
-    float* acc = a.acc + (size_t)b * npix * D;
-    float* fin = a.vm + (size_t)b * npix * D;
-    const uint8_t* Ic = a.bgr + (size_t)b * 2 * npix * 3;   // left colour image of pair b
-    const int d0 = lane * K;
-    float Lp[K];
-    int v = v0, u = u0;
-    for (int s = 0; s < steps; s++, v += sv, u += su) {
-        const size_t p = (size_t)v * W + u;
-        const float* cp = C + p * D;
-        float c[K];
-#pragma unroll
-        for (int k = 0; k < K; k++) c[k] = (d0 + k < D) ? cp[d0 + k] : FLT_MAX;
-        float L[K];
-        if (s == 0) {
-#pragma unroll
-            for (int k = 0; k < K; k++) L[k] = c[k];
-        } else {
-            const uint8_t* q0 = Ic + p * 3;
-            const uint8_t* q1 = Ic + ((size_t)(v - sv) * W + (u - su)) * 3;
-            int D1 = max(max(abs((int)q0[0] - (int)q1[0]), abs((int)q0[1] - (int)q1[1])), abs((int)q0[2] - (int)q1[2]));
-            float P1 = a.p1, P2 = a.p2;
-            if (D1 > a.cor_thres) {
-                P1 /= (float)a.redu;
-                P2 /= (float)a.redu;
-            }
-            float lm = Lp[0];
-#pragma unroll
-            for (int k = 1; k < K; k++) lm = fminf(lm, Lp[k]);
-            const float m = wave_min(lm);
-            P1 -= m;
-            const float left_nb = __shfl_up(Lp[K - 1], 1);
-            const float right_nb = __shfl_down(Lp[0], 1);
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const int d = d0 + k;
-                const float prev = (k == 0) ? left_nb : Lp[k - 1];
-                const float next = (k == K - 1) ? right_nb : Lp[k + 1];
-                const float S1 = Lp[k] - m;
-                const float S2 = d - 1 >= 0 ? prev + P1 : FLT_MAX;
-                const float S3 = d + 1 < D ? next + P1 : FLT_MAX;
-                const float S4 = P2;
-                const float mm = fminf(fminf(S1, S2), fminf(S3, S4));
-                L[k] = (d < D) ? c[k] + mm : FLT_MAX;
-            }
-        }
-        float* ap = acc + p * D;
-        float f[K];
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            const float prev = (MODE & SGM_FIRST) ? 0.f : ((d0 + k < D) ? ap[d0 + k] : 0.f);
-            f[k] = (d0 + k < D) ? prev + L[k] : FLT_MAX;   // sum += Lr[num] (cpp:2046-2049)
-        }
-        if (MODE & SGM_LAST) {
-            if (a.keep_final) {
-#pragma unroll
-                for (int k = 0; k < K; k++)
-                    if (d0 + k < D) fin[p * D + d0 + k] = f[k];
-            }
-            // WTA: local first minimum, then wave min value, then lowest index holding it.
-            float bm = f[0];
-            int bi = d0;
-#pragma unroll
-            for (int k = 1; k < K; k++)
-                if (bm > f[k]) {
-                    bm = f[k];
-                    bi = d0 + k;
-                }
-            const float wm = wave_min(bm);
-            const int cand = (bm == wm && d0 < D) ? bi : 0x7fffffff;
-            const int widx = wave_min_i(cand);
-            if (lane == 0) a.disp[(size_t)b * npix + p] = (int16_t)((wm < FLT_MAX) ? widx : -1);
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                if (d0 + k < D) ap[d0 + k] = f[k];
-        }
-#pragma unroll
-        for (int k = 0; k < K; k++) Lp[k] = L[k];
     }
 }
 
@@ -521,33 +297,10 @@ void launch_cost(const CostArgs& a, int method, int n, hipStream_t st) {
     }
 }
 
-void launch_cbca_pass(const CbcaArgs& a, bool horiz, bool norm, int n, hipStream_t st) {
-    const int nchunks = (a.D + 63) / 64;
-    const int lines = horiz ? a.H : a.W;
-    dim3 grid(lines * nchunks, n);
-    const size_t shm = (size_t)a.ring * 64 * (4 + (norm ? 2 : 0));
-    if (horiz && norm) hipLaunchKernelGGL((k_cbca_pass<true, true>), grid, dim3(64), shm, st, a);
-    else if (horiz) hipLaunchKernelGGL((k_cbca_pass<true, false>), grid, dim3(64), shm, st, a);
-    else if (norm) hipLaunchKernelGGL((k_cbca_pass<false, true>), grid, dim3(64), shm, st, a);
-    else hipLaunchKernelGGL((k_cbca_pass<false, false>), grid, dim3(64), shm, st, a);
-}
-
 void launch_scale(float* vm, size_t n, float w, hipStream_t st) {
     size_t blocks = (n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, st, vm, n, w);
-}
-
-template <int K>
-static void launch_sgm_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
-    int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
-    dim3 grid((nlines + 3) / 4, n);
-    switch (mode) {
-        case SGM_FIRST: hipLaunchKernelGGL((k_sgm_path<K, SGM_FIRST>), grid, dim3(256), 0, st, a); break;
-        case SGM_LAST: hipLaunchKernelGGL((k_sgm_path<K, SGM_LAST>), grid, dim3(256), 0, st, a); break;
-        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm_path<K, SGM_FIRST | SGM_LAST>), grid, dim3(256), 0, st, a); break;
-        default: hipLaunchKernelGGL((k_sgm_path<K, 0>), grid, dim3(256), 0, st, a); break;
-    }
 }
 
 int sgm_k_for(int D) {
@@ -557,19 +310,6 @@ int sgm_k_for(int D) {
     if (k <= 8) return 8;
     if (k <= 12) return 12;
     return 16;
-}
-
-void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {
-    switch (sgm_k_for(a.D)) {
-        case 1: launch_sgm_k<1>(a, mode, n, st); break;
-        case 2: launch_sgm_k<2>(a, mode, n, st); break;
-        case 3: launch_sgm_k<3>(a, mode, n, st); break;
-        case 4: launch_sgm_k<4>(a, mode, n, st); break;
-        case 6: launch_sgm_k<6>(a, mode, n, st); break;
-        case 8: launch_sgm_k<8>(a, mode, n, st); break;
-        case 12: launch_sgm_k<12>(a, mode, n, st); break;
-        default: launch_sgm_k<16>(a, mode, n, st); break;
-    }
 }
 
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st) {

@@ -1,0 +1,269 @@
+// sm_sgm.hip — semi-global matching path sweeps with the path sum and WTA fused in.
+//
+// Reference: sgm (stereoMatching.cpp:6204-6224) runs costScan (cpp:1983-2029) for the direction
+// table rv = {+1,-1,0,0,+1,+1,-1,-1}, ru = {0,0,+1,-1,-1,+1,+1,-1} (numOfDirec = 4 by default),
+// updateCost<float> (h:2206-2280) per pixel, then gen_sgm_vm (cpp:2031-2056) sums the path
+// volumes in path order and gen_dispFromVm (cpp:3928-3967) takes the first strict minimum.
+// For a pixel p whose predecessor p + r is inside the image:
+//   m = min_d Lr(p+r, d);  P1, P2 = 1, 3 (/4 if max_c |I(p) - I(p+r)| > 15);  P1' = P1 - m
+//   Lr(p, d) = C(p, d) + min(min(Lr(p+r,d) - m, Lr(p+r,d-1) + P1'), min(Lr(p+r,d+1) + P1', P2))
+// (out-of-range d neighbours are FLT_MAX); a path starts with Lr = C.
+//
+// gfx950 mapping.  One wave walks one scan line of a direction (the previous pixel of each step
+// is the wave's own previous step), lane l holding disparities [l*K, l*K + K).  The path minimum
+// m is a DPP + permlane wave reduction, the d +/- 1 neighbours cross lanes with DPP wave_shr/shl —
+// no LDS anywhere.  Path order is kept by running the directions as consecutive launches that
+// accumulate into one sum volume: path 0 writes acc = 0 + L0, middle paths acc += Li, and the
+// last path adds its Li, takes the WTA in registers and writes only the int16 disparity (and the
+// summed volume when the caller asks for it).  The next T steps of C and acc are prefetched into
+// registers; the colour-difference penalty flags of every pixel are precomputed once per pair.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_device.h"
+#include "sm_kernels.h"
+
+namespace sm {
+
+__constant__ int c_rv[8] = {+1, -1, 0, 0, +1, +1, -1, -1};
+__constant__ int c_ru[8] = {0, 0, +1, -1, -1, +1, +1, -1};
+
+// bit i of flags(p) = (D1 between p and p + r_i > cor_thres), left colour image (updateCost
+// leftFirst branch, h:2223-2229).  One thread per pixel.
+__global__ void k_penalty_flags(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ flags, int H, int W,
+                                int thres) {
+    const int npix = H * W;
+    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= npix) return;
+    const int b = blockIdx.y;
+    const uint8_t* I = bgr + (size_t)b * 2 * npix * 3;
+    const int v = pix / W, u = pix - v * W;
+    const uint8_t* q0 = I + (size_t)pix * 3;
+    uint32_t f = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int vv = v + c_rv[i], uu = u + c_ru[i];
+        if (vv < 0 || vv >= H || uu < 0 || uu >= W) continue;
+        const uint8_t* q1 = I + ((size_t)vv * W + uu) * 3;
+        const int D1 = max(max(abs((int)q0[0] - (int)q1[0]), abs((int)q0[1] - (int)q1[1])), abs((int)q0[2] - (int)q1[2]));
+        if (D1 > thres) f |= 1u << i;
+    }
+    flags[(size_t)b * npix + pix] = (uint8_t)f;
+}
+
+template <int K>
+__device__ __forceinline__ float dpp_shr1(float v) {  // lane l <- lane l-1; lane 0 <- FLT_MAX
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, FLT_MAX),
+                                                                 __builtin_bit_cast(int, v), DPP_WAVE_SHR1, 0xF, 0xF, false));
+}
+template <int K>
+__device__ __forceinline__ float dpp_shl1(float v) {  // lane l <- lane l+1; lane 63 <- FLT_MAX
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, FLT_MAX),
+                                                                 __builtin_bit_cast(int, v), DPP_WAVE_SHL1, 0xF, 0xF, false));
+}
+
+template <int K, int T>
+struct SgmTile {
+    float c[T][K];
+    float acc[T][K];
+    uint32_t fl;  // lane t < T: penalty flags of the pixel of step j0 + t
+};
+
+template <int K, int MODE, int T>
+__global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int H = a.H, W = a.W, D = a.D;
+    const int b = blockIdx.y;
+    const int rv = a.rv, ru = a.ru;
+    int nlines, v0, u0;
+    if (rv == 0) {
+        nlines = H;
+        v0 = wave;
+        u0 = ru > 0 ? W - 1 : 0;
+    } else if (ru == 0) {
+        nlines = W;
+        u0 = wave;
+        v0 = rv > 0 ? H - 1 : 0;
+    } else {
+        nlines = W + H - 1;
+        const int vedge = rv > 0 ? H - 1 : 0, uedge = ru > 0 ? W - 1 : 0;
+        if (wave < W) {
+            v0 = vedge;
+            u0 = wave;
+        } else {
+            const int k = wave - W;
+            v0 = rv > 0 ? k : k + 1;
+            u0 = uedge;
+        }
+    }
+    if (wave >= nlines) return;  // wave-uniform
+    int steps;
+    {
+        const int nv = rv > 0 ? v0 + 1 : (rv < 0 ? H - v0 : 1 << 30);
+        const int nu = ru > 0 ? u0 + 1 : (ru < 0 ? W - u0 : 1 << 30);
+        steps = min(nv, nu);
+    }
+    const int pstep = -rv * W - ru;  // pixel index delta per step (walk = -r)
+    const size_t npix = (size_t)H * W;
+    const size_t p0 = (size_t)v0 * W + u0;
+    const int d0 = lane * K;
+    // per-element load/store bases: elements past D read a clamped (valid) address and store to
+    // a private dummy slot, so no store is predicated
+    const float* cbase = a.vm + ((size_t)b * npix + p0) * D;
+    float* abase = a.acc + ((size_t)b * npix + p0) * D;
+    float* fbase = a.vm + ((size_t)b * npix + p0) * D;
+    const uint8_t* flbase = a.flags + (size_t)b * npix + p0;
+    int16_t* dbase = a.disp + (size_t)b * npix + p0;
+    const int vstep = pstep * D;
+    int ld[K];          // load column (clamped to a valid address)
+    bool val[K];
+    float* ap[K];       // store targets: real element or this lane's dummy slot (stride 0)
+    float* fp[K];
+    int sst[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        val[k] = d0 + k < D;
+        ld[k] = val[k] ? d0 + k : D - 1;
+        ap[k] = val[k] ? abase + d0 + k : a.dummy + ((lane * K + k) & 63);
+        fp[k] = val[k] ? fbase + d0 + k : a.dummy + ((lane * K + k) & 63);
+        sst[k] = val[k] ? vstep : 0;
+    }
+    int dacc = -1;      // lane s holds the disparity of step j0 + s until the tile's store
+    const float p1 = a.p1, p2 = a.p2;
+    const float p1r = p1 / (float)a.redu, p2r = p2 / (float)a.redu;  // updateCost: P1 /= reduCoeffi1
+    const int dir = a.dir;
+
+    auto clampi = [&](int s) { return s < steps ? s : steps - 1; };
+    auto load = [&](SgmTile<K, T>& t, int j0) {
+#pragma unroll
+        for (int s = 0; s < T; s++) {
+            const int off = clampi(j0 + s) * vstep;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                t.c[s][k] = cbase[off + ld[k]];
+                if (!(MODE & SGM_FIRST)) t.acc[s][k] = abase[off + ld[k]];
+            }
+        }
+        t.fl = flbase[clampi(j0 + min(lane, T - 1)) * pstep];
+    };
+
+    float Lp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) Lp[k] = FLT_MAX;
+
+    auto step = [&](const SgmTile<K, T>& t, int s, int j, bool start) {
+        float L[K];
+        if (start) {
+#pragma unroll
+            for (int k = 0; k < K; k++) L[k] = val[k] ? t.c[s][k] : FLT_MAX;
+        } else {
+            const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)t.fl, s);
+            const bool pen = (fl >> dir) & 1u;
+            const float P1 = pen ? p1r : p1, P2 = pen ? p2r : p2;
+            float lm = Lp[0];
+#pragma unroll
+            for (int k = 1; k < K; k++) lm = fminf(lm, Lp[k]);
+            const float m = wave_min(lm);
+            const float P1m = P1 - m;
+            const float left = dpp_shr1<K>(Lp[K - 1]);
+            const float right = dpp_shl1<K>(Lp[0]);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int d = d0 + k;
+                const float prev = (k == 0) ? left : Lp[k - 1];
+                const float next = (k == K - 1) ? right : Lp[k + 1];
+                const float S1 = Lp[k] - m;
+                const float S2 = d - 1 >= 0 ? prev + P1m : FLT_MAX;
+                const float S3 = d + 1 < D ? next + P1m : FLT_MAX;
+                const float mm = fminf(fminf(S1, S2), fminf(S3, P2));
+                L[k] = val[k] ? t.c[s][k] + mm : FLT_MAX;
+            }
+        }
+        float f[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const float prev = (MODE & SGM_FIRST) ? 0.f : t.acc[s][k];
+            f[k] = val[k] ? prev + L[k] : FLT_MAX;   // sum += Lr[num] (cpp:2046-2049)
+        }
+        if (MODE & SGM_LAST) {
+            if (a.keep_final) {
+#pragma unroll
+                for (int k = 0; k < K; k++) fp[k][j * sst[k]] = f[k];
+            }
+            float bm = f[0];
+            int bi = d0;
+#pragma unroll
+            for (int k = 1; k < K; k++)
+                if (bm > f[k]) {
+                    bm = f[k];
+                    bi = d0 + k;
+                }
+            const float wm = wave_min(bm);
+            const int widx = wave_min_i((bm == wm && d0 < D) ? bi : 0x7fffffff);
+            dacc = (lane == s) ? ((wm < FLT_MAX) ? widx : -1) : dacc;
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; k++) ap[k][j * sst[k]] = f[k];
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) Lp[k] = L[k];
+    };
+
+    auto process = [&](const SgmTile<K, T>& t, int j0) {
+        if (j0 > 0 && j0 + T <= steps) {
+#pragma unroll
+            for (int s = 0; s < T; s++) step(t, s, j0 + s, false);
+        } else {
+#pragma unroll
+            for (int s = 0; s < T; s++)
+                if (j0 + s < steps) step(t, s, j0 + s, j0 + s == 0);
+        }
+        if (MODE & SGM_LAST) {  // one store instruction per tile for the int16 disparities
+            if (lane < T && j0 + lane < steps) dbase[(j0 + lane) * pstep] = (int16_t)dacc;
+        }
+    };
+
+    SgmTile<K, T> ta, tb;
+    load(ta, 0);
+    for (int j0 = 0; j0 < steps; j0 += 2 * T) {
+        load(tb, j0 + T);
+        process(ta, j0);
+        load(ta, j0 + 2 * T);
+        process(tb, j0 + T);
+    }
+}
+
+template <int K>
+static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    const int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
+    dim3 grid((nlines + 3) / 4, n);
+    constexpr int T = K >= 8 ? 2 : 16 / K;
+    switch (mode) {
+        case SGM_FIRST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST, T>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_LAST, T>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST, T>), grid, dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_sgm<K, 0, T>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
+void launch_penalty_flags(const uint8_t* bgr, uint8_t* flags, int n, int H, int W, int thres, hipStream_t st) {
+    dim3 grid((H * W + 255) / 256, n);
+    hipLaunchKernelGGL(k_penalty_flags, grid, dim3(256), 0, st, bgr, flags, H, W, thres);
+}
+
+void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    switch (sgm_k_for(a.D)) {
+        case 1: launch_k<1>(a, mode, n, st); break;
+        case 2: launch_k<2>(a, mode, n, st); break;
+        case 3: launch_k<3>(a, mode, n, st); break;
+        case 4: launch_k<4>(a, mode, n, st); break;
+        case 6: launch_k<6>(a, mode, n, st); break;
+        case 8: launch_k<8>(a, mode, n, st); break;
+        case 12: launch_k<12>(a, mode, n, st); break;
+        default: launch_k<16>(a, mode, n, st); break;
+    }
+}
+
+}  // namespace sm

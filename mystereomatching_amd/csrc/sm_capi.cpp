@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -42,17 +43,20 @@ struct sm_ctx {
     ulonglong2* code = nullptr; // [cap][2][npix]
     float* gx = nullptr;        // [cap][2][npix]
     float* gy = nullptr;
-    uint8_t* arms = nullptr;    // [cap][2][npix][4]
+    uint8_t* arms = nullptr;    // [cap][2 views][2 planes][npix] u32: (L | R<<16), (U | D<<16)
     float* vm0 = nullptr;       // [cap][npix][D]
     float* vm1 = nullptr;       // [cap][npix][D] (right view, optional)
     float* acc = nullptr;       // [cap][npix][D]
     int16_t* disp = nullptr;    // [cap][npix]
     float* dummy = nullptr;     // 64 floats written by lanes past D
     uint8_t* flags = nullptr;   // [cap][npix] SGM colour-difference penalty bits
+    uint32_t* px = nullptr;     // [cap][2][npix] packed BGR
     int n_loaded = 0;
     int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized
     float lut_a[1024], lut_b[1024];
     float ad_oor_exp = 0;
+    bool fuse_norm_scan = false;
+    int sub_batch = 0;             // SM_SUB_BATCH=k: run sm_run in groups of k pairs (0 = all)   // SM_FUSE_NORM_SCAN=1: one sweep for norm(k) + scan(k+1)
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
@@ -136,6 +140,7 @@ sm_status validate(const sm_params& p, std::string& why) {
     auto bad = [&](const char* m) { why = m; return SM_EINVAL; };
     if (p.rows < 2 || p.cols < 2) return bad("rows and cols must be >= 2 (calGrad reads I[1] and I[w-2])");
     if ((long long)p.rows * p.cols > (1LL << 30)) return bad("rows*cols too large");
+    if (p.rows > 65535) return bad("rows must be <= 65535");
     if (p.num_disparities < 1 || p.num_disparities > 1024) return bad("num_disparities must be in [1, 1024]");
     if (p.cost_method < 0 || p.cost_method > 3) return bad("unknown cost_method");
     if (p.aggregation < 0 || p.aggregation > 1) return bad("unknown aggregation");
@@ -182,7 +187,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 }
 
 void free_all(sm_ctx* c) {
-    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms, c->vm0, c->vm1, c->acc, c->disp, c->dummy, c->flags};
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms, c->vm0, c->vm1, c->acc, c->disp, c->dummy, c->flags, c->px};
     for (void* q : ptrs)
         if (q) hipFree(q);
     for (auto& r : c->recs) {
@@ -197,34 +202,85 @@ void free_all(sm_ctx* c) {
 
 // ---- stage drivers (all asynchronous on c->st) -------------------------------------------
 
-sm_status run_prep(sm_ctx* c, int n) {
-    const sm_params& p = c->p;
-    const int H = p.rows, W = p.cols;
-    if (needs_census(p) || p.cost_method == SM_COST_CENSUS_GRAD) {
-        sm_status s = timed(c, "census_grad", (double)n * 2 * c->npix * (1 + 16 + 8), [&] {
-            sm::launch_census_grad(c->gray, c->code, c->gx, c->gy, n, H, W, p.census_rv, p.census_ru, p.census_ring, c->st);
-        });
-        if (s) return s;
-    }
-    if (needs_arms(p)) {
-        sm_status s = timed(c, "arms", (double)n * 2 * c->npix * (3 + 4), [&] {
-            sm::launch_arms(c->bgr, c->arms, n, H, W, p.arm_l, p.arm_l_out, p.arm_c_thresh, p.arm_c_thresh_out,
-                            p.arm_min_l, c->st);
-        });
-        if (s) return s;
-    }
-    return SM_OK;
+// Device pointers of pair `off` onward (the kernels index pairs from their base pointers).
+struct Bufs {
+    uint8_t* bgr;
+    uint8_t* gray;
+    ulonglong2* code;
+    float* gx;
+    float* gy;
+    uint8_t* arms;
+    float* vm0;
+    float* vm1;
+    float* acc;
+    int16_t* disp;
+    uint8_t* flags;
+    uint32_t* px;
+};
+
+Bufs at(const sm_ctx* c, int off) {
+    const size_t o = (size_t)off, np = c->npix, nv = c->nvol;
+    Bufs b;
+    b.bgr = c->bgr + o * 2 * np * 3;
+    b.gray = c->gray + o * 2 * np;
+    b.code = c->code + o * 2 * np;
+    b.gx = c->gx + o * 2 * np;
+    b.gy = c->gy + o * 2 * np;
+    b.arms = c->arms + o * 2 * 2 * np * 4;
+    b.vm0 = c->vm0 + o * nv;
+    b.vm1 = c->vm1 ? c->vm1 + o * nv : nullptr;
+    b.acc = c->acc ? c->acc + o * nv : nullptr;
+    b.disp = c->disp + o * np;
+    b.flags = c->flags + o * np;
+    b.px = c->px + o * 2 * np;
+    return b;
 }
 
-sm_status run_cost(sm_ctx* c, int n, int view) {
+sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
+    const sm_params& p = c->p;
+    const int H = p.rows, W = p.cols;
+    const bool census = needs_census(p), grad = p.cost_method == SM_COST_CENSUS_GRAD, arms = needs_arms(p);
+    const bool flags = p.optimization == SM_OPT_SGM;
+    {
+        sm::PrepArgs a{};
+        a.gray = B.gray;
+        a.bgr = B.bgr;
+        a.px = B.px;
+        a.code = B.code;
+        a.gx = B.gx;
+        a.gy = B.gy;
+        a.arms = B.arms;
+        a.flags = B.flags;
+        a.H = H;
+        a.W = W;
+        a.rv = p.census_rv;
+        a.ru = p.census_ru;
+        a.ring = p.census_ring;
+        a.L = p.arm_l;
+        a.L_out = p.arm_l_out;
+        a.C_D = p.arm_c_thresh;
+        a.C_D_out = p.arm_c_thresh_out;
+        a.minL = p.arm_min_l;
+        a.cor_thres = p.sgm_cor_dif_thres;
+        a.do_census = census;
+        a.do_grad = grad;
+        a.do_arms = arms;
+        a.do_flags = flags;
+        return timed(c, "prep", (double)n * 2 * c->npix * (1 + 3 + (census ? 16 : 0) + (grad ? 8 : 0) + (arms ? 4 : 0)) +
+                                    (flags ? (double)n * c->npix : 0),
+                     [&] { sm::launch_prep(a, n, c->st); });
+    }
+}
+
+sm_status run_cost(sm_ctx* c, int n, int view, const Bufs& B) {
     const sm_params& p = c->p;
     sm::CostArgs a{};
-    a.vm = view == 0 ? c->vm0 : c->vm1;
-    a.code = c->code;
-    a.gx = c->gx;
-    a.gy = c->gy;
-    a.arms = c->arms;
-    a.bgr = c->bgr;
+    a.vm = view == 0 ? B.vm0 : B.vm1;
+    a.code = B.code;
+    a.gx = B.gx;
+    a.gy = B.gy;
+    a.arms = B.arms;
+    a.bgr = B.bgr;
     a.H = p.rows;
     a.W = p.cols;
     a.D = p.num_disparities;
@@ -245,7 +301,7 @@ sm_status run_cost(sm_ctx* c, int n, int view) {
                  [&] { sm::launch_cost(a, m, n, c->st); });
 }
 
-sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w) {
+sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w, const Bufs& B) {
     // cbca_core (cpp:5585-5666): iteration k runs H then V for even k, V then H for odd k.
     // The last pass of iteration k and the first pass of iteration k+1 share a direction and
     // are fused into one CB_NORM_SCAN sweep, so N iterations take N + 1 sweeps.
@@ -253,9 +309,9 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w) {
     const int N = p.cbca_iterations;
     if (N <= 0) return SM_OK;
     sm::CbcaArgs a{};
-    a.vm = c->vm0;
+    a.vm = B.vm0;
     a.dummy = c->dummy;
-    a.arms = (const uint32_t*)c->arms;
+    a.arms = (const uint32_t*)B.arms;
     a.H = p.rows;
     a.W = p.cols;
     a.D = p.num_disparities;
@@ -268,9 +324,15 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w) {
     if (s) return s;
     for (int k = 0; k < N; k++) {
         const bool dir_h = (k % 2 == 1);  // direction of iteration k's second pass
-        if (k + 1 < N) {
+        if (k + 1 < N && c->fuse_norm_scan) {
             s = timed(c, dir_h ? "cbca_h_norm_scan" : "cbca_v_norm_scan", bytes,
                       [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM_SCAN, n, c->st); });
+        } else if (k + 1 < N) {
+            s = timed(c, dir_h ? "cbca_h_norm" : "cbca_v_norm", bytes,
+                      [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM, n, c->st); });
+            if (s) return s;
+            s = timed(c, dir_h ? "cbca_h_scan" : "cbca_v_scan", bytes,
+                      [&] { sm::launch_cbca(a, dir_h, sm::CB_SCAN, n, c->st); });
         } else {
             a.apply_scale = fuse_scale ? 1 : 0;
             s = timed(c, dir_h ? "cbca_h_norm" : "cbca_v_norm", bytes,
@@ -281,29 +343,25 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w) {
     return SM_OK;
 }
 
-sm_status run_scale(sm_ctx* c, int n, float w) {
+sm_status run_scale(sm_ctx* c, int n, float w, const Bufs& B) {
     return timed(c, "solve_all_scale", (double)n * c->nvol * 8.0,
-                 [&] { sm::launch_scale(c->vm0, (size_t)n * c->nvol, w, c->st); });
+                 [&] { sm::launch_scale(B.vm0, (size_t)n * c->nvol, w, c->st); });
 }
 
-sm_status run_optimize(sm_ctx* c, int n) {
+sm_status run_optimize(sm_ctx* c, int n, const Bufs& B) {
     const sm_params& p = c->p;
     if (p.optimization == SM_OPT_SGM) {
         static const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};  // cpp:6207
         static const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};  // cpp:6208
         static const char* NAMES[8] = {"sgm_path0", "sgm_path1", "sgm_path2", "sgm_path3",
                                        "sgm_path4", "sgm_path5", "sgm_path6", "sgm_path7"};
-        sm_status s0 = timed(c, "penalty_flags", (double)n * c->npix * 4, [&] {
-            sm::launch_penalty_flags(c->bgr, c->flags, n, p.rows, p.cols, p.sgm_cor_dif_thres, c->st);
-        });
-        if (s0) return s0;
         sm::SgmArgs a{};
-        a.flags = c->flags;
+        a.flags = B.flags;
         a.dummy = c->dummy;
-        a.vm = c->vm0;
-        a.acc = c->acc;
-        a.bgr = c->bgr;
-        a.disp = c->disp;
+        a.vm = B.vm0;
+        a.acc = B.acc;
+        a.bgr = B.bgr;
+        a.disp = B.disp;
         a.H = p.rows;
         a.W = p.cols;
         a.D = p.num_disparities;
@@ -326,7 +384,7 @@ sm_status run_optimize(sm_ctx* c, int n) {
         }
     } else {
         sm_status s = timed(c, "wta", (double)n * c->nvol * 4.0 + (double)n * c->npix * 2,
-                            [&] { sm::launch_wta(c->vm0, c->disp, n, p.rows, p.cols, p.num_disparities, c->st); });
+                            [&] { sm::launch_wta(B.vm0, B.disp, n, p.rows, p.cols, p.num_disparities, c->st); });
         if (s) return s;
     }
     return SM_OK;
@@ -437,7 +495,7 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->code, cap * 2 * c->npix))) return s;
     if ((s = dalloc(c, &c->gx, cap * 2 * c->npix))) return s;
     if ((s = dalloc(c, &c->gy, cap * 2 * c->npix))) return s;
-    if ((s = dalloc(c, &c->arms, cap * 2 * c->npix * 4))) return s;
+    if ((s = dalloc(c, &c->arms, cap * 2 * 2 * c->npix * 4))) return s;
     if ((s = dalloc(c, &c->vm0, cap * c->nvol))) return s;
     if (p->compute_right_view)
         if ((s = dalloc(c, &c->vm1, cap * c->nvol))) return s;
@@ -446,7 +504,14 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
     if ((s = dalloc(c, &c->dummy, 64))) return s;
     if ((s = dalloc(c, &c->flags, cap * c->npix))) return s;
+    if ((s = dalloc(c, &c->px, cap * 2 * c->npix))) return s;
     build_luts(c);
+    {
+        const char* e = getenv("SM_FUSE_NORM_SCAN");
+        c->fuse_norm_scan = e && e[0] == '1';
+        const char* sb = getenv("SM_SUB_BATCH");
+        c->sub_batch = sb ? atoi(sb) : 0;
+    }
     HIP_TRY(c, sm::upload_luts(c->lut_a, c->lut_b, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     return SM_OK;
@@ -477,10 +542,11 @@ sm_status sm_cost_calculate(sm_ctx* c) {
     if (s) return s;
     if (c->stage < 1) return fail(c, SM_ESTATE, "sm_cost_calculate before sm_set_images");
     const int n = c->n_loaded;
-    if ((s = run_prep(c, n))) return s;
-    if ((s = run_cost(c, n, 0))) return s;
-    if (c->p.compute_right_view && (s = run_cost(c, n, 1))) return s;
-    if (c->p.aggregation == SM_AGG_CBCA && (s = run_cbca(c, n, false, 1.0f))) return s;
+    const Bufs B = at(c, 0);
+    if ((s = run_prep(c, n, B))) return s;
+    if ((s = run_cost(c, n, 0, B))) return s;
+    if (c->p.compute_right_view && (s = run_cost(c, n, 1, B))) return s;
+    if (c->p.aggregation == SM_AGG_CBCA && (s = run_cbca(c, n, false, 1.0f, B))) return s;
     c->stage = 2;
     return SM_OK;
 }
@@ -492,7 +558,7 @@ sm_status sm_solve_all(sm_ctx* c, int32_t py_lev, float reg_lambda) {
     if (py_lev != 1) return fail(c, SM_EINVAL, "only PY_LEV = 1 is supported (main_.cpp:131)");
     const float m = 1 + reg_lambda;
     const float w = (float)(1. / (double)m);  // Mat::inv of the 1x1 regMat (cpp:2164)
-    if ((s = run_scale(c, c->n_loaded, w))) return s;
+    if ((s = run_scale(c, c->n_loaded, w, at(c, 0)))) return s;
     c->stage = 3;
     return SM_OK;
 }
@@ -501,7 +567,7 @@ sm_status sm_disp_optimize(sm_ctx* c, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
     if (c->stage < 2 || c->stage > 3) return fail(c, SM_ESTATE, "sm_disp_optimize must follow sm_cost_calculate / sm_solve_all");
-    if ((s = run_optimize(c, c->n_loaded))) return s;
+    if ((s = run_optimize(c, c->n_loaded, at(c, 0)))) return s;
     c->stage = 4;
     if (disp_out) return sm_download_disp(c, 1, disp_out);
     return SM_OK;
@@ -526,10 +592,15 @@ sm_status sm_get_arms(sm_ctx* c, int32_t view, uint16_t* dst) {
     if (s) return s;
     if (!dst || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
     if (c->stage < 2 || !needs_arms(c->p)) return fail(c, SM_ESTATE, "arms not computed");
-    std::vector<uint8_t> tmp(c->npix * 4);
-    HIP_TRY(c, hipMemcpyAsync(tmp.data(), c->arms + (size_t)view * c->npix * 4, c->npix * 4, hipMemcpyDeviceToHost, c->st));
+    std::vector<uint32_t> tmp(c->npix * 2);
+    HIP_TRY(c, hipMemcpyAsync(tmp.data(), c->arms + (size_t)view * 2 * c->npix * 4, c->npix * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
-    for (size_t i = 0; i < c->npix * 4; i++) dst[i] = tmp[i];
+    for (size_t i = 0; i < c->npix; i++) {
+        dst[i * 4 + 0] = tmp[i] & 0xffff;
+        dst[i * 4 + 1] = tmp[i] >> 16;
+        dst[i * 4 + 2] = tmp[c->npix + i] & 0xffff;
+        dst[i * 4 + 3] = tmp[c->npix + i] >> 16;
+    }
     return SM_OK;
 }
 
@@ -559,15 +630,22 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     if (n < 1 || n > c->n_loaded) return fail(c, SM_EINVAL, "n must be in [1, pairs uploaded]");
     const float m = 1 + reg_lambda;
     const float w = (float)(1. / (double)m);
-    if ((s = run_prep(c, n))) return s;
-    if ((s = run_cost(c, n, 0))) return s;
-    if (c->p.compute_right_view && (s = run_cost(c, n, 1))) return s;
-    if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0) {
-        if ((s = run_cbca(c, n, true, w))) return s;   // SolveAll fused into the last pass
-    } else {
-        if ((s = run_scale(c, n, w))) return s;
+    // Sub-batches: all stages of a group of pairs run back to back so that one pass's output is
+    // still in the 256 MB Infinity Cache when the next pass reads it.
+    const int g = c->sub_batch > 0 ? c->sub_batch : n;
+    for (int off = 0; off < n; off += g) {
+        const int m2 = n - off < g ? n - off : g;
+        const Bufs B = at(c, off);
+        if ((s = run_prep(c, m2, B))) return s;
+        if ((s = run_cost(c, m2, 0, B))) return s;
+        if (c->p.compute_right_view && (s = run_cost(c, m2, 1, B))) return s;
+        if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0) {
+            if ((s = run_cbca(c, m2, true, w, B))) return s;   // SolveAll fused into the last pass
+        } else {
+            if ((s = run_scale(c, m2, w, B))) return s;
+        }
+        if ((s = run_optimize(c, m2, B))) return s;
     }
-    if ((s = run_optimize(c, n))) return s;
     c->stage = 4;
     if (disp_out) return sm_download_disp(c, n, disp_out);
     return SM_OK;

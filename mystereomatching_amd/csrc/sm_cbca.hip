@@ -9,23 +9,26 @@
 //
 // gfx950 mapping.  One wave owns one (line, 64-disparity chunk); lane = disparity.  The prefix
 // sum is evaluated sequentially along the line exactly as the reference does, and its values are
-// kept in an LDS ring of 2*lag+2 slots (lag = longest arm), so each 1-D pass is ONE read and ONE
-// write of the volume (the reference: two reads, two writes and a full-volume temporary).
-// Kernel modes:
+// kept in an LDS ring, so each 1-D pass is ONE read and ONE write of the volume (the reference:
+// two reads, two writes and a full-volume temporary).  Kernel modes:
 //   CB_SCAN       first pass of an iteration:            vm <- diff(prefix(vm))
 //   CB_NORM       last pass of an iteration:             vm <- diff(prefix(vm)) / area  [* SolveAll]
 //   CB_NORM_SCAN  last pass of iteration k fused with the first pass of iteration k+1 (both run
 //                 along the same direction): two S rings, one sweep instead of two.
 // Areas are integers (< 2^16): after the first pass of an iteration the area of (p,d) is
 // tail+head+1 of that pass's intersection arms, so the normalising pass prefix-sums that value
-// modulo 2^16 next to S — no area volume is ever stored.  In CB_NORM_SCAN the same LDS word also
-// carries the position's (tail, head) so the arms are gathered once per position, not per use.
+// modulo 2^16 in a u16 ring next to S — no area volume is ever stored.
 //
-// Latency hiding: the next tile of T steps (volume values and arm words) is loaded into registers
-// while the current tile is processed (loads of step j+T are legal before the stores of step j:
-// stores trail the reads by `lag` positions).  Tiles that lie wholly in the steady state take a
-// branch-free path so the compiler can overlap LDS round trips of consecutive steps; lanes past D
-// read and write a private dummy slot instead of being masked.
+// Instruction budget (the sweeps are issue-bound at 2-3 waves per CU):
+//  * arms are stored as two u16-pair planes per pixel, (L | R<<16) and (U | D<<16), so the
+//    intersection of a pair is one v_pk_min_u16 against the uniform reference-pixel word;
+//  * in horizontal sweeps the right-image arm word of lane d at position q is A1[q - d] — the
+//    window shifts by one lane per step, so it lives in a register advanced with DPP wave_shr
+//    (lanes with q - d < 0 keep the initial 0, which is exactly the reference's zeroed tail);
+//  * ring wraps are single v_min_u32 selections; full 64-lane chunks use uniform addressing.
+// Scheduling: the next tile of T positions (volume values, arm words) is loaded while the
+// current tile is processed; inside a steady-state tile all ring writes precede all ring reads,
+// so a tile costs one or two LDS round trips.  Rings hold 2*lag + T + 1 slots.
 #include <float.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,192 +38,321 @@
 
 namespace sm {
 
-__device__ __forceinline__ uint32_t bmin4(uint32_t a, uint32_t b) {
-    uint32_t r = min(a & 0xffu, b & 0xffu);
-    r |= min(a & 0xff00u, b & 0xff00u);
-    r |= min(a & 0xff0000u, b & 0xff0000u);
-    r |= min(a & 0xff000000u, b & 0xff000000u);
-    return r;
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pkmin(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
+}
+__device__ __forceinline__ uint32_t shr1_in(uint32_t v, uint32_t in) {  // lane l <- lane l-1, lane 0 <- in
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
 }
 
-template <int T, int NSETS>
-struct CbTile {
-    float x[T];            // vm at positions j0 .. j0+T-1
-    uint32_t a0[NSETS];    // lane k < T: A0 at position (j0 + k - set offset)
-    uint32_t a1[NSETS][T]; // A1 at (position, u - d) for this lane
+template <int MODE>
+struct CbCfg {
+    static constexpr int T = MODE == CB_SCAN ? 16 : 8;  // loads + stores per tile stay < 63 (vmcnt)
+    // arm sets: 0 = pass pair at i (= j - lag), 1 = perpendicular pair at j, 2 = pass pair at j - 2 lag
+    static constexpr int NSETS = MODE == CB_SCAN ? 1 : (MODE == CB_NORM ? 2 : 3);
 };
 
-template <bool HORIZ, int MODE, int T>
-struct CbLine {
-    // set 0 = positions i (= j - lag) for SCAN/NORM; set 1 = positions j (NORM); NS uses set 0 = j
-    static constexpr int NSETS = MODE == CB_NORM ? 2 : 1;
-    using Tile = CbTile<T, NSETS>;
+__host__ __device__ inline int cbca_tile(int mode) { return mode == CB_SCAN ? CbCfg<CB_SCAN>::T : CbCfg<CB_NORM>::T; }
+// ring slots: >= 2*lag + T + 1 (a whole tile is written before any of it is read) and a multiple
+// of T (a tile's write slots never wrap)
+__host__ __device__ inline int cbca_ring(int lag, int mode) {
+    const int T = cbca_tile(mode);
+    return (2 * lag + T + 1 + T - 1) / T * T;
+}
 
-    float* lvm;               // this lane's element of the line's first pixel (or a dummy slot)
-    int lstride;              // floats between consecutive positions (0 for dummy lanes)
-    const uint32_t* A0l;      // A0 + first pixel of the line
-    const uint32_t* A1l;      // A1 + first pixel of the line
-    int pstride;              // pixels between consecutive positions
-    int line, len, lag, ring, d, lane;
+template <bool HORIZ, int T, int NSETS>
+struct CbTile {
+    float x[T];                          // vm at positions j0 .. j0+T-1
+    uint32_t a0[NSETS];                  // lane k < T: left arm pair at position (j0 + k - off)
+    uint32_t a1v[NSETS];                 // H: lane k < T: right arm pair at position (j0 + k - off)
+    uint32_t a1[HORIZ ? 1 : NSETS][T];   // V: right arm pair at (row j0 + k - off, u - d)
+};
+
+template <bool HORIZ, int MODE, bool FULL>
+struct CbLine {
+    static constexpr int T = CbCfg<MODE>::T;
+    static constexpr int NSETS = CbCfg<MODE>::NSETS;
+    using Tile = CbTile<HORIZ, T, NSETS>;
+
+    const float* xbase;       // FULL: chunk base (uniform), lane offset added; else per-lane base
+    float* obase;
+    int vstride;              // floats between consecutive positions
+    int lane;
+    const uint32_t* A0[NSETS];  // left / right arm-pair planes for each set, at the line's first pixel
+    const uint32_t* A1[NSETS];
+    int pstride, line, len, lag, ring, d;
+    int c64;                  // first disparity of the chunk
+    uint32_t vmask;           // V sweeps: all ones if u - d >= 0 else 0 (constant along the line)
+    uint32_t sh[NSETS];       // H sweeps: shifted right-arm window per set
     float S1, S2;
     uint32_t Acc;
-    int ws;
+    int ws;                   // ring slot of the tile's first position
     float* r1;
     float* r2;
-    uint32_t* ra;             // NORM: area prefix (low 16 bits); NS: area16 << 16 | tail << 8 | head
+    uint16_t* ra;
     int apply_scale;
     float scale;
 
-    __device__ __forceinline__ int set_off(int s) const {
-        if (MODE == CB_NORM_SCAN) return 0;
-        return s == 0 ? lag : 0;
-    }
+    __device__ __forceinline__ int set_off(int s) const { return s == 0 ? lag : (s == 1 ? 0 : 2 * lag); }
     __device__ __forceinline__ static int clampi(int k, int n) { return k < 0 ? 0 : (k >= n ? n - 1 : k); }
+
+    __device__ __forceinline__ float ldx(int pos) const {
+        return FULL ? xbase[clampi(pos, len) * vstride + lane] : xbase[clampi(pos, len) * vstride];
+    }
+    __device__ __forceinline__ void store(int pos, float v) const {
+        if (FULL)
+            obase[pos * vstride + lane] = v;
+        else if (d < 0x7fffffff)
+            obase[pos * vstride] = v;
+    }
+
+    // uniform base of the output row for positions pos0 .. pos0+T-1 (FULL chunks)
+    __device__ __forceinline__ float* ob_tile(int pos0) const { return FULL ? obase + (long)pos0 * vstride : obase; }
+    __device__ __forceinline__ void store_tile(float* tb, int pos0, int k, float v) const {
+        if (FULL)
+            tb[k * vstride + lane] = v;
+        else
+            store(pos0 + k, v);
+    }
 
     __device__ __forceinline__ void load(Tile& t, int j0) const {
 #pragma unroll
-        for (int k = 0; k < T; k++) t.x[k] = lvm[clampi(j0 + k, len) * lstride];
+        for (int k = 0; k < T; k++) t.x[k] = ldx(j0 + k);
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             const int base = j0 - set_off(s);
-            t.a0[s] = A0l[clampi(base + lane, len) * pstride];
+            const int ql = clampi(base + lane, len) * pstride;
+            t.a0[s] = A0[s][ql];
+            if (HORIZ) {
+                const int q = base + lane - c64;  // right pixel of lane 0 at position base + lane
+                const uint32_t v = A1[s][clampi(q, len)];
+                t.a1v[s] = (q >= 0 && q < len) ? v : 0u;
+            } else {
+#pragma unroll
+                for (int k = 0; k < T; k++) t.a1[s][k] = A1[s][clampi(base + k, len) * pstride];
+            }
+        }
+    }
+
+    // Advance every set's window to position j (call once per position, in order).
+    __device__ __forceinline__ void advance(const Tile& t, int k, int /*j*/) {
+        if (HORIZ) {
+#pragma unroll
+            for (int s = 0; s < NSETS; s++) sh[s] = shr1_in(sh[s], (uint32_t)__builtin_amdgcn_readlane((int)t.a1v[s], k));
+        }
+    }
+
+    // intersection arm pair of set s at tile position k
+    __device__ __forceinline__ uint32_t isect(const Tile& t, int s, int k) const {
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
+        const uint32_t a1 = HORIZ ? sh[s] : (t.a1[s][k] & vmask);
+        return pkmin(a0, a1);
+    }
+
+    __device__ __forceinline__ int uwrap(int s) const {  // uniform slot, any s in (-2 ring, 3 ring)
+        s = s < 0 ? s + ring : s;
+        s = s < 0 ? s + ring : s;
+        s = s >= ring ? s - ring : s;
+        return s >= ring ? s - ring : s;
+    }
+    __device__ __forceinline__ int up(int s) const { return (int)min((uint32_t)s, (uint32_t)(s - ring)); }   // s in [0, 2 ring)
+    __device__ __forceinline__ int dn(int s) const { return (int)min((uint32_t)s, (uint32_t)(s + ring)); }   // s in (-ring, ring)
+
+    __device__ __forceinline__ float finish_norm(float diff, uint32_t area) const {
+        float out = diff / (float)area;
+        if (apply_scale) {
+            float sum = 0.f;
+            sum += scale * out;
+            out = sum;
+        }
+        return out;
+    }
+
+    // ---------------- steady state: every position of the tile is inside every range ----------
+    __device__ __forceinline__ void tile_fast(const Tile& t, int j0) {
+        uint32_t pi[T], pi2[T];
+        // ring % T == 0 and ws % T == 0, so the tile's write slots ws .. ws+T-1 never wrap
+        float* w1 = r1 + ws * 64 + lane;
+        uint16_t* wa = ra + ws * 64 + lane;
+        const int si0 = uwrap(ws - lag);        // slot of i = j0 - lag
+        const int s20 = uwrap(ws - 2 * lag);    // slot of i2 = j0 - 2 lag
+        float* ob = ob_tile(j0 - lag);
+        // phase A: inputs j0 .. j0+T-1 (+ arm windows)
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            advance(t, k, j0 + k);
+            S1 = S1 + t.x[k];
+            w1[k * 64] = S1;
+            pi[k] = isect(t, 0, k);
+            if (MODE != CB_SCAN) {
+                const uint32_t pp = isect(t, 1, k);
+                Acc = Acc + (pp & 0xffffu) + (pp >> 16) + 1u;
+                wa[k * 64] = (uint16_t)Acc;
+            }
+            if (MODE == CB_NORM_SCAN) pi2[k] = isect(t, 2, k);
+        }
+        // phase B: first-stage outputs at i = j - lag (reads batched, then arithmetic)
+        float shv[T], stv[T];
+        uint32_t ahv[T], atv[T];
+        bool inner[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            const int i = j0 + k - lag;
+            const int tl = pi[k] & 0xffff, hd = pi[k] >> 16;
+            const int hs = up(si0 + k + hd);             // slot of i + head  (< 2 ring)
+            const int ts = dn(hs - (hd + tl + 1));       // slot of i - tail - 1 (window < ring)
+            inner[k] = i - tl - 1 >= 0;
+            shv[k] = r1[hs * 64 + lane];
+            stv[k] = r1[ts * 64 + lane];
+            if (MODE != CB_SCAN) {
+                ahv[k] = ra[hs * 64 + lane];
+                atv[k] = ra[ts * 64 + lane];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            const int i = j0 + k - lag;
+            const float diff = shv[k] - (inner[k] ? stv[k] : 0.f);  // == inner ? sh - st : sh
+            if (MODE == CB_SCAN) {
+                store_tile(ob, j0 - lag, k, diff);
+            } else {
+                const uint32_t area = (ahv[k] - (inner[k] ? atv[k] : 0u)) & 0xffffu;
+                if (MODE == CB_NORM) {
+                    store_tile(ob, j0 - lag, k, finish_norm(diff, area));
+                } else {
+                    const float y = diff / (float)area;          // final value of iteration k at i
+                    S2 = S2 + y;                                  // prefix of iteration k+1's first pass
+                    r2[up(si0 + k) * 64 + lane] = S2;
+                }
+            }
+        }
+        // phase C (NS): second-stage outputs at i2 = j - 2 lag
+        if (MODE == CB_NORM_SCAN) {
+            float s2h[T], s2t[T];
+            bool in2[T];
 #pragma unroll
             for (int k = 0; k < T; k++) {
-                const int q = clampi(base + k, len);
-                const int uq = HORIZ ? q : line;
-                t.a1[s][k] = A1l[q * pstride - (uq - d >= 0 ? d : uq)];  // u - d < 0 masked at use
+                const int i2 = j0 + k - 2 * lag;
+                const int tl = pi2[k] & 0xffff, hd = pi2[k] >> 16;
+                const int hs = up(s20 + k + hd);
+                in2[k] = i2 - tl - 1 >= 0;
+                s2h[k] = r2[hs * 64 + lane];
+                s2t[k] = r2[dn(hs - (hd + tl + 1)) * 64 + lane];
             }
+            float* ob2 = ob_tile(j0 - 2 * lag);
+#pragma unroll
+            for (int k = 0; k < T; k++) store_tile(ob2, j0 - 2 * lag, k, s2h[k] - (in2[k] ? s2t[k] : 0.f));
         }
+        ws = (ws + T == ring) ? 0 : ws + T;
     }
 
-    __device__ __forceinline__ uint32_t isect(const Tile& t, int s, int k, int pos) const {
-        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
-        const int u = HORIZ ? pos : line;
-        const uint32_t a1 = (u - d >= 0) ? t.a1[s][k] : 0u;   // genTrueHorVerArms: 0 once u - d < 0
-        return bmin4(a0, a1);
-    }
-
-    __device__ __forceinline__ int wrap1(int s) const { return s < 0 ? s + ring : s; }
-
-    static constexpr int TSH = HORIZ ? 0 : 16, HSH = HORIZ ? 8 : 24;
-    static constexpr int PTS = HORIZ ? 16 : 0, PHS = HORIZ ? 24 : 8;
-
-    // One position of the sweep.  G = guarded (boundary tiles): every range test is evaluated;
-    // G = false: the caller guarantees j < len, lag <= j (and 2*lag <= j for NS).
-    template <bool G>
-    __device__ __forceinline__ void step(const Tile& t, int k, int j) {
-        const int sj = ws;  // slot of position j
-        // ---- input at j
-        if (!G || j < len) {
+    // ---------------- boundary tiles: per position, every range test evaluated ----------------
+    __device__ __forceinline__ void step_guarded(const Tile& t, int k, int j) {
+        advance(t, k, j);
+        const int sj = up(ws + k);
+        if (j < len) {
             const float x = t.x[k];
-            S1 = (G && j == 0) ? x : S1 + x;
+            S1 = (j == 0) ? x : S1 + x;
             r1[sj * 64 + lane] = S1;
-            if (MODE == CB_NORM) {
-                const uint32_t is = isect(t, 1, k, j);
-                const uint32_t ain = ((is >> PTS) & 0xffu) + ((is >> PHS) & 0xffu) + 1u;
-                Acc = (G && j == 0) ? ain : Acc + ain;
-                ra[sj * 64 + lane] = Acc;
-            } else if (MODE == CB_NORM_SCAN) {
-                const uint32_t is = isect(t, 0, k, j);
-                const uint32_t ain = ((is >> PTS) & 0xffu) + ((is >> PHS) & 0xffu) + 1u;
-                Acc = (G && j == 0) ? ain : Acc + ain;
-                ra[sj * 64 + lane] = (Acc << 16) | (((is >> TSH) & 0xffu) << 8) | ((is >> HSH) & 0xffu);
+            if (MODE != CB_SCAN) {
+                const uint32_t pp = isect(t, 1, k);
+                const uint32_t ain = (pp & 0xffffu) + (pp >> 16) + 1u;
+                Acc = (j == 0) ? ain : Acc + ain;
+                ra[sj * 64 + lane] = (uint16_t)Acc;
             }
         }
-        // ---- first-stage output at i = j - lag
         const int i = j - lag;
-        if (!G || (i >= 0 && i < len)) {
-            const int si = wrap1(sj - lag);
-            int tl, hd;
-            if (MODE == CB_NORM_SCAN) {
-                const uint32_t w = ra[si * 64 + lane];
-                tl = (w >> 8) & 0xff;
-                hd = w & 0xff;
-            } else {
-                const uint32_t is = isect(t, 0, k, i);
-                tl = (is >> TSH) & 0xff;
-                hd = (is >> HSH) & 0xff;
-            }
-            const int hs2 = (si + hd >= ring) ? si + hd - ring : si + hd;  // slot of i + head
-            const int ts = wrap1(si - tl - 1);
+        if (i >= 0 && i < len) {
+            const uint32_t pr = isect(t, 0, k);
+            const int tl = pr & 0xffff, hd = pr >> 16;
+            const int si = uwrap(ws + k - lag);
+            const int hs = up(si + hd), ts = dn(si - tl - 1);
             const bool inner = i - tl - 1 >= 0;
-            const float sh = r1[hs2 * 64 + lane];
-            const float st = r1[ts * 64 + lane];
-            float out = sh - (inner ? st : 0.f);  // == inner ? sh - st : sh  (x - +0 == x)
+            const float diff = r1[hs * 64 + lane] - (inner ? r1[ts * 64 + lane] : 0.f);
             if (MODE == CB_SCAN) {
-                lvm[i * lstride] = out;
+                store(i, diff);
             } else {
-                const uint32_t ah = ra[hs2 * 64 + lane], at = ra[ts * 64 + lane];
-                const uint32_t sh16 = MODE == CB_NORM_SCAN ? 16 : 0;
-                const uint32_t area = ((ah >> sh16) - (inner ? (at >> sh16) : 0u)) & 0xffffu;
-                out = out / (float)area;
+                const uint32_t area = (ra[hs * 64 + lane] - (inner ? ra[ts * 64 + lane] : 0u)) & 0xffffu;
                 if (MODE == CB_NORM) {
-                    if (apply_scale) {
-                        float sum = 0.f;
-                        sum += scale * out;
-                        out = sum;
-                    }
-                    lvm[i * lstride] = out;
+                    store(i, finish_norm(diff, area));
                 } else {
-                    S2 = (G && i == 0) ? out : S2 + out;   // prefix of iteration k+1's first pass
+                    const float y = diff / (float)area;
+                    S2 = (i == 0) ? y : S2 + y;
                     r2[si * 64 + lane] = S2;
                 }
             }
         }
-        // ---- second-stage output at i2 = j - 2*lag (NS only)
         if (MODE == CB_NORM_SCAN) {
             const int i2 = j - 2 * lag;
-            if (!G || (i2 >= 0 && i2 < len)) {
-                int s2 = sj - 2 * lag;
-                s2 = s2 < 0 ? s2 + ring : s2;
-                const uint32_t w = ra[s2 * 64 + lane];
-                const int tl = (w >> 8) & 0xff, hd = w & 0xff;
-                const int hs = (s2 + hd >= ring) ? s2 + hd - ring : s2 + hd;
-                const int ts = wrap1(s2 - tl - 1);
-                const float sh = r2[hs * 64 + lane];
-                const float st = r2[ts * 64 + lane];
-                lvm[i2 * lstride] = sh - ((i2 - tl - 1 >= 0) ? st : 0.f);
+            if (i2 >= 0 && i2 < len) {
+                const uint32_t pr = isect(t, 2, k);
+                const int tl = pr & 0xffff, hd = pr >> 16;
+                const int s2 = uwrap(ws + k - 2 * lag);
+                const float v = r2[up(s2 + hd) * 64 + lane] - ((i2 - tl - 1 >= 0) ? r2[dn(s2 - tl - 1) * 64 + lane] : 0.f);
+                store(i2, v);
             }
         }
-        ws = (ws + 1 == ring) ? 0 : ws + 1;
     }
 
     __device__ __forceinline__ void process(const Tile& t, int j0, int nst, int fast_lo) {
-        if (j0 >= fast_lo && j0 + T <= len) {
-#pragma unroll
-            for (int k = 0; k < T; k++) step<false>(t, k, j0 + k);
+        if (j0 >= fast_lo && j0 > 0 && j0 + T <= len) {
+            tile_fast(t, j0);
         } else {
 #pragma unroll
             for (int k = 0; k < T; k++)
-                if (j0 + k < nst) step<true>(t, k, j0 + k);
+                if (j0 + k < nst) step_guarded(t, k, j0 + k);
+            ws = (ws + T == ring) ? 0 : ws + T;
         }
     }
 };
 
-template <bool HORIZ, int MODE, int T>
+template <bool HORIZ, int MODE, bool FULL>
 __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     extern __shared__ float smem[];
-    CbLine<HORIZ, MODE, T> L;
+    CbLine<HORIZ, MODE, FULL> L;
+    constexpr int T = CbCfg<MODE>::T;
+    constexpr int NSETS = CbCfg<MODE>::NSETS;
     L.lane = threadIdx.x;
     const int nchunks = (a.D + 63) >> 6;
     L.line = blockIdx.x / nchunks;
     const int chunk = blockIdx.x - L.line * nchunks;
     const int b = blockIdx.y;
     L.d = chunk * 64 + L.lane;
-    const bool valid = L.d < a.D;
     const size_t npix = (size_t)a.H * a.W;
     const size_t first_pix = HORIZ ? (size_t)L.line * a.W : (size_t)L.line;
     L.pstride = HORIZ ? 1 : a.W;
-    L.lstride = valid ? L.pstride * a.D : 0;
-    L.lvm = valid ? a.vm + ((size_t)b * npix + first_pix) * a.D + L.d : a.dummy + L.lane;
-    L.A0l = a.arms + (size_t)b * 2 * npix + first_pix;
-    L.A1l = L.A0l + npix;
+    L.vstride = L.pstride * a.D;
+    float* chunk_base = a.vm + ((size_t)b * npix + first_pix) * a.D + (size_t)chunk * 64;
+    if (FULL) {
+        L.xbase = chunk_base;
+        L.obase = chunk_base;
+    } else {
+        const bool valid = L.d < a.D;
+        L.xbase = valid ? chunk_base + L.lane : a.vm + ((size_t)b * npix + first_pix) * a.D + (a.D - 1);
+        L.obase = chunk_base + L.lane;
+        if (!valid) L.d = 0x7fffffff;  // store() skips these lanes
+    }
+    const int dl = chunk * 64 + L.lane;  // true disparity (also for masked lanes)
+    // arm planes: [b][view][plane][npix]; plane 0 = (L | R<<16), plane 1 = (U | D<<16)
+    const int pass_plane = HORIZ ? 0 : 1, perp_plane = HORIZ ? 1 : 0;
+    const uint32_t* planeL = a.arms + ((size_t)b * 4) * npix + first_pix;
+#pragma unroll
+    for (int s = 0; s < NSETS; s++) {
+        const int pl = (s == 1) ? perp_plane : pass_plane;
+        L.A0[s] = planeL + (size_t)pl * npix;
+        L.A1[s] = planeL + (size_t)(2 + pl) * npix + (HORIZ ? 0 : -(long)min(dl, L.line));
+        L.sh[s] = 0u;
+    }
+    L.vmask = (!HORIZ && L.line - dl < 0) ? 0u : 0xffffffffu;
+    L.c64 = chunk * 64;
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
-    L.ring = a.ring;
+    L.ring = cbca_ring(a.lag, MODE);
     L.r1 = smem;
-    L.r2 = smem + (size_t)a.ring * 64;
-    L.ra = (uint32_t*)(smem + (size_t)a.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
+    L.r2 = smem + (size_t)L.ring * 64;
+    L.ra = (uint16_t*)(smem + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
     L.apply_scale = a.apply_scale;
     L.scale = a.scale;
     L.S1 = L.S2 = 0.f;
@@ -228,7 +360,7 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.ws = 0;
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
     const int fast_lo = a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    typename CbLine<HORIZ, MODE, T>::Tile ta, tb;
+    typename CbLine<HORIZ, MODE, FULL>::Tile ta, tb;
     L.load(ta, 0);
     for (int j0 = 0; j0 < nst; j0 += 2 * T) {
         L.load(tb, j0 + T);
@@ -238,16 +370,23 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     }
 }
 
+size_t cbca_smem_bytes(int lag, int mode) {
+    const size_t ring = cbca_ring(lag, mode);
+    const size_t floats = mode == CB_NORM_SCAN ? 2 : 1;
+    const size_t u16s = mode == CB_SCAN ? 0 : 1;
+    return ring * 64 * (4 * floats + 2 * u16s);
+}
+
 template <bool HORIZ, int MODE>
 static void launch_mode(const CbcaArgs& a, int n, hipStream_t st) {
     const int nchunks = (a.D + 63) / 64;
     const int lines = HORIZ ? a.H : a.W;
     dim3 grid(lines * nchunks, n);
-    const int nrings = MODE == CB_SCAN ? 1 : (MODE == CB_NORM ? 2 : 3);
-    const size_t shm = (size_t)a.ring * 64 * 4 * nrings;
-    // tile depth: loads per tile (+ the tile's stores) must stay below the 6-bit vmcnt limit
-    constexpr int T = MODE == CB_NORM ? 12 : 16;
-    hipLaunchKernelGGL((k_cbca<HORIZ, MODE, T>), grid, dim3(64), shm, st, a);
+    const size_t shm = cbca_smem_bytes(a.lag, MODE);
+    if (a.D % 64 == 0)
+        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true>), grid, dim3(64), shm, st, a);
+    else
+        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false>), grid, dim3(64), shm, st, a);
 }
 
 void launch_cbca(const CbcaArgs& a, bool horiz, int mode, int n, hipStream_t st) {

@@ -11,6 +11,20 @@ enum { SGM_FIRST = 1, SGM_LAST = 2 };
 enum { CB_SCAN = 0, CB_NORM = 1, CB_NORM_SCAN = 2 };
 constexpr int CBCA_TILE = 16;  // steps of lookahead per wave in the CBCA line sweeps
 
+struct PrepArgs {
+    const uint8_t* gray;        // [n][2][H][W]
+    const uint8_t* bgr;         // [n][2][H][W][3]
+    uint32_t* px;               // [n][2][H][W] packed BGR (written by the pack pass)
+    ulonglong2* code;           // [n][2][H][W]
+    float* gx;
+    float* gy;
+    uint8_t* arms;              // [n][2][H][W][4]
+    uint8_t* flags;             // [n][H][W] (left view only)
+    int H, W, rv, ru, ring;
+    int L, L_out, C_D, C_D_out, minL, cor_thres;
+    int do_census, do_grad, do_arms, do_flags;
+};
+
 struct CostArgs {
     float* vm;                  // [n][H][W][D] destination (view's volume)
     const ulonglong2* code;     // [n][2][H][W]
@@ -50,15 +64,12 @@ struct SgmArgs {
 };
 
 hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st);
-void launch_census_grad(const uint8_t* gray, ulonglong2* code, float* gx, float* gy, int n, int H, int W, int rv,
-                        int ru, int ring, hipStream_t st);
-void launch_arms(const uint8_t* bgr, uint8_t* arms, int n, int H, int W, int L, int L_out, int C_D, int C_D_out,
-                 int minL, hipStream_t st);
 void launch_cost(const CostArgs& a, int method, int n, hipStream_t st);
+void launch_prep(const PrepArgs& a, int n, hipStream_t st);
+size_t prep_smem_bytes(int rv, int ru, int L_out);
 void launch_cbca(const CbcaArgs& a, bool horiz, int mode, int n, hipStream_t st);
 void launch_scale(float* vm, size_t n, float w, hipStream_t st);
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st);
-void launch_penalty_flags(const uint8_t* bgr, uint8_t* flags, int n, int H, int W, int thres, hipStream_t st);
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);
 float expf_host(float x);

@@ -26,203 +26,331 @@ __constant__ float c_lut_b[1024];
 __device__ inline float dev_expf(float x) { return expf_glibc(x, c_exp_tab); }
 
 // ---------------------------------------------------------------------------------------
-// K0a: census codes + x/y gradients for both views of every pair; one thread per pixel.
-// genCensusCode_NC_Sur (h:867-934): MSB-first bit stream, flush when step > 63.
-// calGrad / calGrad_y single-channel branches (cpp:271-287, 320-350).
+// K0: fused per-pixel prep for one view: census code, x/y gradients, cross arms and (left view)
+// the SGM colour-difference penalty flags, from LDS tiles.  Block = 64 x 16 pixels, 256 threads
+// (4 pixels each).  Gray tile with the census halo (REFLECT_101 applied while filling it, as
+// copyMakeBorder does, h:870-871); packed-BGR tile with an L_out halo for the arm walks
+// (out-of-image tile entries are never read: the walk stops at the border first).
 // ---------------------------------------------------------------------------------------
-__global__ void k_census_grad(const uint8_t* __restrict__ gray, ulonglong2* __restrict__ code,
-                              float* __restrict__ gx, float* __restrict__ gy, int H, int W, int rv,
-                              int ru, int ring, int views_per_pair) {
-    const int npix = H * W;
-    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pix >= npix) return;
-    const int view = blockIdx.y;  // 0 left, 1 right
-    const int b = blockIdx.z;
-    const uint8_t* I = gray + ((size_t)b * 2 + view) * npix;
-    const int v = pix / W, u = pix - v * W;
-    const int c = I[pix];
-    uint64_t w[2] = {0, 0};
-    uint64_t cs = 0;
-    int step = 0, dep = 0;
-    for (int dv = -rv; dv <= rv; dv++) {
-        const uint8_t* row = I + (size_t)reflect101(v + dv, H) * W;
-        for (int du = -ru; du <= ru; du++) {
-            if (step > 63) {
-                w[dep & 1] = cs;
-                cs = 0;
-                step = 0;
-                dep++;
-            }
-            cs <<= 1;
-            if (c - (int)row[reflect101(u + du, W)] < 0) cs++;
-            step++;
-        }
-    }
-    if (ring) {
-        const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
-        const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
-        for (int i = 0; i < 8; i++) {
-            int pre = I[(size_t)reflect101(v + dvs[i], H) * W + reflect101(u + dus[i], W)];
-            int aft = I[(size_t)reflect101(v + dvs[i + 1], H) * W + reflect101(u + dus[i + 1], W)];
-            if (step > 63) {
-                w[dep & 1] = cs;
-                cs = 0;
-                step = 0;
-                dep++;
-            }
-            cs <<= 1;
-            if (pre - aft < 0) cs++;
-            step++;
-        }
-    }
-    if (step > 0) w[dep & 1] = cs;
-    const size_t o = ((size_t)b * views_per_pair + view) * npix + pix;
-    code[o] = make_ulonglong2(w[0], w[1]);
-    // gradients (edges: full difference; interior: 0.5 * central difference, exact in f32)
-    const uint8_t* r = I + (size_t)v * W;
-    float g;
-    if (u == 0)
-        g = (float)(r[1] - r[0]);
-    else if (u == W - 1)
-        g = (float)(r[W - 1] - r[W - 2]);
-    else
-        g = 0.5f * (float)(r[u + 1] - r[u - 1]);
-    gx[o] = g;
-    if (v == 0)
-        g = (float)(I[W + u] - I[u]);
-    else if (v == H - 1)
-        g = (float)(I[(size_t)(H - 1) * W + u] - I[(size_t)(H - 2) * W + u]);
-    else
-        g = 0.5f * (float)(I[(size_t)(v + 1) * W + u] - I[(size_t)(v - 1) * W + u]);
-    gy[o] = g;
+constexpr int PREP_TX = 64, PREP_TY = 16;
+
+__device__ __forceinline__ bool color_ok_packed(uint32_t x, uint32_t y, int t) {
+    return abs((int)(x & 0xff) - (int)(y & 0xff)) <= t && abs((int)((x >> 8) & 0xff) - (int)((y >> 8) & 0xff)) <= t &&
+           abs((int)(x >> 16) - (int)(y >> 16)) <= t;
+}
+__device__ __forceinline__ int color_d1(uint32_t x, uint32_t y) {
+    return max(max(abs((int)(x & 0xff) - (int)(y & 0xff)), abs((int)((x >> 8) & 0xff) - (int)((y >> 8) & 0xff))),
+               abs((int)(x >> 16) - (int)(y >> 16)));
 }
 
-// ---------------------------------------------------------------------------------------
-// K0b: cross arms (calHorVerDis 7-arg, cpp:2959-3050); one thread per (pixel, direction).
-// ---------------------------------------------------------------------------------------
-__device__ inline bool color_ok(const uint8_t* a, const uint8_t* b, int t) {
-    return abs((int)a[0] - (int)b[0]) <= t && abs((int)a[1] - (int)b[1]) <= t && abs((int)a[2] - (int)b[2]) <= t;
+// BGR bytes -> one packed u32 per pixel (B | G << 8 | R << 16) for every view of every pair.
+__global__ void k_pack_bgr(const uint8_t* __restrict__ bgr, uint32_t* __restrict__ px, size_t total) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const uint8_t* p = bgr + i * 3;
+        px[i] = p[0] | (p[1] << 8) | (p[2] << 16);
+    }
 }
 
-__global__ void k_arms(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ arms, int H, int W, int L,
-                       int L_out, int C_D, int C_D_out, int minL) {
-    const int npix = H * W;
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= npix * 4) return;
-    const int pix = t >> 2, direc = t & 3;
-    const int view = blockIdx.y, b = blockIdx.z;
-    const uint8_t* I = bgr + ((size_t)b * 2 + view) * npix * 3;
-    const int v = pix / W, u = pix - v * W;
-    const int du = direc == 0 ? -1 : (direc == 1 ? 1 : 0);
-    const int dv = direc == 2 ? -1 : (direc == 3 ? 1 : 0);
-    const uint8_t* IPtr = I + (size_t)pix * 3;
-    int arm = 1;
-    for (; arm <= L_out; arm++) {
-        int va = v + arm * dv, ua = u + arm * du;
-        if (va < 0 || va >= H || ua < 0 || ua >= W) break;
-        const uint8_t* ap = I + ((size_t)va * W + ua) * 3;
-        const uint8_t* pp = ap - (dv * W + du) * 3;
-        bool nb = color_ok(ap, pp, C_D);
-        bool ip = color_ok(IPtr, ap, arm <= L ? C_D : C_D_out);
-        if (!nb || !ip) break;
-    }
-    int out = 0;
-    if (--arm >= minL)
-        out = arm;
-    else {
-        for (int len = minL; len >= 0; len--)
-            if (u + len * du >= 0 && u + len * du <= W - 1 && v + len * dv >= 0 && v + len * dv <= H - 1) {
-                out = len;
-                break;
-            }
-    }
-    arms[(((size_t)b * 2 + view) * npix + pix) * 4 + direc] = (uint8_t)out;
-}
-
-// ---------------------------------------------------------------------------------------
-// K1: cost volume.  One thread per (pixel, d) element; consecutive threads = consecutive d, so
-// the f32 volume write is fully coalesced.  view 0: pairs (u, u-d); view 1: (u+d, u).
-//   census  gen_cenVM_XOR (h:936-981); grad calgradvm (cpp:388-455);
-//   AD      gen_ad_sd_vm (cpp:2468-2509);   fusion gen_vm_from2vm_exp (cpp:3566-3590).
-// The census term exp(-C/lam) (C integer 0..71) and the AD term exp(-AD/lam) (AD = s/3,
-// s integer 0..765) come from host-built LUTs of libm expf; only the gradient term needs
-// sm::dev_expf.
-// ---------------------------------------------------------------------------------------
-template <int METHOD>
-__global__ void k_cost(const CostArgs a) {
-    const size_t nvol = (size_t)a.H * a.W * a.D;
-    const int b = blockIdx.y;
-    const size_t npix = (size_t)a.H * a.W;
-    float* out = a.vm + (size_t)b * nvol;
-    const int lc = a.view == 1 ? 1 : 0, rc = a.view == 1 ? 0 : 1;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < nvol; e += (size_t)gridDim.x * blockDim.x) {
-        const int pix = (int)(e / a.D);
-        const int d = (int)(e - (size_t)pix * a.D);
-        const int v = pix / a.W, u = pix - v * a.W;
-        const int lp = u + d * lc, rp = u - d * rc;
-        const bool oor = lp >= a.W || rp < 0;
-        const size_t rowb = (size_t)v * a.W;
-        float cen = 0.f;
-        if (METHOD != SM_M_AD) {
-            if (oor)
-                cen = a.census_default;
-            else {
-                const ulonglong2 cl = a.code[((size_t)b * 2 + 0) * npix + rowb + lp];
-                const ulonglong2 cr = a.code[((size_t)b * 2 + 1) * npix + rowb + rp];
-                float cost = 0;
-                cost += (float)__popcll(cl.x ^ cr.x);
-                if (a.nwords > 1) cost += (float)__popcll(cl.y ^ cr.y);
-                cen = fminf(cost, a.census_default);
-            }
+__global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
+    extern __shared__ __align__(16) unsigned char prep_raw[];
+    const int H = a.H, W = a.W, rv = a.rv, ru = a.ru, Lo = a.L_out;
+    const int u0 = blockIdx.x * PREP_TX, v0 = blockIdx.y * PREP_TY;
+    const int b = blockIdx.z >> 1, view = blockIdx.z & 1;
+    const size_t npix = (size_t)H * W;
+    const size_t img = (size_t)b * 2 + view;
+    const uint8_t* G = a.gray + img * npix;
+    const uint32_t* P = a.px + img * npix;
+    // gray tile: rows v0-hv .. v0+TY+hv, cols u0-hu .. u0+TX+hu, REFLECT_101 applied on fill
+    const int hv = max(rv, 1), hu = max(ru, 1);
+    const int gw = PREP_TX + 2 * hu, gh = PREP_TY + 2 * hv;
+    uint8_t* gt = prep_raw;
+    const int tid = threadIdx.x;
+    if (a.do_census || a.do_grad) {
+        for (int i = tid; i < gw * gh; i += 256) {
+            const int ty = i / gw, tx = i - ty * gw;
+            const int vv = reflect101(v0 - hv + ty, H), uu = reflect101(u0 - hu + tx, W);
+            gt[i] = G[(size_t)vv * W + uu];
         }
-        float res;
-        if (METHOD == SM_M_CENSUS) {
-            res = cen;
-        } else if (METHOD == SM_M_CENSUS_GRAD) {
-            float g;
-            if (oor)
-                g = a.grad_oor;
-            else {
-                const uint8_t* arm = a.arms + (((size_t)b * 2 + a.view) * npix + pix) * 4;
-                float sH = (float)min(arm[0], arm[1]);
-                float sV = (float)min(arm[2], arm[3]);
-                if (sH == 0) sH = 1;
-                if (sV == 0) sV = 1;
-                const float wa = sH / (sH + sV);
-                const size_t o0 = ((size_t)b * 2 + 0) * npix + rowb + lp;
-                const size_t o1 = ((size_t)b * 2 + 1) * npix + rowb + rp;
-                const float dx = fminf(fabsf(a.gx[o0] - a.gx[o1]), a.grad_trunc);
-                const float dy = fminf(fabsf(a.gy[o0] - a.gy[o1]), a.grad_trunc);
-                if (a.grad_adaptive) {
-                    const float t1 = wa * dx;
-                    const float t2 = (1.0f - wa) * dy;
-                    g = t1 + t2;
-                } else {
-                    g = dx + dy;
+    }
+    __syncthreads();
+    const int x = tid & 63;
+    for (int yy = tid >> 6; yy < PREP_TY; yy += 4) {
+        const int u = u0 + x, v = v0 + yy;
+        if (u >= W || v >= H) continue;
+        const size_t o = img * npix + (size_t)v * W + u;
+        // census (genCensusCode_NC_Sur, h:867-934)
+        if (a.do_census) {
+            const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
+            const int c = g[0];
+            uint64_t w[2] = {0, 0};
+            uint64_t cs = 0;
+            int step = 0, dep = 0;
+            for (int dv = -rv; dv <= rv; dv++)
+                for (int du = -ru; du <= ru; du++) {
+                    if (step > 63) {
+                        w[dep & 1] = cs;
+                        cs = 0;
+                        step = 0;
+                        dep++;
+                    }
+                    cs <<= 1;
+                    if (c - (int)g[dv * gw + du] < 0) cs++;
+                    step++;
+                }
+            if (a.ring) {
+                const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
+                const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int pre = g[dvs[i] * gw + dus[i]], aft = g[dvs[i + 1] * gw + dus[i + 1]];
+                    if (step > 63) {
+                        w[dep & 1] = cs;
+                        cs = 0;
+                        step = 0;
+                        dep++;
+                    }
+                    cs <<= 1;
+                    if (pre - aft < 0) cs++;
+                    step++;
                 }
             }
-            const float e0 = c_lut_a[(int)cen];                 // expf(-C / lamCen)
-            const float e1 = dev_expf(-g / a.lam2);             // expf(-G / lamG)
-            const float t = 2.0f - e0;
-            res = t - e1;
-        } else {  // AD-based: AD = min(s/3, trunc), s = sum_c |L_c - R_c| (integer)
-            int s = 0;
-            if (!oor) {
-                const uint8_t* L = a.bgr + (((size_t)b * 2 + 0) * npix + rowb + lp) * 3;
-                const uint8_t* R = a.bgr + (((size_t)b * 2 + 1) * npix + rowb + rp) * 3;
-                s = abs((int)L[0] - (int)R[0]) + abs((int)L[1] - (int)R[1]) + abs((int)L[2] - (int)R[2]);
+            if (step > 0) w[dep & 1] = cs;
+            a.code[o] = make_ulonglong2(w[0], w[1]);
+        }
+        // gradients (calGrad / calGrad_y single-channel, cpp:271-350); the one-sided border
+        // differences only touch interior rows/cols, so the reflected halo never enters them
+        if (a.do_grad) {
+            const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
+            float gxv, gyv;
+            if (u == 0)
+                gxv = (float)(g[1] - g[0]);
+            else if (u == W - 1)
+                gxv = (float)(g[0] - g[-1]);
+            else
+                gxv = 0.5f * (float)(g[1] - g[-1]);
+            if (v == 0)
+                gyv = (float)(g[gw] - g[0]);
+            else if (v == H - 1)
+                gyv = (float)(g[0] - g[-gw]);
+            else
+                gyv = 0.5f * (float)(g[gw] - g[-gw]);
+            a.gx[o] = gxv;
+            a.gy[o] = gyv;
+        }
+        const uint32_t* pc = P + (size_t)v * W + u;
+        // cross arms (calHorVerDis 7-arg, cpp:2959-3050), direction order L, R, U, D; the walks
+        // read the packed image (lanes = consecutive pixels, so every step is one coalesced load)
+        if (a.do_arms) {
+            const uint32_t center = pc[0];
+            uint32_t packed = 0;
+#pragma unroll
+            for (int direc = 0; direc < 4; direc++) {
+                const int du = direc == 0 ? -1 : (direc == 1 ? 1 : 0);
+                const int dv = direc == 2 ? -1 : (direc == 3 ? 1 : 0);
+                const int off = dv * W + du;
+                int arm = 1;
+                uint32_t prev = center;
+                for (; arm <= Lo; arm++) {
+                    const int va = v + arm * dv, ua = u + arm * du;
+                    if (va < 0 || va >= H || ua < 0 || ua >= W) break;
+                    const uint32_t cur = pc[arm * off];
+                    const bool nb = color_ok_packed(cur, prev, a.C_D);
+                    const bool ip = color_ok_packed(center, cur, arm <= a.L ? a.C_D : a.C_D_out);
+                    if (!nb || !ip) break;
+                    prev = cur;
+                }
+                int outv = 0;
+                if (--arm >= a.minL)
+                    outv = arm;
+                else {
+                    for (int len = a.minL; len >= 0; len--)
+                        if (u + len * du >= 0 && u + len * du <= W - 1 && v + len * dv >= 0 && v + len * dv <= H - 1) {
+                            outv = len;
+                            break;
+                        }
+                }
+                packed |= (uint32_t)outv << (8 * direc);
             }
-            if (METHOD == SM_M_AD) {
-                res = oor ? a.ad_trunc : fminf((float)s / 3.0f, a.ad_trunc);
-            } else {  // ADCensus: 2 - exp(-AD/lamAD) - exp(-C/lamC); AD trunc 1000 > 255 never binds
-                const float e0 = oor ? a.ad_oor_exp : c_lut_b[s];
-                const float e1 = c_lut_a[(int)cen];
+            // two u16-pair planes: (L | R << 16) and (U | D << 16)
+            uint32_t* planes = (uint32_t*)a.arms + img * 2 * npix + (size_t)v * W + u;
+            planes[0] = (packed & 0xffu) | ((packed >> 8 & 0xffu) << 16);
+            planes[npix] = (packed >> 16 & 0xffu) | ((packed >> 24) << 16);
+        }
+        // SGM penalty flags of the left image (updateCost, h:2223-2229)
+        if (a.do_flags && view == 0) {
+            const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};
+            const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};
+            const uint32_t c0 = pc[0];
+            uint32_t f = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int vv = v + RV[i], uu = u + RU[i];
+                if (vv < 0 || vv >= H || uu < 0 || uu >= W) continue;
+                if (color_d1(c0, pc[RV[i] * W + RU[i]]) > a.cor_thres) f |= 1u << i;
+            }
+            a.flags[(size_t)b * npix + (size_t)v * W + u] = (uint8_t)f;
+        }
+    }
+}
+
+size_t prep_smem_bytes(int rv, int ru, int L_out) {
+    const int hv = rv > 1 ? rv : 1, hu = ru > 1 ? ru : 1;
+    (void)L_out;
+    return (size_t)(PREP_TX + 2 * hu) * (PREP_TY + 2 * hv);
+}
+
+void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
+    const size_t total = (size_t)n * 2 * a.H * a.W;
+    size_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_pack_bgr, dim3((unsigned)blocks), dim3(256), 0, st, a.bgr, a.px, total);
+    dim3 grid((a.W + PREP_TX - 1) / PREP_TX, (a.H + PREP_TY - 1) / PREP_TY, 2 * n);
+    hipLaunchKernelGGL(k_prep, grid, dim3(256), prep_smem_bytes(a.rv, a.ru, a.L_out), st, a);
+}
+
+// ---------------------------------------------------------------------------------------
+// K1: cost volume of one view.  Block = one row segment of P pixels x all D disparities.
+// The "fixed" pixel is (v,u) of image `view`; its candidate ("moving") pixel is (v, u - d) in
+// the right image for view 0 and (v, u + d) in the left image for view 1.  Per-pixel inputs of
+// the P fixed and P + D - 1 moving pixels are staged in LDS once, then each wave writes D
+// contiguous floats of one pixel (coalesced).
+//   census  gen_cenVM_XOR (h:936-981); grad calgradvm (cpp:388-455);
+//   AD      gen_ad_sd_vm (cpp:2468-2509);   fusion gen_vm_from2vm_exp (cpp:3566-3590).
+// exp(-C/lam) (C integer 0..128) and exp(-AD/lam) (AD = s/3, s integer 0..765) come from LUTs
+// built on the host with libm expf; the gradient term uses sm::dev_expf, skipped when
+// -G/lamG < -17.5: then expf(-G/lamG) <= 2^-25 and fl(t - e) == t for every t = fl(2 - e0) in
+// [1, 2), so the result is bit-identical without evaluating it.
+// ---------------------------------------------------------------------------------------
+constexpr int COST_P = 32;
+
+template <int METHOD>
+__global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
+    extern __shared__ __align__(16) unsigned char cs_raw[];
+    const int D = a.D, W = a.W;
+    const int u0 = blockIdx.x * COST_P, v = blockIdx.y, b = blockIdx.z;
+    const int np = min(COST_P, W - u0);
+    const int nm = np + D - 1;                      // moving pixels needed
+    const int sgn = a.view == 0 ? 1 : -1;           // moving position = u - sgn * d
+    const int mbase = a.view == 0 ? u0 - (D - 1) : u0;
+    const size_t npix = (size_t)a.H * W;
+    const int fview = a.view, mview = 1 - a.view;
+    const size_t frow = ((size_t)b * 2 + fview) * npix + (size_t)v * W;
+    const size_t mrow = ((size_t)b * 2 + mview) * npix + (size_t)v * W;
+    // LDS carve-up
+    ulonglong2* fcode = (ulonglong2*)cs_raw;                 // [P]
+    ulonglong2* mcode = fcode + COST_P;                      // [P + D - 1]
+    float* fgx = (float*)(mcode + (COST_P + D - 1));         // [P]
+    float* fgy = fgx + COST_P;
+    float* fwa = fgy + COST_P;                               // adaptive weight a
+    float* fwb = fwa + COST_P;                               // 1 - a
+    float* mgx = fwb + COST_P;                               // [P + D - 1]
+    float* mgy = mgx + (COST_P + D - 1);
+    uint32_t* fbgr = (uint32_t*)(mgy + (COST_P + D - 1));    // [P]
+    uint32_t* mbgr = fbgr + COST_P;                          // [P + D - 1]
+    const int tid = threadIdx.y * 64 + threadIdx.x;
+    for (int i = tid; i < np; i += 256) {
+        const int u = u0 + i;
+        if (METHOD != SM_M_AD) fcode[i] = a.code[frow + u];
+        if (METHOD == SM_M_CENSUS_GRAD) {
+            fgx[i] = a.gx[frow + u];
+            fgy[i] = a.gy[frow + u];
+            const uint32_t* planes = (const uint32_t*)a.arms + ((size_t)b * 2 + fview) * 2 * npix + (size_t)v * W + u;
+            const uint32_t ph = planes[0], pv = planes[npix];
+            float sH = (float)min(ph & 0xffffu, ph >> 16);
+            float sV = (float)min(pv & 0xffffu, pv >> 16);
+            if (sH == 0) sH = 1;
+            if (sV == 0) sV = 1;
+            const float wa = sH / (sH + sV);
+            fwa[i] = wa;
+            fwb[i] = 1.0f - wa;
+        }
+        if (METHOD == SM_M_AD || METHOD == SM_M_AD_CENSUS) {
+            const uint8_t* p = a.bgr + (frow + u) * 3;
+            fbgr[i] = p[0] | (p[1] << 8) | (p[2] << 16);
+        }
+    }
+    for (int i = tid; i < nm; i += 256) {
+        const int q = mbase + i;
+        if (q < 0 || q >= W) continue;
+        if (METHOD != SM_M_AD) mcode[i] = a.code[mrow + q];
+        if (METHOD == SM_M_CENSUS_GRAD) {
+            mgx[i] = a.gx[mrow + q];
+            mgy[i] = a.gy[mrow + q];
+        }
+        if (METHOD == SM_M_AD || METHOD == SM_M_AD_CENSUS) {
+            const uint8_t* p = a.bgr + (mrow + q) * 3;
+            mbgr[i] = p[0] | (p[1] << 8) | (p[2] << 16);
+        }
+    }
+    __syncthreads();
+    float* out = a.vm + ((size_t)b * npix + (size_t)v * W + u0) * D;
+    for (int pl = threadIdx.y; pl < np; pl += 4) {
+        const int u = u0 + pl;
+        const ulonglong2 cf = (METHOD != SM_M_AD) ? fcode[pl] : make_ulonglong2(0, 0);
+        for (int d = threadIdx.x; d < D; d += 64) {
+            const int q = u - sgn * d;                 // moving position
+            const bool oor = q < 0 || q >= W;
+            const int mi = q - mbase;
+            float cen = 0.f;
+            if (METHOD != SM_M_AD) {
+                if (oor)
+                    cen = a.census_default;
+                else {
+                    const ulonglong2 cm = mcode[mi];
+                    float cost = 0;
+                    cost += (float)__popcll(cf.x ^ cm.x);
+                    if (a.nwords > 1) cost += (float)__popcll(cf.y ^ cm.y);
+                    cen = fminf(cost, a.census_default);
+                }
+            }
+            float res;
+            if (METHOD == SM_M_CENSUS) {
+                res = cen;
+            } else if (METHOD == SM_M_CENSUS_GRAD) {
+                float g;
+                if (oor)
+                    g = a.grad_oor;
+                else {
+                    const float dx = fminf(fabsf(fgx[pl] - mgx[mi]), a.grad_trunc);
+                    const float dy = fminf(fabsf(fgy[pl] - mgy[mi]), a.grad_trunc);
+                    if (a.grad_adaptive) {
+                        const float t1 = fwa[pl] * dx;
+                        const float t2 = fwb[pl] * dy;
+                        g = t1 + t2;
+                    } else {
+                        g = dx + dy;
+                    }
+                }
+                const float e0 = c_lut_a[(int)cen];       // expf(-C / lamCen)
+                const float xg = -g / a.lam2;
+                float e1 = 0.f;
+                if (xg >= -17.5f) e1 = dev_expf(xg);      // expf(-G / lamG)
                 const float t = 2.0f - e0;
                 res = t - e1;
+            } else {
+                int s = 0;
+                if (!oor) {
+                    const uint32_t x = fbgr[pl], y = mbgr[mi];
+                    s = abs((int)(x & 0xff) - (int)(y & 0xff)) + abs((int)((x >> 8) & 0xff) - (int)((y >> 8) & 0xff)) +
+                        abs((int)(x >> 16) - (int)(y >> 16));
+                }
+                if (METHOD == SM_M_AD) {
+                    res = oor ? a.ad_trunc : fminf((float)s / 3.0f, a.ad_trunc);
+                } else {
+                    const float e0 = oor ? a.ad_oor_exp : c_lut_b[s];
+                    const float e1 = c_lut_a[(int)cen];
+                    const float t = 2.0f - e0;
+                    res = t - e1;
+                }
             }
+            out[(size_t)pl * D + d] = res;
         }
-        out[e] = res;
     }
+}
+
+size_t cost_smem_bytes(int D) {
+    const size_t nm = COST_P + D - 1;
+    return 16 * (COST_P + nm) + 4 * (4 * COST_P + 2 * nm) + 4 * (COST_P + nm);
 }
 
 // SolveAll with PY_LVL = 1 as a standalone pass (used by the reference-ordered API):
@@ -272,28 +400,15 @@ hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st) {
     return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut_b), lut_b, sizeof(float) * 1024, 0, hipMemcpyHostToDevice, st);
 }
 
-void launch_census_grad(const uint8_t* gray, ulonglong2* code, float* gx, float* gy, int n, int H, int W, int rv,
-                        int ru, int ring, hipStream_t st) {
-    dim3 grid((H * W + 255) / 256, 2, n);
-    hipLaunchKernelGGL(k_census_grad, grid, dim3(256), 0, st, gray, code, gx, gy, H, W, rv, ru, ring, 2);
-}
-
-void launch_arms(const uint8_t* bgr, uint8_t* arms, int n, int H, int W, int L, int L_out, int C_D, int C_D_out,
-                 int minL, hipStream_t st) {
-    dim3 grid((H * W * 4 + 255) / 256, 2, n);
-    hipLaunchKernelGGL(k_arms, grid, dim3(256), 0, st, bgr, arms, H, W, L, L_out, C_D, C_D_out, minL);
-}
-
 void launch_cost(const CostArgs& a, int method, int n, hipStream_t st) {
-    const size_t nvol = (size_t)a.H * a.W * a.D;
-    size_t blocks = (nvol + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    dim3 grid((unsigned)blocks, n);
+    dim3 grid((a.W + COST_P - 1) / COST_P, a.H, n);
+    dim3 block(64, 4);
+    const size_t shm = cost_smem_bytes(a.D);
     switch (method) {
-        case SM_M_CENSUS_GRAD: hipLaunchKernelGGL(k_cost<SM_M_CENSUS_GRAD>, grid, dim3(256), 0, st, a); break;
-        case SM_M_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_CENSUS>, grid, dim3(256), 0, st, a); break;
-        case SM_M_AD_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_AD_CENSUS>, grid, dim3(256), 0, st, a); break;
-        default: hipLaunchKernelGGL(k_cost<SM_M_AD>, grid, dim3(256), 0, st, a); break;
+        case SM_M_CENSUS_GRAD: hipLaunchKernelGGL(k_cost<SM_M_CENSUS_GRAD>, grid, block, shm, st, a); break;
+        case SM_M_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_CENSUS>, grid, block, shm, st, a); break;
+        case SM_M_AD_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_AD_CENSUS>, grid, block, shm, st, a); break;
+        default: hipLaunchKernelGGL(k_cost<SM_M_AD>, grid, block, shm, st, a); break;
     }
 }
 

@@ -16,7 +16,7 @@
 // accumulate into one sum volume: path 0 writes acc = 0 + L0, middle paths acc += Li, and the
 // last path adds its Li, takes the WTA in registers and writes only the int16 disparity (and the
 // summed volume when the caller asks for it).  The next T steps of C and acc are prefetched into
-// registers; the colour-difference penalty flags of every pixel are precomputed once per pair.
+// registers; the colour-difference penalty flags of every pixel come from the prep kernel.
 #include <float.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,32 +25,6 @@
 #include "sm_kernels.h"
 
 namespace sm {
-
-__constant__ int c_rv[8] = {+1, -1, 0, 0, +1, +1, -1, -1};
-__constant__ int c_ru[8] = {0, 0, +1, -1, -1, +1, +1, -1};
-
-// bit i of flags(p) = (D1 between p and p + r_i > cor_thres), left colour image (updateCost
-// leftFirst branch, h:2223-2229).  One thread per pixel.
-__global__ void k_penalty_flags(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ flags, int H, int W,
-                                int thres) {
-    const int npix = H * W;
-    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pix >= npix) return;
-    const int b = blockIdx.y;
-    const uint8_t* I = bgr + (size_t)b * 2 * npix * 3;
-    const int v = pix / W, u = pix - v * W;
-    const uint8_t* q0 = I + (size_t)pix * 3;
-    uint32_t f = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int vv = v + c_rv[i], uu = u + c_ru[i];
-        if (vv < 0 || vv >= H || uu < 0 || uu >= W) continue;
-        const uint8_t* q1 = I + ((size_t)vv * W + uu) * 3;
-        const int D1 = max(max(abs((int)q0[0] - (int)q1[0]), abs((int)q0[1] - (int)q1[1])), abs((int)q0[2] - (int)q1[2]));
-        if (D1 > thres) f |= 1u << i;
-    }
-    flags[(size_t)b * npix + pix] = (uint8_t)f;
-}
 
 template <int K>
 __device__ __forceinline__ float dpp_shr1(float v) {  // lane l <- lane l-1; lane 0 <- FLT_MAX
@@ -246,11 +220,6 @@ static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
         case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST, T>), grid, dim3(256), 0, st, a); break;
         default: hipLaunchKernelGGL((k_sgm<K, 0, T>), grid, dim3(256), 0, st, a); break;
     }
-}
-
-void launch_penalty_flags(const uint8_t* bgr, uint8_t* flags, int n, int H, int W, int thres, hipStream_t st) {
-    dim3 grid((H * W + 255) / 256, n);
-    hipLaunchKernelGGL(k_penalty_flags, grid, dim3(256), 0, st, bgr, flags, H, W, thres);
 }
 
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {

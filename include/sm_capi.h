@@ -108,11 +108,13 @@ SM_API sm_status sm_disp_optimize(sm_ctx* ctx, int16_t* disp_out);
 SM_API sm_status sm_get_volume(sm_ctx* ctx, int32_t view, float* dst);   /* H*W*D floats */
 SM_API sm_status sm_get_arms(sm_ctx* ctx, int32_t view, uint16_t* dst);  /* H*W*4 (L,R,U,D) */
 
-/* Batched, device-resident API.  Inputs are packed [n][H][W][3] (BGR) and [n][H][W] (gray). */
+/* Batched, device-resident API.  Inputs are packed [n][H][W][3] (BGR) and [n][H][W] (gray) and may
+ * be host or device pointers (unified addressing: e.g. a torch tensor already in HBM is copied
+ * device-to-device).  A device source must be complete before the call (its stream synchronized). */
 SM_API sm_status sm_upload_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
                                  const uint8_t* lgray, const uint8_t* rgray);
 /* Run cost -> CBCA -> SolveAll(py_lev=1, reg_lambda) -> SGM -> WTA on the n uploaded pairs.
- * Asynchronous on the ctx stream.  disp_out: host [n][H][W] int16 (synchronous copy-back) or
+ * Asynchronous on the ctx stream.  disp_out: host or device [n][H][W] int16 (synchronous copy) or
  * NULL to leave the maps on the device (read them with sm_download_disp). */
 SM_API sm_status sm_run(sm_ctx* ctx, int32_t n, float reg_lambda, int16_t* disp_out);
 SM_API sm_status sm_download_disp(sm_ctx* ctx, int32_t n, int16_t* disp_out);

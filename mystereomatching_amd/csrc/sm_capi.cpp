@@ -401,9 +401,9 @@ sm_status upload(sm_ctx* c, int n, const uint8_t* lbgr, const uint8_t* rbgr, siz
         const uint8_t* gsrc = view == 0 ? lgray : rgray;
         for (int b = 0; b < n; b++) {
             uint8_t* dst = c->bgr + ((size_t)b * 2 + view) * c->npix * 3;
-            HIP_TRY(c, hipMemcpy2DAsync(dst, crow, src + (size_t)b * H * cstride, cstride, crow, H, hipMemcpyHostToDevice, c->st));
+            HIP_TRY(c, hipMemcpy2DAsync(dst, crow, src + (size_t)b * H * cstride, cstride, crow, H, hipMemcpyDefault, c->st));
             uint8_t* gdst = c->gray + ((size_t)b * 2 + view) * c->npix;
-            HIP_TRY(c, hipMemcpy2DAsync(gdst, W, gsrc + (size_t)b * H * gstride, gstride, W, H, hipMemcpyHostToDevice, c->st));
+            HIP_TRY(c, hipMemcpy2DAsync(gdst, W, gsrc + (size_t)b * H * gstride, gstride, W, H, hipMemcpyDefault, c->st));
         }
     }
     HIP_TRY(c, hipStreamSynchronize(c->st));
@@ -656,7 +656,7 @@ sm_status sm_download_disp(sm_ctx* c, int32_t n, int16_t* disp_out) {
     if (s) return s;
     if (!disp_out || n < 1 || n > c->cap) return fail(c, SM_EINVAL, "bad arguments");
     if (c->stage != 4) return fail(c, SM_ESTATE, "no disparity map yet");
-    HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDefault, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     return SM_OK;
 }

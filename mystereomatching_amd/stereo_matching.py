@@ -193,6 +193,14 @@ def SolveAll(smPyr: Sequence[StereoMatching], PY_LVL: int, REG_LAMBDA: float):
     _capi.check(sm._lib, sm._ctx, sm._lib.sm_solve_all(sm._ctx, int(PY_LVL), float(REG_LAMBDA)), "SolveAll")
 
 
+def _is_device_tensor(a) -> bool:
+    return type(a).__module__.startswith("torch") and getattr(a, "is_cuda", False)
+
+
+def _to_numpy(a):
+    return a.numpy() if type(a).__module__.startswith("torch") else a
+
+
 class StereoBatch:
     """n independent pairs of one size through the whole main_.cpp sequence in one set of launches."""
 
@@ -217,9 +225,21 @@ class StereoBatch:
         self.close()
 
     def upload(self, lbgr, rbgr, lgray, rgray):
-        arrs = [np.ascontiguousarray(a, np.uint8) for a in (lbgr, rbgr, lgray, rgray)]
-        n = arrs[0].shape[0]
-        st = self._lib.sm_upload_batch(self._ctx, n, *[_capi.ptr(a) for a in arrs])
+        """Stacked numpy arrays (host) or uint8 torch tensors already on the GPU (copied
+        device-to-device; the caller's stream is synchronized first)."""
+        if all(_is_device_tensor(a) for a in (lbgr, rbgr, lgray, rgray)):
+            import torch
+            ts = [a.contiguous() for a in (lbgr, rbgr, lgray, rgray)]
+            if any(t.dtype != torch.uint8 for t in ts):
+                raise TypeError("device images must be uint8 tensors")
+            torch.cuda.current_stream(ts[0].device).synchronize()
+            ptrs = [C.c_void_p(t.data_ptr()) for t in ts]
+            n = ts[0].shape[0]
+        else:
+            arrs = [np.ascontiguousarray(_to_numpy(a), np.uint8) for a in (lbgr, rbgr, lgray, rgray)]
+            ptrs = [_capi.ptr(a) for a in arrs]
+            n = arrs[0].shape[0]
+        st = self._lib.sm_upload_batch(self._ctx, n, *ptrs)
         _capi.check(self._lib, self._ctx, st, "sm_upload_batch")
         self.n = n
 
@@ -229,9 +249,18 @@ class StereoBatch:
         _capi.check(self._lib, self._ctx, st, "sm_run")
         return out
 
-    def download(self) -> np.ndarray:
-        out = np.empty((self.n, self.shape[0], self.shape[1]), np.int16)
-        _capi.check(self._lib, self._ctx, self._lib.sm_download_disp(self._ctx, self.n, _capi.ptr(out)), "download")
+    def download(self, out=None):
+        """The n int16 maps into a new numpy array, or into `out` (numpy, or an int16 torch
+        tensor on the GPU: device-to-device copy)."""
+        if out is None:
+            out = np.empty((self.n, self.shape[0], self.shape[1]), np.int16)
+        if _is_device_tensor(out):
+            if not out.is_contiguous() or out.numel() < self.n * self.shape[0] * self.shape[1]:
+                raise ValueError("out must be a contiguous tensor of at least n*H*W int16")
+            dst = C.c_void_p(out.data_ptr())
+        else:
+            dst = _capi.ptr(out)
+        _capi.check(self._lib, self._ctx, self._lib.sm_download_disp(self._ctx, self.n, dst), "download")
         return out
 
     def synchronize(self):

@@ -1,0 +1,49 @@
+"""GPU: device-resident batch entry points and the batch runner's product compute path."""
+import numpy as np
+import pytest
+
+from mystereomatching_amd import StereoBatch
+from mystereomatching_amd import synthetic as S
+from mystereomatching_amd.batch import DistributedBatchRunner, hip_compute_fn
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("lbgr", "rbgr", "lgray", "rgray")
+
+
+def _oracle_maps(oracle, batch, H, W, md):
+    cfg = oracle.config(H, W, md)
+    return np.stack([oracle.run({k: batch[k][i] for k in KEYS}, cfg)["disp"] for i in range(batch["lgray"].shape[0])])
+
+
+def test_device_tensor_upload_download(oracle):
+    import torch
+    H, W, md, n = 41, 67, 23, 3
+    batch = S.make_batch(n, H, W, md + 1, first_index=300)
+    sb = StereoBatch(md, H, W, n, device=0)
+    try:
+        dev = {k: torch.from_numpy(np.ascontiguousarray(batch[k])).cuda() for k in KEYS}
+        sb.upload(*(dev[k] for k in KEYS))
+        sb.run(0.3, download=False)
+        out = torch.full((n, H, W), 7, dtype=torch.int16, device="cuda")
+        sb.download(out)
+        got = out.cpu().numpy()
+        np.testing.assert_array_equal(got, _oracle_maps(oracle, batch, H, W, md))
+        # host path gives the same maps
+        sb.upload(*(batch[k] for k in KEYS))
+        np.testing.assert_array_equal(sb.run(0.3), got)
+    finally:
+        sb.close()
+
+
+def test_runner_single_rank_hip(oracle):
+    import torch
+    H, W, md, n = 30, 52, 15, 4
+    batch = S.make_batch(n, H, W, md + 1, first_index=400)
+    fn = hip_compute_fn(md, H, W, n, device=0)
+    try:
+        runner = DistributedBatchRunner(fn, device=torch.device("cuda", 0))
+        got = runner.run(batch, max_disp=md, reg_lambda=0.3)
+        np.testing.assert_array_equal(got, _oracle_maps(oracle, batch, H, W, md))
+    finally:
+        fn.close()

@@ -47,19 +47,33 @@ __device__ __forceinline__ uint32_t shr1_in(uint32_t v, uint32_t in) {  // lane 
     return (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
 }
 
-template <int MODE>
+// Positions per tile and tiles prefetched ahead: the sweeps are bound by memory latency at the
+// 5-6 waves per CU the LDS rings allow, so PF tiles of loads are kept in flight; the loads of PF
+// tiles plus the stores of one stay below the 63 of vmcnt (V sweeps load one right-arm word per
+// position and set, hence their shorter tiles).
+__host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
+    return mode == CB_SCAN || (horiz && mode == CB_NORM) ? 16 : 8;
+}
+template <bool HORIZ, int MODE>
 struct CbCfg {
-    static constexpr int T = MODE == CB_SCAN ? 16 : 8;  // loads + stores per tile stay < 63 (vmcnt)
+    static constexpr int T = cbca_tile(HORIZ, MODE);
+    static constexpr int PF = (!HORIZ && MODE != CB_NORM) ? 1 : 2;
     // arm sets: 0 = pass pair at i (= j - lag), 1 = perpendicular pair at j, 2 = pass pair at j - 2 lag
     static constexpr int NSETS = MODE == CB_SCAN ? 1 : (MODE == CB_NORM ? 2 : 3);
 };
 
-__host__ __device__ inline int cbca_tile(int mode) { return mode == CB_SCAN ? CbCfg<CB_SCAN>::T : CbCfg<CB_NORM>::T; }
 // ring slots: >= 2*lag + T + 1 (a whole tile is written before any of it is read) and a multiple
 // of T (a tile's write slots never wrap)
-__host__ __device__ inline int cbca_ring(int lag, int mode) {
-    const int T = cbca_tile(mode);
+__host__ __device__ inline int cbca_ring(int lag, bool horiz, int mode) {
+    const int T = cbca_tile(horiz, mode);
     return (2 * lag + T + 1 + T - 1) / T * T;
+}
+// dynamic LDS in 4-byte words: S ring(s) of ring x 64 floats, then the u16 area ring
+__host__ __device__ inline int cbca_smem_words(int lag, bool horiz, int mode) {
+    const int ring = cbca_ring(lag, horiz, mode);
+    const int floats = mode == CB_NORM_SCAN ? 2 : 1;
+    const int u16s = mode == CB_SCAN ? 0 : 1;
+    return ring * 64 * floats + ring * 32 * u16s;
 }
 
 template <bool HORIZ, int T, int NSETS>
@@ -70,10 +84,10 @@ struct CbTile {
     uint32_t a1[HORIZ ? 1 : NSETS][T];   // V: right arm pair at (row j0 + k - off, u - d)
 };
 
-template <bool HORIZ, int MODE, bool FULL>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE>
 struct CbLine {
-    static constexpr int T = CbCfg<MODE>::T;
-    static constexpr int NSETS = CbCfg<MODE>::NSETS;
+    static constexpr int T = CbCfg<HORIZ, MODE>::T;
+    static constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
     using Tile = CbTile<HORIZ, T, NSETS>;
 
     const float* xbase;       // FULL: chunk base (uniform), lane offset added; else per-lane base
@@ -92,7 +106,6 @@ struct CbLine {
     float* r1;
     float* r2;
     uint16_t* ra;
-    int apply_scale;
     float scale;
 
     __device__ __forceinline__ int set_off(int s) const { return s == 0 ? lag : (s == 1 ? 0 : 2 * lag); }
@@ -160,25 +173,30 @@ struct CbLine {
     __device__ __forceinline__ int up(int s) const { return (int)min((uint32_t)s, (uint32_t)(s - ring)); }   // s in [0, 2 ring)
     __device__ __forceinline__ int dn(int s) const { return (int)min((uint32_t)s, (uint32_t)(s + ring)); }   // s in (-ring, ring)
 
+    // genfinalVm_cbca's division, then (last pass only) SolveAll's `sum = 0; sum += w * v`
+    // (cpp:2189-2201): 0 + x == x for every x except -0, and no CBCA value is ever -0 (costs are
+    // >= +0, prefix sums of them too, and x - x rounds to +0), so the add is dropped.
     __device__ __forceinline__ float finish_norm(float diff, uint32_t area) const {
-        float out = diff / (float)area;
-        if (apply_scale) {
-            float sum = 0.f;
-            sum += scale * out;
-            out = sum;
-        }
-        return out;
+        const float out = diff / (float)area;
+        return SCALE ? scale * out : out;
     }
 
-    // ---------------- steady state: every position of the tile is inside every range ----------
-    __device__ __forceinline__ void tile_fast(const Tile& t, int j0) {
+    // ---------------- one tile of T positions, branch-free ------------------------------------
+    // Every tile runs the same straight-line code.  Inputs past the line end are clamped loads
+    // whose prefix values are never read (heads stop at the border); positions before the line
+    // start read the zeroed ring, which is exactly the reference's border case
+    // out = S[i + head] (cal1DCost, h:1643-1715).  Only the two ends of a line (GUARD) test
+    // whether an output position exists before storing it.
+    template <bool GUARD>
+    __device__ __forceinline__ void tile(const Tile& t, int j0) {
         uint32_t pi[T], pi2[T];
         // ring % T == 0 and ws % T == 0, so the tile's write slots ws .. ws+T-1 never wrap
         float* w1 = r1 + ws * 64 + lane;
         uint16_t* wa = ra + ws * 64 + lane;
         const int si0 = uwrap(ws - lag);        // slot of i = j0 - lag
         const int s20 = uwrap(ws - 2 * lag);    // slot of i2 = j0 - 2 lag
-        float* ob = ob_tile(j0 - lag);
+        const int i0 = j0 - lag;
+        float* ob = ob_tile(i0);
         // phase A: inputs j0 .. j0+T-1 (+ arm windows)
 #pragma unroll
         for (int k = 0; k < T; k++) {
@@ -196,14 +214,11 @@ struct CbLine {
         // phase B: first-stage outputs at i = j - lag (reads batched, then arithmetic)
         float shv[T], stv[T];
         uint32_t ahv[T], atv[T];
-        bool inner[T];
 #pragma unroll
         for (int k = 0; k < T; k++) {
-            const int i = j0 + k - lag;
             const int tl = pi[k] & 0xffff, hd = pi[k] >> 16;
             const int hs = up(si0 + k + hd);             // slot of i + head  (< 2 ring)
             const int ts = dn(hs - (hd + tl + 1));       // slot of i - tail - 1 (window < ring)
-            inner[k] = i - tl - 1 >= 0;
             shv[k] = r1[hs * 64 + lane];
             stv[k] = r1[ts * 64 + lane];
             if (MODE != CB_SCAN) {
@@ -213,16 +228,17 @@ struct CbLine {
         }
 #pragma unroll
         for (int k = 0; k < T; k++) {
-            const int i = j0 + k - lag;
-            const float diff = shv[k] - (inner[k] ? stv[k] : 0.f);  // == inner ? sh - st : sh
+            const float diff = shv[k] - stv[k];
+            const bool live = !GUARD || (unsigned)(i0 + k) < (unsigned)len;
             if (MODE == CB_SCAN) {
-                store_tile(ob, j0 - lag, k, diff);
+                if (live) store_tile(ob, i0, k, diff);
             } else {
-                const uint32_t area = (ahv[k] - (inner[k] ? atv[k] : 0u)) & 0xffffu;
+                const uint32_t area = (ahv[k] - atv[k]) & 0xffffu;
                 if (MODE == CB_NORM) {
-                    store_tile(ob, j0 - lag, k, finish_norm(diff, area));
+                    if (live) store_tile(ob, i0, k, finish_norm(diff, area));
                 } else {
-                    const float y = diff / (float)area;          // final value of iteration k at i
+                    float y = diff / (float)area;                 // final value of iteration k at i
+                    if (GUARD) y = (i0 + k >= 0) ? y : 0.f;       // nothing accumulates before the line
                     S2 = S2 + y;                                  // prefix of iteration k+1's first pass
                     r2[up(si0 + k) * 64 + lane] = S2;
                 }
@@ -231,94 +247,46 @@ struct CbLine {
         // phase C (NS): second-stage outputs at i2 = j - 2 lag
         if (MODE == CB_NORM_SCAN) {
             float s2h[T], s2t[T];
-            bool in2[T];
 #pragma unroll
             for (int k = 0; k < T; k++) {
-                const int i2 = j0 + k - 2 * lag;
                 const int tl = pi2[k] & 0xffff, hd = pi2[k] >> 16;
                 const int hs = up(s20 + k + hd);
-                in2[k] = i2 - tl - 1 >= 0;
                 s2h[k] = r2[hs * 64 + lane];
                 s2t[k] = r2[dn(hs - (hd + tl + 1)) * 64 + lane];
             }
-            float* ob2 = ob_tile(j0 - 2 * lag);
+            const int i20 = j0 - 2 * lag;
+            float* ob2 = ob_tile(i20);
 #pragma unroll
-            for (int k = 0; k < T; k++) store_tile(ob2, j0 - 2 * lag, k, s2h[k] - (in2[k] ? s2t[k] : 0.f));
+            for (int k = 0; k < T; k++)
+                if (!GUARD || (unsigned)(i20 + k) < (unsigned)len) store_tile(ob2, i20, k, s2h[k] - s2t[k]);
         }
         ws = (ws + T == ring) ? 0 : ws + T;
     }
 
-    // ---------------- boundary tiles: per position, every range test evaluated ----------------
-    __device__ __forceinline__ void step_guarded(const Tile& t, int k, int j) {
-        advance(t, k, j);
-        const int sj = up(ws + k);
-        if (j < len) {
-            const float x = t.x[k];
-            S1 = (j == 0) ? x : S1 + x;
-            r1[sj * 64 + lane] = S1;
-            if (MODE != CB_SCAN) {
-                const uint32_t pp = isect(t, 1, k);
-                const uint32_t ain = (pp & 0xffffu) + (pp >> 16) + 1u;
-                Acc = (j == 0) ? ain : Acc + ain;
-                ra[sj * 64 + lane] = (uint16_t)Acc;
-            }
-        }
-        const int i = j - lag;
-        if (i >= 0 && i < len) {
-            const uint32_t pr = isect(t, 0, k);
-            const int tl = pr & 0xffff, hd = pr >> 16;
-            const int si = uwrap(ws + k - lag);
-            const int hs = up(si + hd), ts = dn(si - tl - 1);
-            const bool inner = i - tl - 1 >= 0;
-            const float diff = r1[hs * 64 + lane] - (inner ? r1[ts * 64 + lane] : 0.f);
-            if (MODE == CB_SCAN) {
-                store(i, diff);
-            } else {
-                const uint32_t area = (ra[hs * 64 + lane] - (inner ? ra[ts * 64 + lane] : 0u)) & 0xffffu;
-                if (MODE == CB_NORM) {
-                    store(i, finish_norm(diff, area));
-                } else {
-                    const float y = diff / (float)area;
-                    S2 = (i == 0) ? y : S2 + y;
-                    r2[si * 64 + lane] = S2;
-                }
-            }
-        }
-        if (MODE == CB_NORM_SCAN) {
-            const int i2 = j - 2 * lag;
-            if (i2 >= 0 && i2 < len) {
-                const uint32_t pr = isect(t, 2, k);
-                const int tl = pr & 0xffff, hd = pr >> 16;
-                const int s2 = uwrap(ws + k - 2 * lag);
-                const float v = r2[up(s2 + hd) * 64 + lane] - ((i2 - tl - 1 >= 0) ? r2[dn(s2 - tl - 1) * 64 + lane] : 0.f);
-                store(i2, v);
-            }
-        }
-    }
-
-    __device__ __forceinline__ void process(const Tile& t, int j0, int nst, int fast_lo) {
-        if (j0 >= fast_lo && j0 > 0 && j0 + T <= len) {
-            tile_fast(t, j0);
-        } else {
-#pragma unroll
-            for (int k = 0; k < T; k++)
-                if (j0 + k < nst) step_guarded(t, k, j0 + k);
-            ws = (ws + T == ring) ? 0 : ws + T;
-        }
+    __device__ __forceinline__ void process(const Tile& t, int j0) {
+        constexpr int stages = MODE == CB_NORM_SCAN ? 2 : 1;
+        const int last_out = j0 + T - 1 - lag * stages;        // last output position of the tile
+        if (j0 - lag >= 0 && last_out < len && (MODE != CB_NORM_SCAN || j0 - 2 * lag >= 0))
+            tile<false>(t, j0);
+        else
+            tile<true>(t, j0);
     }
 };
 
-template <bool HORIZ, int MODE, bool FULL>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE>
 __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     extern __shared__ float smem[];
-    CbLine<HORIZ, MODE, FULL> L;
-    constexpr int T = CbCfg<MODE>::T;
-    constexpr int NSETS = CbCfg<MODE>::NSETS;
+    CbLine<HORIZ, MODE, FULL, SCALE> L;
+    constexpr int T = CbCfg<HORIZ, MODE>::T;
+    constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
     L.lane = threadIdx.x;
     const int nchunks = (a.D + 63) >> 6;
-    L.line = blockIdx.x / nchunks;
-    const int chunk = blockIdx.x - L.line * nchunks;
-    const int b = blockIdx.y;
+    const int per_pair = (HORIZ ? a.H : a.W) * nchunks;
+    const int blk = xcd_swizzle(blockIdx.x, gridDim.x);   // neighbouring lines on one XCD
+    const int b = blk / per_pair;
+    const int lc = blk - b * per_pair;
+    L.line = lc / nchunks;
+    const int chunk = lc - L.line * nchunks;
     L.d = chunk * 64 + L.lane;
     const size_t npix = (size_t)a.H * a.W;
     const size_t first_pix = HORIZ ? (size_t)L.line * a.W : (size_t)L.line;
@@ -349,44 +317,66 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.c64 = chunk * 64;
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
-    L.ring = cbca_ring(a.lag, MODE);
+    L.ring = cbca_ring(a.lag, HORIZ, MODE);
     L.r1 = smem;
     L.r2 = smem + (size_t)L.ring * 64;
     L.ra = (uint16_t*)(smem + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
-    L.apply_scale = a.apply_scale;
     L.scale = a.scale;
+    {   // zero the rings: reads of positions before the line start then yield S = 0, area = 0
+        const int words = (int)(cbca_smem_words(a.lag, HORIZ, MODE));
+        for (int w = L.lane; w < words; w += 64) smem[w] = 0.f;
+        __syncthreads();  // one wave; also orders the float stores before the u16 ring reads
+    }
     L.S1 = L.S2 = 0.f;
     L.Acc = 0;
     L.ws = 0;
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    const int fast_lo = a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    typename CbLine<HORIZ, MODE, FULL>::Tile ta, tb;
-    L.load(ta, 0);
-    for (int j0 = 0; j0 < nst; j0 += 2 * T) {
-        L.load(tb, j0 + T);
-        L.process(ta, j0, nst, fast_lo);
-        L.load(ta, j0 + 2 * T);
-        L.process(tb, j0 + T, nst, fast_lo);
+    typename CbLine<HORIZ, MODE, FULL, SCALE>::Tile ta, tb, tc;
+    if constexpr (CbCfg<HORIZ, MODE>::PF == 2) {
+        L.load(ta, 0);
+        L.load(tb, T);
+        for (int j0 = 0; j0 < nst; j0 += 3 * T) {
+            L.load(tc, j0 + 2 * T);
+            L.process(ta, j0);
+            if (j0 + T >= nst) break;
+            L.load(ta, j0 + 3 * T);
+            L.process(tb, j0 + T);
+            if (j0 + 2 * T >= nst) break;
+            L.load(tb, j0 + 4 * T);
+            L.process(tc, j0 + 2 * T);
+        }
+    } else {
+        L.load(ta, 0);
+        for (int j0 = 0; j0 < nst; j0 += 2 * T) {
+            L.load(tb, j0 + T);
+            L.process(ta, j0);
+            if (j0 + T >= nst) break;
+            L.load(ta, j0 + 2 * T);
+            L.process(tb, j0 + T);
+        }
     }
 }
 
-size_t cbca_smem_bytes(int lag, int mode) {
-    const size_t ring = cbca_ring(lag, mode);
-    const size_t floats = mode == CB_NORM_SCAN ? 2 : 1;
-    const size_t u16s = mode == CB_SCAN ? 0 : 1;
-    return ring * 64 * (4 * floats + 2 * u16s);
+size_t cbca_smem_bytes(int lag, bool horiz, int mode) { return 4 * cbca_smem_words(lag, horiz, mode); }
+
+template <bool HORIZ, int MODE, bool SCALE>
+static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
+    const int nchunks = (a.D + 63) / 64;
+    const int lines = HORIZ ? a.H : a.W;
+    dim3 grid(lines * nchunks * n);
+    const size_t shm = cbca_smem_bytes(a.lag, HORIZ, MODE);
+    if (a.D % 64 == 0)
+        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE>), grid, dim3(64), shm, st, a);
+    else
+        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE>), grid, dim3(64), shm, st, a);
 }
 
 template <bool HORIZ, int MODE>
 static void launch_mode(const CbcaArgs& a, int n, hipStream_t st) {
-    const int nchunks = (a.D + 63) / 64;
-    const int lines = HORIZ ? a.H : a.W;
-    dim3 grid(lines * nchunks, n);
-    const size_t shm = cbca_smem_bytes(a.lag, MODE);
-    if (a.D % 64 == 0)
-        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true>), grid, dim3(64), shm, st, a);
-    else
-        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false>), grid, dim3(64), shm, st, a);
+    if constexpr (MODE == CB_NORM) {
+        if (a.apply_scale) return launch_scaled<HORIZ, MODE, true>(a, n, st);
+    }
+    launch_scaled<HORIZ, MODE, false>(a, n, st);
 }
 
 void launch_cbca(const CbcaArgs& a, bool horiz, int mode, int n, hipStream_t st) {

@@ -65,6 +65,15 @@ __host__ __device__ inline int reflect101(int p, int len) {
     return p;
 }
 
+// XCD-aware block order (speed only, never correctness): the dispatcher deals workgroups
+// round-robin over the 8 XCDs, so hardware block `orig` runs on XCD group orig % 8.  This
+// bijection gives each XCD group a contiguous range of logical blocks, so neighbouring lines
+// that read the same arm / image rows share one XCD's L2.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+    const int xcd = orig & 7, idx = orig >> 3, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 // wave64 cross-lane helpers (device only)
 // DPP controls (GFX9 encoding).
 enum : int {

@@ -27,11 +27,10 @@
 namespace sm {
 
 // expf core; `tab` is the 32-entry 2^(i/32) table (device: __constant__, host: static).
+// Main path only: valid for -0x1.9fe368p6 <= x <= 0x1.62e42ep6 (callers that cannot be outside
+// that range, or that discard such results, skip the special cases).
 template <typename Tab>
-__host__ __device__ inline float expf_glibc(float x, const Tab& tab) {
-    // Special cases of glibc's expf for |x| >= 88 that the main path does not cover.
-    if (x < -0x1.9fe368p6f) return 0.0f;           // underflow (also -inf)
-    if (x > 0x1.62e42ep6f) return __builtin_inff(); // overflow (never reached on the hot path)
+__host__ __device__ inline float expf_glibc_core(float x, const Tab& tab) {
     const double InvLn2N = 0x1.71547652b82fep+0 * 32;
     const double SHIFT = 0x1.8p+52;
     const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32;
@@ -52,6 +51,14 @@ __host__ __device__ inline float expf_glibc(float x, const Tab& tab) {
     y = __builtin_fma(zz, r2, y);
     y = y * s;
     return (float)y;
+}
+
+template <typename Tab>
+__host__ __device__ inline float expf_glibc(float x, const Tab& tab) {
+    // Special cases of glibc's expf for |x| >= 88 that the main path does not cover.
+    if (x < -0x1.9fe368p6f) return 0.0f;           // underflow (also -inf)
+    if (x > 0x1.62e42ep6f) return __builtin_inff(); // overflow (never reached on the hot path)
+    return expf_glibc_core(x, tab);
 }
 
 __host__ __device__ inline int reflect101(int p, int len) {
@@ -106,6 +113,30 @@ __device__ inline unsigned perm32_min_u(unsigned v, bool is_float) {
     auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
     if (is_float) return __builtin_bit_cast(unsigned, fminf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1])));
     return (unsigned)min((int)r[0], (int)r[1]);
+}
+
+// Min over the wave of NON-NEGATIVE floats (and +inf / FLT_MAX): their IEEE order is the
+// unsigned order of the bit patterns, so the reduction runs on v_min_u32 (no NaN
+// canonicalisation) and ends with the GFX9 row broadcasts; the result is wave-uniform.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t umin_dpp(uint32_t v) {
+    return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffffu, (int)v, CTRL, ROWS, 0xF, false));
+}
+enum : int { DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143 };
+__device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
+    v = umin_dpp<DPP_QUAD_1032>(v);
+    v = umin_dpp<DPP_QUAD_2301>(v);
+    v = umin_dpp<DPP_ROW_HALF_MIRROR>(v);
+    v = umin_dpp<DPP_ROW_MIRROR>(v);          // every lane: its row's min
+    v = umin_dpp<DPP_ROW_BCAST15, 0xA>(v);    // rows 1, 3 also see rows 0, 2
+    v = umin_dpp<DPP_ROW_BCAST31, 0xC>(v);    // rows 2, 3 also see row 1: lane 63 = wave min
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ float wave_min_pos(float v) {
+    return __builtin_bit_cast(float, wave_umin(__builtin_bit_cast(uint32_t, v)));
+}
+__device__ __forceinline__ float fmin_pos(float a, float b) {  // a, b >= +0
+    return __builtin_bit_cast(float, min(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)));
 }
 
 // Full-wave min; every lane receives the result.  min is exact, so the combine order is free.

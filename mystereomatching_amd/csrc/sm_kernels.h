@@ -7,7 +7,7 @@
 namespace sm {
 
 enum { SM_M_CENSUS_GRAD = 0, SM_M_CENSUS = 1, SM_M_AD_CENSUS = 2, SM_M_AD = 3 };
-enum { SGM_FIRST = 1, SGM_LAST = 2 };
+enum { SGM_FIRST = 1, SGM_LAST = 2, SGM_KEEP = 4 };  // KEEP: last path also writes the summed volume
 enum { CB_SCAN = 0, CB_NORM = 1, CB_NORM_SCAN = 2 };
 constexpr int CBCA_TILE = 16;  // steps of lookahead per wave in the CBCA line sweeps
 

@@ -217,54 +217,78 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 //   census  gen_cenVM_XOR (h:936-981); grad calgradvm (cpp:388-455);
 //   AD      gen_ad_sd_vm (cpp:2468-2509);   fusion gen_vm_from2vm_exp (cpp:3566-3590).
 // exp(-C/lam) (C integer 0..128) and exp(-AD/lam) (AD = s/3, s integer 0..765) come from LUTs
-// built on the host with libm expf; the gradient term uses sm::dev_expf, skipped when
-// -G/lamG < -17.5: then expf(-G/lamG) <= 2^-25 and fl(t - e) == t for every t = fl(2 - e0) in
-// [1, 2), so the result is bit-identical without evaluating it.
+// built on the host with libm expf (staged in LDS); the gradient term is sm::expf_glibc_core,
+// whose result is discarded when -G/lamG < -17.5: then expf(-G/lamG) <= 2^-25 and
+// fl(t - e) == t for every t = fl(2 - e0) in [1, 2), so the reference's value is t itself.
+// The element loop is branch-free: out-of-range candidates (u - d < 0 or u + d >= W) read a
+// clamped, staged neighbour and select the reference's out-of-range cost afterwards; without
+// the adaptive weights the weights are 1, and 1 * x + 1 * y == x + y exactly.  lamG == 1 (the
+// default) skips the division, since -G / 1 == -G.
 // ---------------------------------------------------------------------------------------
-constexpr int COST_P = 32;
+constexpr int COST_P = 64;
+constexpr int LUT_A_N = 129, LUT_B_N = 766;
 
-template <int METHOD>
+template <int METHOD, bool LAM1>
 __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     extern __shared__ __align__(16) unsigned char cs_raw[];
-    const int D = a.D, W = a.W;
-    const int u0 = blockIdx.x * COST_P, v = blockIdx.y, b = blockIdx.z;
+    const int D = a.D, W = a.W, H = a.H;
+    const int nbx = (W + COST_P - 1) / COST_P;
+    const int blk = xcd_swizzle(blockIdx.x, gridDim.x);  // neighbouring segments share an XCD's L2
+    const int bx = blk % nbx, rest = blk / nbx;
+    const int v = rest % H, b = rest / H;
+    const int u0 = bx * COST_P;
     const int np = min(COST_P, W - u0);
     const int nm = np + D - 1;                      // moving pixels needed
     const int sgn = a.view == 0 ? 1 : -1;           // moving position = u - sgn * d
     const int mbase = a.view == 0 ? u0 - (D - 1) : u0;
-    const size_t npix = (size_t)a.H * W;
+    const size_t npix = (size_t)H * W;
     const int fview = a.view, mview = 1 - a.view;
     const size_t frow = ((size_t)b * 2 + fview) * npix + (size_t)v * W;
     const size_t mrow = ((size_t)b * 2 + mview) * npix + (size_t)v * W;
-    // LDS carve-up
+    constexpr bool CEN = METHOD != SM_M_AD;
+    constexpr bool GRAD = METHOD == SM_M_CENSUS_GRAD;
+    constexpr bool ADM = METHOD == SM_M_AD || METHOD == SM_M_AD_CENSUS;
+    // LDS carve-up (16-byte items first)
     ulonglong2* fcode = (ulonglong2*)cs_raw;                 // [P]
     ulonglong2* mcode = fcode + COST_P;                      // [P + D - 1]
-    float* fgx = (float*)(mcode + (COST_P + D - 1));         // [P]
+    uint64_t* etab = (uint64_t*)(mcode + (COST_P + D - 1));  // [32] 2^(i/32)
+    float* fgx = (float*)(etab + 32);                        // [P]
     float* fgy = fgx + COST_P;
-    float* fwa = fgy + COST_P;                               // adaptive weight a
-    float* fwb = fwa + COST_P;                               // 1 - a
+    float* fwa = fgy + COST_P;                               // adaptive weight a (1 if off)
+    float* fwb = fwa + COST_P;                               // 1 - a (1 if off)
     float* mgx = fwb + COST_P;                               // [P + D - 1]
     float* mgy = mgx + (COST_P + D - 1);
     uint32_t* fbgr = (uint32_t*)(mgy + (COST_P + D - 1));    // [P]
     uint32_t* mbgr = fbgr + COST_P;                          // [P + D - 1]
+    float* luta = (float*)(mbgr + (COST_P + D - 1));         // [LUT_A_N]
+    float* lutb = luta + LUT_A_N;                            // [LUT_B_N]
     const int tid = threadIdx.y * 64 + threadIdx.x;
+    if (GRAD && tid < 32) etab[tid] = c_exp_tab[tid];
+    if (CEN)
+        for (int i = tid; i < LUT_A_N; i += 256) luta[i] = c_lut_a[i];
+    if (METHOD == SM_M_AD_CENSUS)
+        for (int i = tid; i < LUT_B_N; i += 256) lutb[i] = c_lut_b[i];
     for (int i = tid; i < np; i += 256) {
         const int u = u0 + i;
-        if (METHOD != SM_M_AD) fcode[i] = a.code[frow + u];
-        if (METHOD == SM_M_CENSUS_GRAD) {
+        if (CEN) fcode[i] = a.code[frow + u];
+        if (GRAD) {
             fgx[i] = a.gx[frow + u];
             fgy[i] = a.gy[frow + u];
-            const uint32_t* planes = (const uint32_t*)a.arms + ((size_t)b * 2 + fview) * 2 * npix + (size_t)v * W + u;
-            const uint32_t ph = planes[0], pv = planes[npix];
-            float sH = (float)min(ph & 0xffffu, ph >> 16);
-            float sV = (float)min(pv & 0xffffu, pv >> 16);
-            if (sH == 0) sH = 1;
-            if (sV == 0) sV = 1;
-            const float wa = sH / (sH + sV);
+            float wa = 1.f, wb = 1.f;
+            if (a.grad_adaptive) {
+                const uint32_t* planes = (const uint32_t*)a.arms + ((size_t)b * 2 + fview) * 2 * npix + (size_t)v * W + u;
+                const uint32_t ph = planes[0], pv = planes[npix];
+                float sH = (float)min(ph & 0xffffu, ph >> 16);
+                float sV = (float)min(pv & 0xffffu, pv >> 16);
+                if (sH == 0) sH = 1;
+                if (sV == 0) sV = 1;
+                wa = sH / (sH + sV);
+                wb = 1.0f - wa;
+            }
             fwa[i] = wa;
-            fwb[i] = 1.0f - wa;
+            fwb[i] = wb;
         }
-        if (METHOD == SM_M_AD || METHOD == SM_M_AD_CENSUS) {
+        if (ADM) {
             const uint8_t* p = a.bgr + (frow + u) * 3;
             fbgr[i] = p[0] | (p[1] << 8) | (p[2] << 16);
         }
@@ -272,73 +296,66 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     for (int i = tid; i < nm; i += 256) {
         const int q = mbase + i;
         if (q < 0 || q >= W) continue;
-        if (METHOD != SM_M_AD) mcode[i] = a.code[mrow + q];
-        if (METHOD == SM_M_CENSUS_GRAD) {
+        if (CEN) mcode[i] = a.code[mrow + q];
+        if (GRAD) {
             mgx[i] = a.gx[mrow + q];
             mgy[i] = a.gy[mrow + q];
         }
-        if (METHOD == SM_M_AD || METHOD == SM_M_AD_CENSUS) {
+        if (ADM) {
             const uint8_t* p = a.bgr + (mrow + q) * 3;
             mbgr[i] = p[0] | (p[1] << 8) | (p[2] << 16);
         }
     }
     __syncthreads();
+    const float cd = a.census_default;
     float* out = a.vm + ((size_t)b * npix + (size_t)v * W + u0) * D;
     for (int pl = threadIdx.y; pl < np; pl += 4) {
         const int u = u0 + pl;
-        const ulonglong2 cf = (METHOD != SM_M_AD) ? fcode[pl] : make_ulonglong2(0, 0);
+        const ulonglong2 cf = CEN ? fcode[pl] : make_ulonglong2(0, 0);
+        float fx = 0.f, fy = 0.f, wa = 0.f, wb = 0.f;
+        uint32_t fc = 0;
+        if (GRAD) {
+            fx = fgx[pl];
+            fy = fgy[pl];
+            wa = fwa[pl];
+            wb = fwb[pl];
+        }
+        if (ADM) fc = fbgr[pl];
         for (int d = threadIdx.x; d < D; d += 64) {
             const int q = u - sgn * d;                 // moving position
-            const bool oor = q < 0 || q >= W;
-            const int mi = q - mbase;
+            const bool oor = (unsigned)q >= (unsigned)W;
+            const int mi = min(max(q, 0), W - 1) - mbase;  // clamped, always a staged entry
             float cen = 0.f;
-            if (METHOD != SM_M_AD) {
-                if (oor)
-                    cen = a.census_default;
-                else {
-                    const ulonglong2 cm = mcode[mi];
-                    float cost = 0;
-                    cost += (float)__popcll(cf.x ^ cm.x);
-                    if (a.nwords > 1) cost += (float)__popcll(cf.y ^ cm.y);
-                    cen = fminf(cost, a.census_default);
-                }
+            if (CEN) {
+                const ulonglong2 cm = mcode[mi];
+                uint32_t pc = __popcll(cf.x ^ cm.x);
+                if (a.nwords > 1) pc += __popcll(cf.y ^ cm.y);
+                cen = oor ? cd : fminf((float)pc, cd);
             }
             float res;
             if (METHOD == SM_M_CENSUS) {
                 res = cen;
-            } else if (METHOD == SM_M_CENSUS_GRAD) {
-                float g;
-                if (oor)
-                    g = a.grad_oor;
-                else {
-                    const float dx = fminf(fabsf(fgx[pl] - mgx[mi]), a.grad_trunc);
-                    const float dy = fminf(fabsf(fgy[pl] - mgy[mi]), a.grad_trunc);
-                    if (a.grad_adaptive) {
-                        const float t1 = fwa[pl] * dx;
-                        const float t2 = fwb[pl] * dy;
-                        g = t1 + t2;
-                    } else {
-                        g = dx + dy;
-                    }
-                }
-                const float e0 = c_lut_a[(int)cen];       // expf(-C / lamCen)
-                const float xg = -g / a.lam2;
-                float e1 = 0.f;
-                if (xg >= -17.5f) e1 = dev_expf(xg);      // expf(-G / lamG)
+            } else if (GRAD) {
+                const float dx = fminf(fabsf(fx - mgx[mi]), a.grad_trunc);
+                const float dy = fminf(fabsf(fy - mgy[mi]), a.grad_trunc);
+                const float t1 = wa * dx;
+                const float t2 = wb * dy;
+                const float g = oor ? a.grad_oor : t1 + t2;
+                const float e0 = luta[(int)cen];          // expf(-C / lamCen)
+                const float xg = LAM1 ? -g : -g / a.lam2;
+                const float ex = expf_glibc_core(xg, etab); // expf(-G / lamG)
+                const float e1 = xg >= -17.5f ? ex : 0.f;
                 const float t = 2.0f - e0;
                 res = t - e1;
             } else {
-                int s = 0;
-                if (!oor) {
-                    const uint32_t x = fbgr[pl], y = mbgr[mi];
-                    s = abs((int)(x & 0xff) - (int)(y & 0xff)) + abs((int)((x >> 8) & 0xff) - (int)((y >> 8) & 0xff)) +
-                        abs((int)(x >> 16) - (int)(y >> 16));
-                }
+                const uint32_t y = mbgr[mi];
+                const int s3 = abs((int)(fc & 0xff) - (int)(y & 0xff)) +
+                               abs((int)((fc >> 8) & 0xff) - (int)((y >> 8) & 0xff)) + abs((int)(fc >> 16) - (int)(y >> 16));
                 if (METHOD == SM_M_AD) {
-                    res = oor ? a.ad_trunc : fminf((float)s / 3.0f, a.ad_trunc);
+                    res = oor ? a.ad_trunc : fminf((float)s3 / 3.0f, a.ad_trunc);
                 } else {
-                    const float e0 = oor ? a.ad_oor_exp : c_lut_b[s];
-                    const float e1 = c_lut_a[(int)cen];
+                    const float e0 = oor ? a.ad_oor_exp : lutb[s3];
+                    const float e1 = luta[(int)cen];
                     const float t = 2.0f - e0;
                     res = t - e1;
                 }
@@ -350,7 +367,7 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
 
 size_t cost_smem_bytes(int D) {
     const size_t nm = COST_P + D - 1;
-    return 16 * (COST_P + nm) + 4 * (4 * COST_P + 2 * nm) + 4 * (COST_P + nm);
+    return 16 * (COST_P + nm) + 8 * 32 + 4 * (4 * COST_P + 2 * nm) + 4 * (COST_P + nm) + 4 * (LUT_A_N + LUT_B_N);
 }
 
 // SolveAll with PY_LVL = 1 as a standalone pass (used by the reference-ordered API):
@@ -382,7 +399,8 @@ __global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vm, int16
             bi = d0 + k;
         }
     const float wm = wave_min(bm);
-    const int widx = wave_min_i(bm == wm ? bi : 0x7fffffff);
+    const uint64_t hit = __ballot(bm == wm);   // lowest lane holding the minimum = first index
+    const int widx = __builtin_amdgcn_readlane(bi, (int)__builtin_ctzll(hit));
     if (lane == 0) disp[(size_t)b * npix + wave] = (int16_t)((wm < FLT_MAX) ? widx : -1);
 }
 
@@ -401,14 +419,19 @@ hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st) {
 }
 
 void launch_cost(const CostArgs& a, int method, int n, hipStream_t st) {
-    dim3 grid((a.W + COST_P - 1) / COST_P, a.H, n);
+    dim3 grid((unsigned)((a.W + COST_P - 1) / COST_P * a.H * n));
     dim3 block(64, 4);
     const size_t shm = cost_smem_bytes(a.D);
     switch (method) {
-        case SM_M_CENSUS_GRAD: hipLaunchKernelGGL(k_cost<SM_M_CENSUS_GRAD>, grid, block, shm, st, a); break;
-        case SM_M_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_CENSUS>, grid, block, shm, st, a); break;
-        case SM_M_AD_CENSUS: hipLaunchKernelGGL(k_cost<SM_M_AD_CENSUS>, grid, block, shm, st, a); break;
-        default: hipLaunchKernelGGL(k_cost<SM_M_AD>, grid, block, shm, st, a); break;
+        case SM_M_CENSUS_GRAD:
+            if (a.lam2 == 1.0f)
+                hipLaunchKernelGGL((k_cost<SM_M_CENSUS_GRAD, true>), grid, block, shm, st, a);
+            else
+                hipLaunchKernelGGL((k_cost<SM_M_CENSUS_GRAD, false>), grid, block, shm, st, a);
+            break;
+        case SM_M_CENSUS: hipLaunchKernelGGL((k_cost<SM_M_CENSUS, false>), grid, block, shm, st, a); break;
+        case SM_M_AD_CENSUS: hipLaunchKernelGGL((k_cost<SM_M_AD_CENSUS, false>), grid, block, shm, st, a); break;
+        default: hipLaunchKernelGGL((k_cost<SM_M_AD, false>), grid, block, shm, st, a); break;
     }
 }
 

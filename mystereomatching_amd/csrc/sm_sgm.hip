@@ -44,7 +44,7 @@ struct SgmTile {
     uint32_t fl;  // lane t < T: penalty flags of the pixel of step j0 + t
 };
 
-template <int K, int MODE, int T>
+template <int K, int MODE, int T, bool FULL>
 __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
@@ -127,42 +127,47 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
 #pragma unroll
     for (int k = 0; k < K; k++) Lp[k] = FLT_MAX;
 
+    // All path costs are >= +0 (C >= 0; Lp - m >= 0; Lp[d +/- 1] + (P1 - m) >= 0 because
+    // fl(P1 - m) >= -m; P2 > 0), so every min below is an exact unsigned min on the bit patterns.
+    // Out-of-range neighbours (d - 1 < 0, d + 1 >= D) hold FLT_MAX from the DPP shift's bound
+    // value or the padded lanes; FLT_MAX + (P1 - m) never undercuts P2 <= 3, so those terms
+    // cannot win the min and need no separate select.
     auto step = [&](const SgmTile<K, T>& t, int s, int j, bool start) {
         float L[K];
         if (start) {
 #pragma unroll
-            for (int k = 0; k < K; k++) L[k] = val[k] ? t.c[s][k] : FLT_MAX;
+            for (int k = 0; k < K; k++) L[k] = (FULL || val[k]) ? t.c[s][k] : FLT_MAX;
         } else {
             const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)t.fl, s);
             const bool pen = (fl >> dir) & 1u;
             const float P1 = pen ? p1r : p1, P2 = pen ? p2r : p2;
             float lm = Lp[0];
 #pragma unroll
-            for (int k = 1; k < K; k++) lm = fminf(lm, Lp[k]);
-            const float m = wave_min(lm);
+            for (int k = 1; k < K; k++) lm = fmin_pos(lm, Lp[k]);
+            const float m = wave_min_pos(lm);           // wave-uniform
             const float P1m = P1 - m;
             const float left = dpp_shr1<K>(Lp[K - 1]);
             const float right = dpp_shl1<K>(Lp[0]);
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                const int d = d0 + k;
                 const float prev = (k == 0) ? left : Lp[k - 1];
                 const float next = (k == K - 1) ? right : Lp[k + 1];
                 const float S1 = Lp[k] - m;
-                const float S2 = d - 1 >= 0 ? prev + P1m : FLT_MAX;
-                const float S3 = d + 1 < D ? next + P1m : FLT_MAX;
-                const float mm = fminf(fminf(S1, S2), fminf(S3, P2));
-                L[k] = val[k] ? t.c[s][k] + mm : FLT_MAX;
+                const float S2 = prev + P1m;
+                const float S3 = next + P1m;
+                const float mm = fmin_pos(fmin_pos(S1, S2), fmin_pos(S3, P2));
+                const float Lk = t.c[s][k] + mm;
+                L[k] = (FULL || val[k]) ? Lk : FLT_MAX;
             }
         }
         float f[K];
 #pragma unroll
         for (int k = 0; k < K; k++) {
             const float prev = (MODE & SGM_FIRST) ? 0.f : t.acc[s][k];
-            f[k] = val[k] ? prev + L[k] : FLT_MAX;   // sum += Lr[num] (cpp:2046-2049)
+            f[k] = prev + L[k];   // sum += Lr[num] (cpp:2046-2049); padded lanes stay FLT_MAX
         }
         if (MODE & SGM_LAST) {
-            if (a.keep_final) {
+            if (MODE & SGM_KEEP) {
 #pragma unroll
                 for (int k = 0; k < K; k++) fp[k][j * sst[k]] = f[k];
             }
@@ -174,9 +179,13 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
                     bm = f[k];
                     bi = d0 + k;
                 }
-            const float wm = wave_min(bm);
-            const int widx = wave_min_i((bm == wm && d0 < D) ? bi : 0x7fffffff);
-            dacc = (lane == s) ? ((wm < FLT_MAX) ? widx : -1) : dacc;
+            // first minimum: lowest lane holding the wave minimum, then that lane's first index
+            // (padded lanes hold FLT_MAX and only match when every cost is FLT_MAX -> -1)
+            const float wm = wave_min_pos(bm);
+            const uint64_t hit = __ballot(bm == wm);
+            const int widx = __builtin_amdgcn_readlane(bi, (int)__builtin_ctzll(hit));
+            const int dsel = (wm < FLT_MAX) ? widx : -1;
+            dacc = (lane == s) ? dsel : dacc;
         } else {
 #pragma unroll
             for (int k = 0; k < K; k++) ap[k][j * sst[k]] = f[k];
@@ -209,17 +218,30 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
     }
 }
 
-template <int K>
-static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
+template <int K, bool FULL>
+static void launch_kf(const SgmArgs& a, int mode, int n, hipStream_t st) {
     const int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
     dim3 grid((nlines + 3) / 4, n);
     constexpr int T = K >= 8 ? 2 : 16 / K;
+    if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
     switch (mode) {
-        case SGM_FIRST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST, T>), grid, dim3(256), 0, st, a); break;
-        case SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_LAST, T>), grid, dim3(256), 0, st, a); break;
-        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST, T>), grid, dim3(256), 0, st, a); break;
-        default: hipLaunchKernelGGL((k_sgm<K, 0, T>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST, T, FULL>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_LAST, T, FULL>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST | SGM_KEEP: hipLaunchKernelGGL((k_sgm<K, SGM_LAST | SGM_KEEP, T, FULL>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST, T, FULL>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST | SGM_KEEP:
+            hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST | SGM_KEEP, T, FULL>), grid, dim3(256), 0, st, a);
+            break;
+        default: hipLaunchKernelGGL((k_sgm<K, 0, T, FULL>), grid, dim3(256), 0, st, a); break;
     }
+}
+
+template <int K>
+static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    if (a.D == 64 * K)
+        launch_kf<K, true>(a, mode, n, st);
+    else
+        launch_kf<K, false>(a, mode, n, st);
 }
 
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {

@@ -75,11 +75,13 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    # SM_HIP_LIB: an alternative build of the same library (tuning sweeps, tools/build_variants.sh)
+    path = os.environ.get("SM_HIP_LIB") or LIB_PATH
+    if not os.path.exists(path):
         raise FileNotFoundError(
-            f"{LIB_PATH} is missing; build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            f"{path} is missing; build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C mystereomatching_amd/csrc`")
-    lib = C.CDLL(LIB_PATH)
+    lib = C.CDLL(path)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res

@@ -316,7 +316,6 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w, const Bufs& B) {
     a.W = p.cols;
     a.D = p.num_disparities;
     a.lag = cbca_lag(p);
-    a.ring = 2 * a.lag + 2;
     a.scale = w;
     a.apply_scale = 0;
     const double bytes = (double)n * c->nvol * 8.0;

@@ -51,13 +51,40 @@ __device__ __forceinline__ uint32_t shr1_in(uint32_t v, uint32_t in) {  // lane 
 // 5-6 waves per CU the LDS rings allow, so PF tiles of loads are kept in flight; the loads of PF
 // tiles plus the stores of one stay below the 63 of vmcnt (V sweeps load one right-arm word per
 // position and set, hence their shorter tiles).
+// (Overridable at build time for tuning sweeps, see tools/build_variants.sh.)
+#ifndef SM_CB_T_SCAN_H
+#define SM_CB_T_SCAN_H 24
+#endif
+#ifndef SM_CB_T_SCAN_V
+#define SM_CB_T_SCAN_V 24
+#endif
+#ifndef SM_CB_T_NORM_H
+#define SM_CB_T_NORM_H 24
+#endif
+#ifndef SM_CB_T_NORM_V
+#define SM_CB_T_NORM_V 16
+#endif
+#ifndef SM_CB_PF_SCAN_H
+#define SM_CB_PF_SCAN_H 1
+#endif
+#ifndef SM_CB_PF_SCAN_V
+#define SM_CB_PF_SCAN_V 1
+#endif
+#ifndef SM_CB_PF_NORM_H
+#define SM_CB_PF_NORM_H 1
+#endif
+#ifndef SM_CB_PF_NORM_V
+#define SM_CB_PF_NORM_V 1
+#endif
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
-    return mode == CB_SCAN || (horiz && mode == CB_NORM) ? 16 : 8;
+    return mode == CB_SCAN ? (horiz ? SM_CB_T_SCAN_H : SM_CB_T_SCAN_V)
+                           : (mode == CB_NORM ? (horiz ? SM_CB_T_NORM_H : SM_CB_T_NORM_V) : 8);
 }
 template <bool HORIZ, int MODE>
 struct CbCfg {
     static constexpr int T = cbca_tile(HORIZ, MODE);
-    static constexpr int PF = (!HORIZ && MODE != CB_NORM) ? 1 : 2;
+    static constexpr int PF = MODE == CB_SCAN ? (HORIZ ? SM_CB_PF_SCAN_H : SM_CB_PF_SCAN_V)
+                                              : (MODE == CB_NORM ? (HORIZ ? SM_CB_PF_NORM_H : SM_CB_PF_NORM_V) : (HORIZ ? 2 : 1));
     // arm sets: 0 = pass pair at i (= j - lag), 1 = perpendicular pair at j, 2 = pass pair at j - 2 lag
     static constexpr int NSETS = MODE == CB_SCAN ? 1 : (MODE == CB_NORM ? 2 : 3);
 };
@@ -68,7 +95,8 @@ __host__ __device__ inline int cbca_ring(int lag, bool horiz, int mode) {
     const int T = cbca_tile(horiz, mode);
     return (2 * lag + T + 1 + T - 1) / T * T;
 }
-// dynamic LDS in 4-byte words: S ring(s) of ring x 64 floats, then the u16 area ring
+// dynamic LDS in 4-byte words: S ring(s) of ring x 64 floats, then the u16 area ring (6 bytes
+// per slot and lane; 8-byte {S, area} records were measured slower: one wave less per CU)
 __host__ __device__ inline int cbca_smem_words(int lag, bool horiz, int mode) {
     const int ring = cbca_ring(lag, horiz, mode);
     const int floats = mode == CB_NORM_SCAN ? 2 : 1;
@@ -323,7 +351,7 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.ra = (uint16_t*)(smem + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
     L.scale = a.scale;
     {   // zero the rings: reads of positions before the line start then yield S = 0, area = 0
-        const int words = (int)(cbca_smem_words(a.lag, HORIZ, MODE));
+        const int words = cbca_smem_words(a.lag, HORIZ, MODE);
         for (int w = L.lane; w < words; w += 64) smem[w] = 0.f;
         __syncthreads();  // one wave; also orders the float stores before the u16 ring reads
     }
@@ -357,14 +385,12 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     }
 }
 
-size_t cbca_smem_bytes(int lag, bool horiz, int mode) { return 4 * cbca_smem_words(lag, horiz, mode); }
-
 template <bool HORIZ, int MODE, bool SCALE>
 static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
     const int nchunks = (a.D + 63) / 64;
     const int lines = HORIZ ? a.H : a.W;
     dim3 grid(lines * nchunks * n);
-    const size_t shm = cbca_smem_bytes(a.lag, HORIZ, MODE);
+    const size_t shm = 4 * (size_t)cbca_smem_words(a.lag, HORIZ, MODE);
     if (a.D % 64 == 0)
         hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE>), grid, dim3(64), shm, st, a);
     else

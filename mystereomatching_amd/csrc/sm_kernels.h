@@ -18,7 +18,7 @@ struct PrepArgs {
     ulonglong2* code;           // [n][2][H][W]
     float* gx;
     float* gy;
-    uint8_t* arms;              // [n][2][H][W][4]
+    uint8_t* arms;              // [n][view][plane][H][W] u32: plane 0 = L | R<<16, plane 1 = U | D<<16
     uint8_t* flags;             // [n][H][W] (left view only)
     int H, W, rv, ru, ring;
     int L, L_out, C_D, C_D_out, minL, cor_thres;
@@ -30,7 +30,7 @@ struct CostArgs {
     const ulonglong2* code;     // [n][2][H][W]
     const float* gx;            // [n][2][H][W]
     const float* gy;
-    const uint8_t* arms;        // [n][2][H][W][4]
+    const uint8_t* arms;        // [n][view][plane][H][W] u32: plane 0 = L | R<<16, plane 1 = U | D<<16
     const uint8_t* bgr;         // [n][2][H][W][3]
     int H, W, D, view, nwords;
     float census_default;       // codeLength * truncRat (h:938)
@@ -44,9 +44,9 @@ struct CostArgs {
 struct CbcaArgs {
     float* vm;                  // [n][H][W][D], in place
     float* dummy;               // 64 floats: private slots for lanes past D
-    const uint32_t* arms;       // [n][2][H][W] packed L|R<<8|U<<16|D<<24
+    const uint32_t* arms;       // [n][view][plane][H][W]: plane 0 = L | R<<16, plane 1 = U | D<<16
     int H, W, D;
-    int lag, ring;              // lag = max arm length, ring = 2*lag + 2
+    int lag;                    // max arm length (the ring size is derived in sm_cbca.hip)
     int apply_scale;
     float scale;                // SolveAll weight (fused into the last normalising pass)
 };

@@ -1,10 +1,10 @@
 // sm_kernels.hip — hand-written gfx950 kernels for the census / CBCA / SGM / WTA hot path.
 //
-// Layout in HBM (per pair b, all packed, see DESIGN.md §3):
+// Layout in HBM (per pair b, all packed, see DESIGN.md §4):
 //   bgr   [b][view][H][W][3] u8  gray [b][view][H][W] u8   (view 0 = left, 1 = right)
 //   code  [b][view][H][W] ulonglong2   (census words 0,1; genCensusCode_NC_Sur h:867-934)
 //   gx,gy [b][view][H][W] f32    (calGrad / calGrad_y cpp:271-386)
-//   arms  [b][view][H][W] u8x4   (L,R,U,D; calHorVerDis cpp:2959-3050)
+//   arms  [b][view][plane][H][W] u32 (L | R<<16, U | D<<16; calHorVerDis cpp:2959-3050)
 //   vm    [b][H][W][D] f32       (d innermost, as the reference's CV_32FC(D), cpp:2080)
 //   acc   [b][H][W][D] f32       (SGM path sum in path order, gen_sgm_vm cpp:2031-2056)
 //   disp  [b][H][W] i16          (DP[0], gen_dispFromVm cpp:3928-3967)

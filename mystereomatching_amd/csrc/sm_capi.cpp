@@ -44,6 +44,8 @@ struct sm_ctx {
     float* gx = nullptr;        // [cap][2][npix]
     float* gy = nullptr;
     uint8_t* arms = nullptr;    // [cap][2 views][2 planes][npix] u32: (L | R<<16), (U | D<<16)
+    uint8_t* arms_alloc = nullptr;  // arms - front pad of 2 * lag rows (CBCA V sweeps read there)
+    size_t arms_bytes = 0;
     float* vm0 = nullptr;       // [cap][npix][D]
     float* vm1 = nullptr;       // [cap][npix][D] (right view, optional)
     float* acc = nullptr;       // [cap][npix][D]
@@ -187,7 +189,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 }
 
 void free_all(sm_ctx* c) {
-    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms, c->vm0, c->vm1, c->acc, c->disp, c->dummy, c->flags, c->px};
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp, c->dummy, c->flags, c->px};
     for (void* q : ptrs)
         if (q) hipFree(q);
     for (auto& r : c->recs) {
@@ -316,6 +318,8 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w, const Bufs& B) {
     a.W = p.cols;
     a.D = p.num_disparities;
     a.lag = cbca_lag(p);
+    a.vm_end = c->vm0 + (size_t)c->cap * c->nvol;
+    a.arms_end = (const uint32_t*)(c->arms + c->arms_bytes);
     a.scale = w;
     a.apply_scale = 0;
     const double bytes = (double)n * c->nvol * 8.0;
@@ -494,7 +498,12 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->code, cap * 2 * c->npix))) return s;
     if ((s = dalloc(c, &c->gx, cap * 2 * c->npix))) return s;
     if ((s = dalloc(c, &c->gy, cap * 2 * c->npix))) return s;
-    if ((s = dalloc(c, &c->arms, cap * 2 * 2 * c->npix * 4))) return s;
+    {
+        const size_t pad = ((size_t)2 * cbca_lag(*p) * p->cols * 4 + 255) / 256 * 256;
+        c->arms_bytes = cap * 2 * 2 * c->npix * 4;
+        if ((s = dalloc(c, &c->arms_alloc, pad + c->arms_bytes))) return s;
+        c->arms = c->arms_alloc + pad;
+    }
     if ((s = dalloc(c, &c->vm0, cap * c->nvol))) return s;
     if (p->compute_right_view)
         if ((s = dalloc(c, &c->vm1, cap * c->nvol))) return s;

@@ -118,13 +118,22 @@ struct CbLine {
     static constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
     using Tile = CbTile<HORIZ, T, NSETS>;
 
-    const float* xbase;       // FULL: chunk base (uniform), lane offset added; else per-lane base
-    float* obase;
-    int vstride;              // floats between consecutive positions
+    // Volume and V-sweep arm accesses are buffer instructions: the tile's first position in the
+    // resource base, lane + k * stride in a loop-invariant VGPR.  Loads are not clamped: the
+    // resource's range ends at the allocation's end (reads past it return 0; those positions are
+    // never output) and the arm planes carry a 2 * lag row front pad for set positions < 0.
+    const char* xline;        // byte address of (line, position 0, chunk's first disparity)
+    const char* xend;         // end of the volume allocation
+    const char* aend;         // end of the arm allocation
+    uint32_t xo[T];           // lane's load offset of tile position k (lanes past D re-read D - 1)
+    uint32_t ao[HORIZ ? 1 : T];  // V: lane's arm offset (column u - d) of tile position k
+    uint32_t ov;              // lane's store offset (lanes past D: out of range, dropped)
+    uint32_t vsb;             // bytes between consecutive positions
     int lane;
-    const uint32_t* A0[NSETS];  // left / right arm-pair planes for each set, at the line's first pixel
-    const uint32_t* A1[NSETS];
-    int pstride, line, len, lag, ring, d;
+    const uint32_t* A0[NSETS];  // left-image arm-pair plane of each set, at the line's first pixel
+    const uint32_t* A1[NSETS];  // H: right-image plane at the line's first pixel
+    const char* A1v[NSETS];     // V: right-image plane, row 0 (uniform)
+    int pstride, line, len, lag, ring;
     int c64;                  // first disparity of the chunk
     uint32_t vmask;           // V sweeps: all ones if u - d >= 0 else 0 (constant along the line)
     uint32_t sh[NSETS];       // H sweeps: shifted right-arm window per set
@@ -139,28 +148,28 @@ struct CbLine {
     __device__ __forceinline__ int set_off(int s) const { return s == 0 ? lag : (s == 1 ? 0 : 2 * lag); }
     __device__ __forceinline__ static int clampi(int k, int n) { return k < 0 ? 0 : (k >= n ? n - 1 : k); }
 
-    __device__ __forceinline__ float ldx(int pos) const {
-        return FULL ? xbase[clampi(pos, len) * vstride + lane] : xbase[clampi(pos, len) * vstride];
+    // resource for the tile whose first position is pos0 (may lie before the line: only
+    // positions inside it are ever stored)
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(int pos0) const {
+        return buf_rsrc(xline + (long)pos0 * (long)vsb);
     }
-    __device__ __forceinline__ void store(int pos, float v) const {
-        if (FULL)
-            obase[pos * vstride + lane] = v;
-        else if (d < 0x7fffffff)
-            obase[pos * vstride] = v;
+    __device__ __forceinline__ static __amdgpu_buffer_rsrc_t bounded_rsrc(const char* base, const char* end) {
+        const long room = end - base;
+        return buf_rsrc(base, room <= 0 ? 0 : (room > 0x7fffffffL ? 0x7fffffff : (int)room));
     }
-
-    // uniform base of the output row for positions pos0 .. pos0+T-1 (FULL chunks)
-    __device__ __forceinline__ float* ob_tile(int pos0) const { return FULL ? obase + (long)pos0 * vstride : obase; }
-    __device__ __forceinline__ void store_tile(float* tb, int pos0, int k, float v) const {
+    __device__ __forceinline__ void store_tile(const __amdgpu_buffer_rsrc_t& r, int k, float v) const {
         if (FULL)
-            tb[k * vstride + lane] = v;
+            buf_st(r, xo[k], 0, v);
         else
-            store(pos0 + k, v);
+            buf_st(r, ov, (uint32_t)k * vsb, v);
     }
 
+    // Tile loads: positions past the line end read the next line (or 0 past the allocation);
+    // their prefix values are never read.
     __device__ __forceinline__ void load(Tile& t, int j0) const {
+        const __amdgpu_buffer_rsrc_t rx = bounded_rsrc(xline + (long)j0 * (long)vsb, xend);
 #pragma unroll
-        for (int k = 0; k < T; k++) t.x[k] = ldx(j0 + k);
+        for (int k = 0; k < T; k++) t.x[k] = buf_ld(rx, xo[k], 0);
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             const int base = j0 - set_off(s);
@@ -171,8 +180,9 @@ struct CbLine {
                 const uint32_t v = A1[s][clampi(q, len)];
                 t.a1v[s] = (q >= 0 && q < len) ? v : 0u;
             } else {
+                const __amdgpu_buffer_rsrc_t ra1 = bounded_rsrc(A1v[s] + (long)base * (long)(pstride * 4), aend);
 #pragma unroll
-                for (int k = 0; k < T; k++) t.a1[s][k] = A1[s][clampi(base + k, len) * pstride];
+                for (int k = 0; k < T; k++) t.a1[s][k] = buf_ld_u32(ra1, ao[k], 0);
             }
         }
     }
@@ -224,7 +234,7 @@ struct CbLine {
         const int si0 = uwrap(ws - lag);        // slot of i = j0 - lag
         const int s20 = uwrap(ws - 2 * lag);    // slot of i2 = j0 - 2 lag
         const int i0 = j0 - lag;
-        float* ob = ob_tile(i0);
+        const __amdgpu_buffer_rsrc_t ob = tile_rsrc(i0);
         // phase A: inputs j0 .. j0+T-1 (+ arm windows)
 #pragma unroll
         for (int k = 0; k < T; k++) {
@@ -259,11 +269,11 @@ struct CbLine {
             const float diff = shv[k] - stv[k];
             const bool live = !GUARD || (unsigned)(i0 + k) < (unsigned)len;
             if (MODE == CB_SCAN) {
-                if (live) store_tile(ob, i0, k, diff);
+                if (live) store_tile(ob, k, diff);
             } else {
                 const uint32_t area = (ahv[k] - atv[k]) & 0xffffu;
                 if (MODE == CB_NORM) {
-                    if (live) store_tile(ob, i0, k, finish_norm(diff, area));
+                    if (live) store_tile(ob, k, finish_norm(diff, area));
                 } else {
                     float y = diff / (float)area;                 // final value of iteration k at i
                     if (GUARD) y = (i0 + k >= 0) ? y : 0.f;       // nothing accumulates before the line
@@ -283,10 +293,10 @@ struct CbLine {
                 s2t[k] = r2[dn(hs - (hd + tl + 1)) * 64 + lane];
             }
             const int i20 = j0 - 2 * lag;
-            float* ob2 = ob_tile(i20);
+            const __amdgpu_buffer_rsrc_t ob2 = tile_rsrc(i20);
 #pragma unroll
             for (int k = 0; k < T; k++)
-                if (!GUARD || (unsigned)(i20 + k) < (unsigned)len) store_tile(ob2, i20, k, s2h[k] - s2t[k]);
+                if (!GUARD || (unsigned)(i20 + k) < (unsigned)len) store_tile(ob2, k, s2h[k] - s2t[k]);
         }
         ws = (ws + T == ring) ? 0 : ws + T;
     }
@@ -315,22 +325,20 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     const int lc = blk - b * per_pair;
     L.line = lc / nchunks;
     const int chunk = lc - L.line * nchunks;
-    L.d = chunk * 64 + L.lane;
     const size_t npix = (size_t)a.H * a.W;
     const size_t first_pix = HORIZ ? (size_t)L.line * a.W : (size_t)L.line;
     L.pstride = HORIZ ? 1 : a.W;
-    L.vstride = L.pstride * a.D;
-    float* chunk_base = a.vm + ((size_t)b * npix + first_pix) * a.D + (size_t)chunk * 64;
-    if (FULL) {
-        L.xbase = chunk_base;
-        L.obase = chunk_base;
-    } else {
-        const bool valid = L.d < a.D;
-        L.xbase = valid ? chunk_base + L.lane : a.vm + ((size_t)b * npix + first_pix) * a.D + (a.D - 1);
-        L.obase = chunk_base + L.lane;
-        if (!valid) L.d = 0x7fffffff;  // store() skips these lanes
-    }
+    L.vsb = (uint32_t)(L.pstride * a.D * 4);
+    L.xline = (const char*)(a.vm + ((size_t)b * npix + first_pix) * a.D + (size_t)chunk * 64);
     const int dl = chunk * 64 + L.lane;  // true disparity (also for masked lanes)
+    {
+        const uint32_t xv = FULL ? (uint32_t)L.lane * 4u : (uint32_t)min(L.lane, a.D - 1 - chunk * 64) * 4u;
+#pragma unroll
+        for (int k = 0; k < T; k++) L.xo[k] = xv + (uint32_t)k * L.vsb;
+        L.ov = (FULL || dl < a.D) ? (uint32_t)L.lane * 4u : 0x80000000u;
+    }
+    L.xend = (const char*)a.vm_end;
+    L.aend = (const char*)a.arms_end;
     // arm planes: [b][view][plane][npix]; plane 0 = (L | R<<16), plane 1 = (U | D<<16)
     const int pass_plane = HORIZ ? 0 : 1, perp_plane = HORIZ ? 1 : 0;
     const uint32_t* planeL = a.arms + ((size_t)b * 4) * npix + first_pix;
@@ -338,8 +346,14 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     for (int s = 0; s < NSETS; s++) {
         const int pl = (s == 1) ? perp_plane : pass_plane;
         L.A0[s] = planeL + (size_t)pl * npix;
-        L.A1[s] = planeL + (size_t)(2 + pl) * npix + (HORIZ ? 0 : -(long)min(dl, L.line));
+        L.A1[s] = planeL + (size_t)(2 + pl) * npix;
+        L.A1v[s] = (const char*)(a.arms + ((size_t)b * 4 + 2 + pl) * npix);
         L.sh[s] = 0u;
+    }
+    if (!HORIZ) {
+        const uint32_t col = (uint32_t)(L.line - min(dl, L.line)) * 4u;  // u - d, clamped (vmask zeroes)
+#pragma unroll
+        for (int k = 0; k < (HORIZ ? 1 : T); k++) L.ao[k] = col + (uint32_t)(k * a.W * 4);
     }
     L.vmask = (!HORIZ && L.line - dl < 0) ? 0u : 0xffffffffu;
     L.c64 = chunk * 64;

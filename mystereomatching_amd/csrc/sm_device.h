@@ -81,6 +81,21 @@ __device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Buffer-instruction access (gfx9 resource word 3 = 0x00020000, 32-bit data).  The range limit
+// is 2^31 - 1 bytes, so a lane offset of 0x80000000 turns its load into 0 and drops its store.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int num_bytes = 0x7fffffff) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, num_bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ uint32_t buf_ld_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, 0);
+}
+
 // wave64 cross-lane helpers (device only)
 // DPP controls (GFX9 encoding).
 enum : int {

@@ -45,6 +45,8 @@ struct CbcaArgs {
     float* vm;                  // [n][H][W][D], in place
     float* dummy;               // 64 floats: private slots for lanes past D
     const uint32_t* arms;       // [n][view][plane][H][W]: plane 0 = L | R<<16, plane 1 = U | D<<16
+    const float* vm_end;        // end of the volume allocation (reads past it return 0)
+    const uint32_t* arms_end;   // end of the arm allocation (which has a 2 * lag row front pad)
     int H, W, D;
     int lag;                    // max arm length (the ring size is derived in sm_cbca.hip)
     int apply_scale;

@@ -130,8 +130,8 @@ struct CbLine {
     uint32_t ov;              // lane's store offset (lanes past D: out of range, dropped)
     uint32_t vsb;             // bytes between consecutive positions
     int lane;
-    const uint32_t* A0[NSETS];  // left-image arm-pair plane of each set, at the line's first pixel
-    const uint32_t* A1[NSETS];  // H: right-image plane at the line's first pixel
+    __amdgpu_buffer_rsrc_t A0r[NSETS];  // left-image arm-pair plane of each set over the line
+    __amdgpu_buffer_rsrc_t A1r[NSETS];  // H: right-image plane over the line
     const char* A1v[NSETS];     // V: right-image plane, row 0 (uniform)
     int pstride, line, len, lag, ring;
     int c64;                  // first disparity of the chunk
@@ -170,15 +170,18 @@ struct CbLine {
         const __amdgpu_buffer_rsrc_t rx = bounded_rsrc(xline + (long)j0 * (long)vsb, xend);
 #pragma unroll
         for (int k = 0; k < T; k++) t.x[k] = buf_ld(rx, xo[k], 0);
+        // lane-vector arm loads: positions outside the line read 0 (an out-of-range offset) --
+        // for the right image's arms that is the reference's zeroed intersection when u - d < 0.
+        // The offset is a select, never a wrapped negative sum: the range check does not wrap,
+        // and the compiler would otherwise move constant parts of a sum into the immediate field.
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             const int base = j0 - set_off(s);
-            const int ql = clampi(base + lane, len) * pstride;
-            t.a0[s] = A0[s][ql];
+            const int p0 = base + lane;
+            t.a0[s] = buf_ld_u32(A0r[s], (unsigned)p0 < (unsigned)len ? (uint32_t)(p0 * pstride) * 4u : 0x80000000u, 0);
             if (HORIZ) {
                 const int q = base + lane - c64;  // right pixel of lane 0 at position base + lane
-                const uint32_t v = A1[s][clampi(q, len)];
-                t.a1v[s] = (q >= 0 && q < len) ? v : 0u;
+                t.a1v[s] = buf_ld_u32(A1r[s], (unsigned)q < (unsigned)len ? (uint32_t)q * 4u : 0x80000000u, 0);
             } else {
                 const __amdgpu_buffer_rsrc_t ra1 = bounded_rsrc(A1v[s] + (long)base * (long)(pstride * 4), aend);
 #pragma unroll
@@ -345,8 +348,9 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
 #pragma unroll
     for (int s = 0; s < NSETS; s++) {
         const int pl = (s == 1) ? perp_plane : pass_plane;
-        L.A0[s] = planeL + (size_t)pl * npix;
-        L.A1[s] = planeL + (size_t)(2 + pl) * npix;
+        const int line_bytes = (((HORIZ ? a.W : a.H) - 1) * L.pstride + 1) * 4;
+        L.A0r[s] = buf_rsrc(planeL + (size_t)pl * npix, line_bytes);
+        L.A1r[s] = buf_rsrc(planeL + (size_t)(2 + pl) * npix, line_bytes);
         L.A1v[s] = (const char*)(a.arms + ((size_t)b * 4 + 2 + pl) * npix);
         L.sh[s] = 0u;
     }

@@ -17,14 +17,14 @@ from collections import defaultdict
 
 
 def profile_name(sym: str, seen: dict) -> str:
-    m = re.search(r"k_cbca<(true|false), (\d), (true|false)>", sym)
+    m = re.search(r"k_cbca<(true|false), (\d)[,>]", sym)
     if m:
         h = m.group(1) == "true"
         mode = {"0": "scan", "1": "norm", "2": "norm_scan"}[m.group(2)]
         return f"cbca_{'h' if h else 'v'}_{mode}"
-    m = re.search(r"k_sgm<\d+, (\d), \d+>", sym)
+    m = re.search(r"k_sgm<\d+, (\d+),", sym)
     if m:
-        mode = int(m.group(1))
+        mode = int(m.group(1))  # SGM_FIRST = 1, SGM_LAST = 2, SGM_KEEP = 4
         if mode & 2:
             return "sgm_last_wta"
         if mode & 1:

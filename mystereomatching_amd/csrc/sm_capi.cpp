@@ -504,11 +504,13 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->arms_alloc, pad + c->arms_bytes))) return s;
         c->arms = c->arms_alloc + pad;
     }
-    if ((s = dalloc(c, &c->vm0, cap * c->nvol))) return s;
+    // volumes carry a 4 KiB tail: vectorised SGM lanes past D read (never write) into it
+    const size_t vpad = 1024;
+    if ((s = dalloc(c, &c->vm0, cap * c->nvol + vpad))) return s;
     if (p->compute_right_view)
-        if ((s = dalloc(c, &c->vm1, cap * c->nvol))) return s;
+        if ((s = dalloc(c, &c->vm1, cap * c->nvol + vpad))) return s;
     if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
-        if ((s = dalloc(c, &c->acc, cap * c->nvol))) return s;
+        if ((s = dalloc(c, &c->acc, cap * c->nvol + vpad))) return s;
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
     if ((s = dalloc(c, &c->dummy, 64))) return s;
     if ((s = dalloc(c, &c->flags, cap * c->npix))) return s;

@@ -63,6 +63,7 @@ struct SgmArgs {
     int H, W, D, rv, ru, dir;
     float p1, p2;
     int cor_thres, redu, keep_final;
+    int n;                      // pairs in the launch
 };
 
 hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st);

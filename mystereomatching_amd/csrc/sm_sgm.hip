@@ -20,6 +20,7 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sm_device.h"
 #include "sm_kernels.h"
@@ -218,6 +219,236 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Straight paths (rv == 0 or ru == 0) with D % 4 == 0: four lines per wave, one DPP row of 16
+// lanes per line, K = 4 * KV consecutive disparities per lane.  Every step of a wave then moves
+// 4 x 256 B per volume with dwordx4 accesses (uniform tile base + 32-bit lane offset), the path minimum is a 4-stage DPP row
+// reduction, d +/- 1 neighbours cross lanes with row_shr / row_shl (whose row boundaries are
+// the line boundaries), and the colour-difference flag of each line's pixel reaches its row
+// with one ds_bpermute.  Arithmetic and its order are those of k_sgm.
+// ---------------------------------------------------------------------------------------
+enum : int { DPP_ROW_SHL1 = 0x101, DPP_ROW_SHR1 = 0x111 };
+
+template <int CTRL>
+__device__ __forceinline__ float row_shift(float v) {  // lane l <- lane l -/+ 1 within its row; FLT_MAX at the row end
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, FLT_MAX),
+                                                                 __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t row_umin(uint32_t v) {  // every lane: min over its row of 16
+    v = umin_dpp<DPP_QUAD_1032>(v);
+    v = umin_dpp<DPP_QUAD_2301>(v);
+    v = umin_dpp<DPP_ROW_HALF_MIRROR>(v);
+    return umin_dpp<DPP_ROW_MIRROR>(v);
+}
+
+template <int KV, int T>
+struct RowTile {
+    float c[T][4 * KV];
+    float acc[T][4 * KV];
+    uint32_t fl;  // lane l16 < T: flags of the row's pixel at step j0 + l16
+};
+
+template <int KV, int MODE, int T, bool FULLC>
+__global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
+    constexpr int K = 4 * KV;
+    const int lane = threadIdx.x & 63, row = lane >> 4, l16 = lane & 15;
+    const int H = a.H, W = a.W, D = a.D;
+    const bool vert = a.ru == 0;                      // lines are columns
+    const bool neg = vert ? a.rv > 0 : a.ru > 0;      // walk starts at the far end
+    const int nl = vert ? W : H, steps = vert ? H : W;
+    const int wpp = (nl + 3) >> 2;
+    // wave index made provably uniform: buffer resources must live in SGPRs (a VGPR-resident
+    // resource makes the compiler wrap every access in a readfirstlane loop)
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256 + threadIdx.x) >> 6));
+    const int b = wave / wpp;
+    if (b >= a.n) return;                             // wave-uniform
+    const int w = wave - b * wpp;
+    const int line0 = 4 * w;
+    const bool line_ok = line0 + row < nl;
+    const int line = line_ok ? line0 + row : nl - 1;
+    const size_t npix = (size_t)H * W;
+    const long step_px = vert ? W : 1;                // pixels between consecutive steps
+    const long line_px = vert ? 1 : W;                // pixels between consecutive lines
+    // pixel of (line, step j) relative to the pair: vert (v, u) = (neg ? H-1-j : j, line)
+    auto pix = [&](int ln, int j) -> long {
+        const int t = neg ? steps - 1 - j : j;
+        return vert ? (long)t * W + ln : (long)ln * W + t;
+    };
+    const int d0 = l16 * K;
+    const uint32_t rowoff = (uint32_t)((line - line0) * line_px * D * 4);
+    uint32_t voff[KV];                                 // lane byte offset of each 4-disparity chunk
+    bool cval[KV];                                     // chunk inside D (D % 4 == 0: all or nothing)
+#pragma unroll
+    for (int c = 0; c < KV; c++) {
+        cval[c] = d0 + 4 * c < D;
+        voff[c] = rowoff + (uint32_t)(d0 + 4 * c) * 4u;  // chunks past D read the next pixel (padded allocation)
+    }
+    const bool st_ok = line_ok;                        // rows past the last line never store
+    const uint32_t sstride = (uint32_t)(step_px * D * 4);
+    const float* vmp = a.vm + (size_t)b * npix * D;
+    float* accp = a.acc + (size_t)b * npix * D;
+    const uint8_t* flp = a.flags + (size_t)b * npix;
+    int16_t* dp = a.disp + (size_t)b * npix;
+    const float p1 = a.p1, p2 = a.p2;
+    const float p1r = p1 / (float)a.redu, p2r = p2 / (float)a.redu;
+    const int dir = a.dir;
+
+    // tile geometry: the lowest-address pixel of steps j0 .. j0+T-1 (clamped to the line) is the
+    // resource base; step s sits at soff(s) bytes above it
+    // (prefetched tiles may start past the line end: every step clamps to the last pixel, so no
+    // address ever leaves the line)
+    auto tile_base = [&](int j0) -> long { return pix(line0, neg ? min(j0 + T - 1, steps - 1) : min(j0, steps - 1)); };
+    auto soff = [&](int j0, int s) -> uint32_t {
+        const int js = min(j0 + s, steps - 1);
+        const int rel = neg ? min(j0 + T - 1, steps - 1) - js : js - min(j0, steps - 1);
+        return (uint32_t)rel * sstride;
+    };
+    auto load = [&](RowTile<KV, T>& t, int j0) {
+        const long bp = tile_base(j0);
+        const char* rc = (const char*)(vmp + bp * D);
+        const char* ra = (const char*)(accp + bp * D);
+#pragma unroll
+        for (int s = 0; s < T; s++) {
+            const uint32_t so = soff(j0, s);
+#pragma unroll
+            for (int c = 0; c < KV; c++) {
+                const float4 v = *(const float4*)(rc + so + voff[c]);
+                t.c[s][4 * c + 0] = v.x;
+                t.c[s][4 * c + 1] = v.y;
+                t.c[s][4 * c + 2] = v.z;
+                t.c[s][4 * c + 3] = v.w;
+                if (!(MODE & SGM_FIRST)) {
+                    const float4 q = *(const float4*)(ra + so + voff[c]);
+                    t.acc[s][4 * c + 0] = q.x;
+                    t.acc[s][4 * c + 1] = q.y;
+                    t.acc[s][4 * c + 2] = q.z;
+                    t.acc[s][4 * c + 3] = q.w;
+                }
+            }
+        }
+        t.fl = flp[pix(line, min(j0 + min(l16, T - 1), steps - 1))];
+    };
+
+    float Lp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) Lp[k] = FLT_MAX;
+    int dacc = -1;
+
+    auto step = [&](const RowTile<KV, T>& t, int s, bool start, float* f) {
+        float L[K];
+        if (start) {
+#pragma unroll
+            for (int k = 0; k < K; k++) L[k] = cval[k / 4] ? t.c[s][k] : FLT_MAX;
+        } else {
+            const uint32_t fl = (uint32_t)__builtin_amdgcn_ds_bpermute(row * 64 + s * 4, (int)t.fl);  // row's lane s
+            const bool pen = (fl >> dir) & 1u;
+            const float P1 = pen ? p1r : p1, P2 = pen ? p2r : p2;
+            float lm = Lp[0];
+#pragma unroll
+            for (int k = 1; k < K; k++) lm = fmin_pos(lm, Lp[k]);
+            const float m = __builtin_bit_cast(float, row_umin(__builtin_bit_cast(uint32_t, lm)));
+            const float P1m = P1 - m;
+            const float left = row_shift<DPP_ROW_SHR1>(Lp[K - 1]);
+            const float right = row_shift<DPP_ROW_SHL1>(Lp[0]);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const float prev = (k == 0) ? left : Lp[k - 1];
+                const float next = (k == K - 1) ? right : Lp[k + 1];
+                const float S1 = Lp[k] - m;
+                const float S2 = prev + P1m;
+                const float S3 = next + P1m;
+                const float mm = fmin_pos(fmin_pos(S1, S2), fmin_pos(S3, P2));
+                const float Lk = t.c[s][k] + mm;
+                L[k] = cval[k / 4] ? Lk : FLT_MAX;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const float prev = (MODE & SGM_FIRST) ? 0.f : t.acc[s][k];
+            f[k] = prev + L[k];
+            Lp[k] = L[k];
+        }
+    };
+
+    auto store4 = [&](char* r, uint32_t so, const float* f) {
+#pragma unroll
+        for (int c = 0; c < KV; c++)
+            if (FULLC || cval[c]) *(float4*)(r + so + voff[c]) = make_float4(f[4 * c + 0], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]);
+    };
+
+    auto process = [&](const RowTile<KV, T>& t, int j0) {
+        const long bp = tile_base(j0);
+        char* rout = (char*)((MODE & SGM_LAST) ? (float*)vmp + bp * D : accp + bp * D);
+#pragma unroll
+        for (int s = 0; s < T; s++) {
+            if (j0 + s >= steps) break;                   // wave-uniform
+            float f[K];
+            step(t, s, j0 + s == 0, f);
+            const uint32_t so = soff(j0, s);
+            if ((!(MODE & SGM_LAST) || (MODE & SGM_KEEP)) && st_ok) store4(rout, so, f);
+            if (MODE & SGM_LAST) {
+                // first minimum of the row: lowest lane of the row holding its minimum, then that
+                // lane's first index (chunks past D hold FLT_MAX: -1 when everything is FLT_MAX)
+                float bm = f[0];
+                int bi = d0;
+#pragma unroll
+                for (int k = 1; k < K; k++)
+                    if (bm > f[k]) {
+                        bm = f[k];
+                        bi = d0 + k;
+                    }
+                const float wm = __builtin_bit_cast(float, row_umin(__builtin_bit_cast(uint32_t, bm)));
+                const uint64_t hit = __ballot(bm == wm);
+                const uint32_t rmask = (uint32_t)(hit >> (row * 16)) & 0xffffu;
+                const int src = row * 16 + __builtin_ctz(rmask);
+                const int widx = __builtin_amdgcn_ds_bpermute(src * 4, bi);
+                const int dsel = (wm < FLT_MAX) ? widx : -1;
+                dacc = (l16 == s) ? dsel : dacc;
+            }
+        }
+        if (MODE & SGM_LAST) {
+            if (line_ok && l16 < T && j0 + l16 < steps) dp[pix(line, j0 + l16)] = (int16_t)dacc;
+        }
+    };
+
+    RowTile<KV, T> ta, tb;
+    load(ta, 0);
+    for (int j0 = 0; j0 < steps; j0 += 2 * T) {
+        load(tb, j0 + T);
+        process(ta, j0);
+        if (j0 + T >= steps) break;
+        load(ta, j0 + 2 * T);
+        process(tb, j0 + T);
+    }
+}
+
+template <int KV, bool FULLC>
+static void launch_rows_f(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    const int nl = a.ru == 0 ? a.W : a.H;
+    const int waves = (nl + 3) / 4 * n;
+    dim3 grid((waves + 3) / 4);
+    constexpr int T = KV == 1 ? 8 : (KV == 2 ? 4 : 2);
+    if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
+    switch (mode) {
+        case SGM_FIRST: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_FIRST, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_LAST, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST | SGM_KEEP: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_LAST | SGM_KEEP, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_FIRST | SGM_LAST, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST | SGM_KEEP:
+            hipLaunchKernelGGL((k_sgm_rows<KV, SGM_FIRST | SGM_LAST | SGM_KEEP, T, FULLC>), grid, dim3(256), 0, st, a);
+            break;
+        default: hipLaunchKernelGGL((k_sgm_rows<KV, 0, T, FULLC>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
+template <int KV>
+static void launch_rows(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    if (a.D == 16 * 4 * KV)
+        launch_rows_f<KV, true>(a, mode, n, st);
+    else
+        launch_rows_f<KV, false>(a, mode, n, st);
+}
+
 template <int K, bool FULL>
 static void launch_kf(const SgmArgs& a, int mode, int n, hipStream_t st) {
     const int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
@@ -244,7 +475,28 @@ static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
         launch_kf<K, false>(a, mode, n, st);
 }
 
+// Lanes-per-line layout for straight paths.  Measured on MI355X (Teddy x16): faster for the
+// vertical paths and the last (WTA) path, slower for the middle horizontal one, whose K = 1
+// sweep already streams whole rows.  SM_SGM_ROWS = bit mask over path indices (tuning).
+static int rows_kv(const SgmArgs& a, int mode) {
+    static const int mask = [] { const char* e = getenv("SM_SGM_ROWS"); return e ? (int)strtol(e, nullptr, 0) : -1; }();
+    if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > 256) return 0;
+    const bool use = mask >= 0 ? ((mask >> a.dir) & 1) : (a.ru == 0 || (mode & SGM_LAST));
+    if (!use) return 0;
+    const int K = (a.D + 15) / 16;
+    return (K + 3) / 4;
+}
+
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    SgmArgs b = a;
+    b.n = n;
+    switch (rows_kv(a, mode)) {
+        case 1: return launch_rows<1>(b, mode, n, st);
+        case 2: return launch_rows<2>(b, mode, n, st);
+        case 3: return launch_rows<3>(b, mode, n, st);
+        case 4: return launch_rows<4>(b, mode, n, st);
+        default: break;
+    }
     switch (sgm_k_for(a.D)) {
         case 1: launch_k<1>(a, mode, n, st); break;
         case 2: launch_k<2>(a, mode, n, st); break;

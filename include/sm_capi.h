@@ -137,6 +137,10 @@ SM_API float sm_expf_host(float x);   /* the device expf algorithm, evaluated on
 /* Device expf over the float bit patterns [first_bits, first_bits + n) into host out[n]. */
 SM_API sm_status sm_expf_device_range(sm_ctx* ctx, uint32_t first_bits, uint32_t n, float* out);
 SM_API sm_status sm_get_census(sm_ctx* ctx, int32_t view, uint64_t* dst); /* H*W*2 words */
+/* CBCA's area division (div_area, sm_device.h) against IEEE division on the device: every
+ * dividend mantissa at binary exponent `exp2` (a in [2^exp2, 2^(exp2+1))) for every divisor
+ * 1 <= b <= bmax; *mismatches receives the number of differing results. */
+SM_API sm_status sm_div_area_check(sm_ctx* ctx, int32_t exp2, int32_t bmax, uint64_t* mismatches);
 
 #ifdef __cplusplus
 }

@@ -64,6 +64,7 @@ SIGNATURES = [
     ("sm_profile_reset", C.c_int, [_P]),
     ("sm_expf_host", C.c_float, [C.c_float]),
     ("sm_expf_device_range", C.c_int, [_P, C.c_uint32, C.c_uint32, _P]),
+    ("sm_div_area_check", C.c_int, [_P, C.c_int32, C.c_int32, _P]),
     ("sm_get_census", C.c_int, [_P, C.c_int32, _P]),
 ]
 
@@ -83,6 +84,8 @@ def load() -> C.CDLL:
             "or `make -C mystereomatching_amd/csrc`")
     lib = C.CDLL(path)
     for name, res, args in SIGNATURES:
+        if path != LIB_PATH and not hasattr(lib, name):
+            continue  # an older tuning build may predate a diagnostic entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -753,4 +753,24 @@ sm_status sm_expf_device_range(sm_ctx* c, uint32_t first_bits, uint32_t n, float
     return SM_OK;
 }
 
+sm_status sm_div_area_check(sm_ctx* c, int32_t exp2, int32_t bmax, uint64_t* mismatches) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!mismatches || bmax < 1 || bmax > 65535 || exp2 < -126 || exp2 > 126) return fail(c, SM_EINVAL, "bad arguments");
+    unsigned long long* dbad = nullptr;
+    if ((s = dalloc(c, &dbad, 1))) return s;
+    hipError_t e = hipMemsetAsync(dbad, 0, sizeof(*dbad), c->st);
+    if (e == hipSuccess) {
+        sm::launch_div_check(exp2, bmax, dbad, c->st);
+        e = hipGetLastError();
+    }
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, dbad, sizeof(h), hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    hipFree(dbad);
+    if (e != hipSuccess) return hip_fail(c, e, "sm_div_area_check");
+    *mismatches = h;
+    return SM_OK;
+}
+
 }  // extern "C"

@@ -214,13 +214,10 @@ struct CbLine {
     __device__ __forceinline__ int up(int s) const { return (int)min((uint32_t)s, (uint32_t)(s - ring)); }   // s in [0, 2 ring)
     __device__ __forceinline__ int dn(int s) const { return (int)min((uint32_t)s, (uint32_t)(s + ring)); }   // s in (-ring, ring)
 
-    // genfinalVm_cbca's division, then (last pass only) SolveAll's `sum = 0; sum += w * v`
-    // (cpp:2189-2201): 0 + x == x for every x except -0, and no CBCA value is ever -0 (costs are
-    // >= +0, prefix sums of them too, and x - x rounds to +0), so the add is dropped.
-    __device__ __forceinline__ float finish_norm(float diff, uint32_t area) const {
-        const float out = diff / (float)area;
-        return SCALE ? scale * out : out;
-    }
+    // (last pass only) SolveAll's `sum = 0; sum += w * v` (cpp:2189-2201): 0 + x == x for every
+    // x except -0, and no CBCA value is ever -0 (costs are >= +0, prefix sums of them too, and
+    // x - x rounds to +0), so the add is dropped.
+    __device__ __forceinline__ float finish_norm(float q) const { return SCALE ? scale * q : q; }
 
     // ---------------- one tile of T positions, branch-free ------------------------------------
     // Every tile runs the same straight-line code.  Inputs past the line end are clamped loads
@@ -267,18 +264,34 @@ struct CbLine {
                 atv[k] = ra[ts * 64 + lane];
             }
         }
+        if (MODE == CB_SCAN) {
 #pragma unroll
-        for (int k = 0; k < T; k++) {
-            const float diff = shv[k] - stv[k];
-            const bool live = !GUARD || (unsigned)(i0 + k) < (unsigned)len;
-            if (MODE == CB_SCAN) {
-                if (live) store_tile(ob, k, diff);
-            } else {
-                const uint32_t area = (ahv[k] - atv[k]) & 0xffffu;
+            for (int k = 0; k < T; k++)
+                if (!GUARD || (unsigned)(i0 + k) < (unsigned)len) store_tile(ob, k, shv[k] - stv[k]);
+        } else {
+            // genfinalVm_cbca's division (cpp:3969-3992) by the integer area, through div_area
+            // (sm_device.h); tiles holding a dividend below its proven range redo the IEEE
+            // division (a uniform branch that never runs on real costs)
+            float dv[T], qv[T];
+            uint32_t av[T];
+            uint64_t tiny = 0;
+#pragma unroll
+            for (int k = 0; k < T; k++) {
+                dv[k] = shv[k] - stv[k];
+                av[k] = (ahv[k] - atv[k]) & 0xffffu;
+                qv[k] = div_area(dv[k], av[k]);
+                tiny |= __ballot(div_area_needs_ieee(dv[k]));
+            }
+            if (tiny) {
+#pragma unroll
+                for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)av[k];
+            }
+#pragma unroll
+            for (int k = 0; k < T; k++) {
                 if (MODE == CB_NORM) {
-                    if (live) store_tile(ob, k, finish_norm(diff, area));
+                    if (!GUARD || (unsigned)(i0 + k) < (unsigned)len) store_tile(ob, k, finish_norm(qv[k]));
                 } else {
-                    float y = diff / (float)area;                 // final value of iteration k at i
+                    float y = qv[k];                              // final value of iteration k at i
                     if (GUARD) y = (i0 + k >= 0) ? y : 0.f;       // nothing accumulates before the line
                     S2 = S2 + y;                                  // prefix of iteration k+1's first pass
                     r2[up(si0 + k) * 64 + lane] = S2;

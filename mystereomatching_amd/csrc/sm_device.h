@@ -96,6 +96,28 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, 0);
 }
 
+// a / b for a float a >= 0 and an integer 1 <= b < 2^16 (CBCA support areas), correctly
+// rounded like IEEE division, in 4 instructions instead of the 11 of the general sequence:
+//   y = rcp(b) (|rel. error| <= 2^-22 suffices), q0 = RN(a y), r = a - q0 b (exact), q = RN(q0 + r y).
+// Proof: with Q = a / b, |Q - q0| <= 4.5 ulp(Q), r is a multiple of ulp(q0) below 2^24 of them,
+// so the fma's r is exact and q0 + r y = Q + (Q - q0) e with |(Q - q0) e| <= 2^-19.8 ulp(Q).  A
+// midpoint M of Q's binade satisfies b Q - b M = integer * ulp(Q) / 2 and is never hit exactly
+// (b M has more than 24 significant bits unless b is a power of two, where q0 is already
+// exact), so |Q - M| >= ulp(Q) / (2 b) >= 2^-17 ulp(Q) > the perturbation: RN(q0 + r y) =
+// RN(Q).  Needs q0 and r representable without underflow: a == 0 or a >= 2^-110
+// (div_area_needs_ieee tells the caller when to use the IEEE division instead).
+// tests/test_gpu_parity.py::test_div_area_exhaustive checks it against IEEE on the device.
+__device__ __forceinline__ float div_area(float a, uint32_t b) {
+    const float bf = (float)b;
+    const float y = __builtin_amdgcn_rcpf(bf);
+    const float q0 = a * y;
+    const float r = __builtin_fmaf(-q0, bf, a);
+    return __builtin_fmaf(r, y, q0);
+}
+__device__ __forceinline__ bool div_area_needs_ieee(float a) {  // 0 < |a| < 2^-110
+    return (__builtin_bit_cast(uint32_t, a) & 0x7fffffffu) - 1u < 0x087fffffu;
+}
+
 // wave64 cross-lane helpers (device only)
 // DPP controls (GFX9 encoding).
 enum : int {

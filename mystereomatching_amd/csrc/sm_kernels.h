@@ -75,6 +75,7 @@ void launch_scale(float* vm, size_t n, float w, hipStream_t st);
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st);
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);
+void launch_div_check(int exp2, int bmax, unsigned long long* bad, hipStream_t st);
 float expf_host(float x);
 int sgm_k_for(int D);
 

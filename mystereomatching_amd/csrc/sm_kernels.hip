@@ -404,6 +404,24 @@ __global__ __launch_bounds__(256) void k_wta(const float* __restrict__ vm, int16
     if (lane == 0) disp[(size_t)b * npix + wave] = (int16_t)((wm < FLT_MAX) ? widx : -1);
 }
 
+// div_area vs IEEE: block y = divisor, threads sweep the 2^23 mantissas of exponent exp2
+__global__ void k_div_check(int exp2, unsigned long long* __restrict__ bad) {
+    const uint32_t b = blockIdx.y + 1;
+    const uint32_t ebits = (uint32_t)(exp2 + 127) << 23;
+    uint32_t nbad = 0;
+    for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < (1u << 23); m += gridDim.x * blockDim.x) {
+        const float a = __builtin_bit_cast(float, ebits | m);
+        const float fast = div_area(a, b);
+        const float ref = a / (float)b;
+        nbad += __builtin_bit_cast(uint32_t, fast) != __builtin_bit_cast(uint32_t, ref);
+    }
+    if (nbad) atomicAdd(bad, (unsigned long long)nbad);
+}
+
+void launch_div_check(int exp2, int bmax, unsigned long long* bad, hipStream_t st) {
+    hipLaunchKernelGGL(k_div_check, dim3(64, bmax), dim3(256), 0, st, exp2, bad);
+}
+
 __global__ void k_expf_range(uint32_t first, uint32_t n, float* __restrict__ out) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         out[i] = dev_expf(__builtin_bit_cast(float, first + i));

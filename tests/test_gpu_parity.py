@@ -190,6 +190,25 @@ def test_device_expf_exhaustive(oracle):
         lib.sm_destroy(ctx)
 
 
+@pytest.mark.parametrize("exp2", [0, -110, -60, 40, 120])
+def test_div_area_exhaustive(exp2):
+    """CBCA's 4-instruction area division equals IEEE a / b for every mantissa of a at the
+    exponent and every area b up to the largest a config allows ((2*84+1)^2 = 28561; the default
+    arms give 4761).  Exponents >= -110 behave alike (no underflow), so exponent 0 with all b is
+    the proof's check; the others sample the range ends."""
+    lib = _capi.load()
+    p = _capi.default_params(15, 8, 8)
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        bad = C.c_uint64(0)
+        bmax = 28561 if exp2 == 0 else 4761
+        _capi.check(lib, ctx, lib.sm_div_area_check(ctx, exp2, bmax, C.byref(bad)))
+        assert bad.value == 0
+    finally:
+        lib.sm_destroy(ctx)
+
+
 def test_state_errors():
     lib = _capi.load()
     p = _capi.default_params(15, 16, 16)

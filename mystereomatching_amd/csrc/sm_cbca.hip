@@ -177,11 +177,13 @@ struct CbLine {
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             const int base = j0 - set_off(s);
+            // (only lanes k < T are read back; the others stay off the memory system, which
+            // matters for the strided column loads of vertical sweeps)
             const int p0 = base + lane;
-            t.a0[s] = buf_ld_u32(A0r[s], (unsigned)p0 < (unsigned)len ? (uint32_t)(p0 * pstride) * 4u : 0x80000000u, 0);
+            t.a0[s] = buf_ld_u32(A0r[s], (lane < T && (unsigned)p0 < (unsigned)len) ? (uint32_t)(p0 * pstride) * 4u : 0x80000000u, 0);
             if (HORIZ) {
                 const int q = base + lane - c64;  // right pixel of lane 0 at position base + lane
-                t.a1v[s] = buf_ld_u32(A1r[s], (unsigned)q < (unsigned)len ? (uint32_t)q * 4u : 0x80000000u, 0);
+                t.a1v[s] = buf_ld_u32(A1r[s], (lane < T && (unsigned)q < (unsigned)len) ? (uint32_t)q * 4u : 0x80000000u, 0);
             } else {
                 const __amdgpu_buffer_rsrc_t ra1 = bounded_rsrc(A1v[s] + (long)base * (long)(pstride * 4), aend);
 #pragma unroll

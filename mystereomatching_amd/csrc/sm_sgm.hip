@@ -25,6 +25,36 @@
 #include "sm_device.h"
 #include "sm_kernels.h"
 
+// Steps prefetched per tile (two tiles in flight).  Large-D launches have few waves per SIMD
+// (one line per wave, or four per wave in k_sgm_rows), so their tiles are deep.
+#ifndef SM_SGM_ROWS_T1
+#define SM_SGM_ROWS_T1 8
+#endif
+#ifndef SM_SGM_ROWS_T2
+#define SM_SGM_ROWS_T2 4
+#endif
+#ifndef SM_SGM_ROWS_T3
+#define SM_SGM_ROWS_T3 2
+#endif
+#ifndef SM_SGM_ROWS_T4
+#define SM_SGM_ROWS_T4 2
+#endif
+#ifndef SM_SGM_T_K3
+#define SM_SGM_T_K3 5
+#endif
+#ifndef SM_SGM_T_K4
+#define SM_SGM_T_K4 4
+#endif
+#ifndef SM_SGM_VEC_MIN_D
+#define SM_SGM_VEC_MIN_D 128
+#endif
+#ifndef SM_SGM_T_V4
+#define SM_SGM_T_V4 8
+#endif
+#ifndef SM_SGM_T_BIG
+#define SM_SGM_T_BIG 2
+#endif
+
 namespace sm {
 
 template <int K>
@@ -45,8 +75,11 @@ struct SgmTile {
     uint32_t fl;  // lane t < T: penalty flags of the pixel of step j0 + t
 };
 
-template <int K, int MODE, int T, bool FULL>
+template <int K, int MODE, int T, bool FULL, bool VEC>
 __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
+    // VEC (D % 4 == 0, K % 4 == 0): each lane's K consecutive disparities move as K / 4 dwordx4
+    // accesses, so a step of a line is one contiguous D * 4-byte access per volume
+    constexpr int KV = VEC ? K / 4 : 1;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     const int H = a.H, W = a.W, D = a.D;
@@ -85,18 +118,20 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
     const size_t p0 = (size_t)v0 * W + u0;
     const int d0 = lane * K;
     // per-element load/store bases: elements past D read a clamped (valid) address and store to
-    // a private dummy slot, so no store is predicated
+    // a private dummy slot (VEC: the store is skipped), so no scalar store is predicated
     const float* cbase = a.vm + ((size_t)b * npix + p0) * D;
     float* abase = a.acc + ((size_t)b * npix + p0) * D;
     float* fbase = a.vm + ((size_t)b * npix + p0) * D;
     const uint8_t* flbase = a.flags + (size_t)b * npix + p0;
     int16_t* dbase = a.disp + (size_t)b * npix + p0;
-    const int vstep = pstep * D;
+    const long vstep = (long)pstep * D;
     int ld[K];          // load column (clamped to a valid address)
     bool val[K];
     float* ap[K];       // store targets: real element or this lane's dummy slot (stride 0)
     float* fp[K];
-    int sst[K];
+    long sst[K];
+    bool cval[KV];      // VEC: chunk inside D
+    int ldc[KV];        // VEC: chunk load column (clamped)
 #pragma unroll
     for (int k = 0; k < K; k++) {
         val[k] = d0 + k < D;
@@ -104,6 +139,11 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
         ap[k] = val[k] ? abase + d0 + k : a.dummy + ((lane * K + k) & 63);
         fp[k] = val[k] ? fbase + d0 + k : a.dummy + ((lane * K + k) & 63);
         sst[k] = val[k] ? vstep : 0;
+    }
+#pragma unroll
+    for (int c = 0; c < KV; c++) {
+        cval[c] = d0 + 4 * c < D;
+        ldc[c] = cval[c] ? d0 + 4 * c : D - 4;
     }
     int dacc = -1;      // lane s holds the disparity of step j0 + s until the tile's store
     const float p1 = a.p1, p2 = a.p2;
@@ -114,14 +154,43 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
     auto load = [&](SgmTile<K, T>& t, int j0) {
 #pragma unroll
         for (int s = 0; s < T; s++) {
-            const int off = clampi(j0 + s) * vstep;
+            const long off = (long)clampi(j0 + s) * vstep;
+            if (VEC) {
 #pragma unroll
-            for (int k = 0; k < K; k++) {
-                t.c[s][k] = cbase[off + ld[k]];
-                if (!(MODE & SGM_FIRST)) t.acc[s][k] = abase[off + ld[k]];
+                for (int c = 0; c < KV; c++) {
+                    const float4 v = *(const float4*)(cbase + off + ldc[c]);
+                    t.c[s][4 * c + 0] = v.x;
+                    t.c[s][4 * c + 1] = v.y;
+                    t.c[s][4 * c + 2] = v.z;
+                    t.c[s][4 * c + 3] = v.w;
+                    if (!(MODE & SGM_FIRST)) {
+                        const float4 q = *(const float4*)(abase + off + ldc[c]);
+                        t.acc[s][4 * c + 0] = q.x;
+                        t.acc[s][4 * c + 1] = q.y;
+                        t.acc[s][4 * c + 2] = q.z;
+                        t.acc[s][4 * c + 3] = q.w;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    t.c[s][k] = cbase[off + ld[k]];
+                    if (!(MODE & SGM_FIRST)) t.acc[s][k] = abase[off + ld[k]];
+                }
             }
         }
-        t.fl = flbase[clampi(j0 + min(lane, T - 1)) * pstep];
+        t.fl = flbase[(long)clampi(j0 + min(lane, T - 1)) * pstep];
+    };
+    auto store = [&](float* base, float* const* pk, int j, const float* f) {
+        if (VEC) {
+#pragma unroll
+            for (int c = 0; c < KV; c++)
+                if (FULL || cval[c])
+                    *(float4*)(base + (long)j * vstep + d0 + 4 * c) = make_float4(f[4 * c + 0], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; k++) pk[k][(long)j * sst[k]] = f[k];
+        }
     };
 
     float Lp[K];
@@ -168,10 +237,7 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
             f[k] = prev + L[k];   // sum += Lr[num] (cpp:2046-2049); padded lanes stay FLT_MAX
         }
         if (MODE & SGM_LAST) {
-            if (MODE & SGM_KEEP) {
-#pragma unroll
-                for (int k = 0; k < K; k++) fp[k][j * sst[k]] = f[k];
-            }
+            if (MODE & SGM_KEEP) store(fbase, fp, j, f);
             float bm = f[0];
             int bi = d0;
 #pragma unroll
@@ -188,8 +254,7 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
             const int dsel = (wm < FLT_MAX) ? widx : -1;
             dacc = (lane == s) ? dsel : dacc;
         } else {
-#pragma unroll
-            for (int k = 0; k < K; k++) ap[k][j * sst[k]] = f[k];
+            store(abase, ap, j, f);
         }
 #pragma unroll
         for (int k = 0; k < K; k++) Lp[k] = L[k];
@@ -205,7 +270,7 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
                 if (j0 + s < steps) step(t, s, j0 + s, j0 + s == 0);
         }
         if (MODE & SGM_LAST) {  // one store instruction per tile for the int16 disparities
-            if (lane < T && j0 + lane < steps) dbase[(j0 + lane) * pstep] = (int16_t)dacc;
+            if (lane < T && j0 + lane < steps) dbase[(long)(j0 + lane) * pstep] = (int16_t)dacc;
         }
     };
 
@@ -427,7 +492,7 @@ static void launch_rows_f(const SgmArgs& a, int mode, int n, hipStream_t st) {
     const int nl = a.ru == 0 ? a.W : a.H;
     const int waves = (nl + 3) / 4 * n;
     dim3 grid((waves + 3) / 4);
-    constexpr int T = KV == 1 ? 8 : (KV == 2 ? 4 : 2);
+    constexpr int T = KV == 1 ? SM_SGM_ROWS_T1 : (KV == 2 ? SM_SGM_ROWS_T2 : (KV == 3 ? SM_SGM_ROWS_T3 : SM_SGM_ROWS_T4));
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
     switch (mode) {
         case SGM_FIRST: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_FIRST, T, FULLC>), grid, dim3(256), 0, st, a); break;
@@ -449,21 +514,22 @@ static void launch_rows(const SgmArgs& a, int mode, int n, hipStream_t st) {
         launch_rows_f<KV, false>(a, mode, n, st);
 }
 
-template <int K, bool FULL>
+template <int K, bool FULL, bool VEC = false>
 static void launch_kf(const SgmArgs& a, int mode, int n, hipStream_t st) {
     const int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
     dim3 grid((nlines + 3) / 4, n);
-    constexpr int T = K >= 8 ? 2 : 16 / K;
+    constexpr int T = VEC ? (K == 4 ? SM_SGM_T_V4 : SM_SGM_T_BIG)
+                          : (K >= 8 ? SM_SGM_T_BIG : (K == 3 ? SM_SGM_T_K3 : (K == 4 ? SM_SGM_T_K4 : 16 / K)));
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
     switch (mode) {
-        case SGM_FIRST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST, T, FULL>), grid, dim3(256), 0, st, a); break;
-        case SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_LAST, T, FULL>), grid, dim3(256), 0, st, a); break;
-        case SGM_LAST | SGM_KEEP: hipLaunchKernelGGL((k_sgm<K, SGM_LAST | SGM_KEEP, T, FULL>), grid, dim3(256), 0, st, a); break;
-        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST, T, FULL>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_LAST, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST | SGM_KEEP: hipLaunchKernelGGL((k_sgm<K, SGM_LAST | SGM_KEEP, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
         case SGM_FIRST | SGM_LAST | SGM_KEEP:
-            hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST | SGM_KEEP, T, FULL>), grid, dim3(256), 0, st, a);
+            hipLaunchKernelGGL((k_sgm<K, SGM_FIRST | SGM_LAST | SGM_KEEP, T, FULL, VEC>), grid, dim3(256), 0, st, a);
             break;
-        default: hipLaunchKernelGGL((k_sgm<K, 0, T, FULL>), grid, dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_sgm<K, 0, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
     }
 }
 
@@ -475,12 +541,15 @@ static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
         launch_kf<K, false>(a, mode, n, st);
 }
 
-// Lanes-per-line layout for straight paths.  Measured on MI355X (Teddy x16): faster for the
-// vertical paths and the last (WTA) path, slower for the middle horizontal one, whose K = 1
-// sweep already streams whole rows.  SM_SGM_ROWS = bit mask over path indices (tuning).
+// Lanes-per-line layout for straight paths with D <= SM_SGM_VEC_MIN_D.  Measured on MI355X
+// (Teddy x16): faster for the vertical paths and the last (WTA) path, slower for the middle
+// horizontal one, whose K = 1 sweep already streams whole rows.  SM_SGM_ROWS = bit mask over
+// path indices (tuning).  Larger D runs every direction one line per wave with dwordx4 lanes
+// (k_sgm VEC): the four-lines-per-wave layout leaves too few waves in flight there
+// (tools/ubench_sgm.hip, KITTI D = 192: 3.5 TB/s with 4 lines per wave vs 5.0 TB/s with one).
 static int rows_kv(const SgmArgs& a, int mode) {
     static const int mask = [] { const char* e = getenv("SM_SGM_ROWS"); return e ? (int)strtol(e, nullptr, 0) : -1; }();
-    if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > 256) return 0;
+    if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > SM_SGM_VEC_MIN_D) return 0;
     const bool use = mask >= 0 ? ((mask >> a.dir) & 1) : (a.ru == 0 || (mode & SGM_LAST));
     if (!use) return 0;
     const int K = (a.D + 15) / 16;
@@ -496,6 +565,13 @@ void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {
         case 3: return launch_rows<3>(b, mode, n, st);
         case 4: return launch_rows<4>(b, mode, n, st);
         default: break;
+    }
+    if (a.D > SM_SGM_VEC_MIN_D && a.D <= 256 && a.D % 4 == 0) {  // one line per wave, dwordx4 per lane
+        if (a.D == 256)
+            launch_kf<4, true, true>(b, mode, n, st);
+        else
+            launch_kf<4, false, true>(b, mode, n, st);
+        return;
     }
     switch (sgm_k_for(a.D)) {
         case 1: launch_k<1>(a, mode, n, st); break;

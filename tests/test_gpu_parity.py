@@ -113,9 +113,11 @@ def test_census_and_arms(oracle):
 
 
 @pytest.mark.parametrize("H,W,md,paths", [(2, 2, 0, 4), (3, 70, 63, 4), (70, 3, 5, 8), (17, 23, 64, 8),
-                                          (25, 31, 127, 4), (13, 90, 191, 8), (9, 40, 255, 4)])
+                                          (25, 31, 127, 4), (13, 90, 191, 8), (9, 40, 255, 4),
+                                          (11, 37, 199, 8), (7, 30, 130, 4)])
 def test_shapes_and_edge_cases(oracle, H, W, md, paths):
-    """Tiny/ragged images, D not a multiple of 64, D > W, D = 1, 8 paths."""
+    """Tiny/ragged images, D not a multiple of 64 (or of 4), D > W, D = 1, 8 paths; every SGM
+    kernel layout (rows for D <= 128, dwordx4 lanes for 128 < D <= 256 with D % 4 == 0, scalar lanes)."""
     pair = S.make_pair(H, W, md + 1, 14 + H)
     cfg = oracle.config(H, W, md, sgm_paths=paths)
     ref = oracle.run(pair, cfg, dumps=True)

@@ -288,6 +288,7 @@ sm_status run_cost(sm_ctx* c, int n, int view, const Bufs& B) {
     a.D = p.num_disparities;
     a.view = view;
     a.nwords = (census_len(p) + 63) / 64;
+    a.cwords = (census_len(p) + 31) / 32;
     a.census_default = (float)census_len(p) * 1.0f;
     a.grad_trunc = p.grad_trunc;
     a.grad_oor = (float)sqrt(pow((double)p.grad_trunc, 2) * 2);

@@ -33,6 +33,7 @@ struct CostArgs {
     const uint8_t* arms;        // [n][view][plane][H][W] u32: plane 0 = L | R<<16, plane 1 = U | D<<16
     const uint8_t* bgr;         // [n][2][H][W][3]
     int H, W, D, view, nwords;
+    int cwords;                 // 32-bit census words in use: ceil(bits / 32)
     float census_default;       // codeLength * truncRat (h:938)
     float grad_trunc, grad_oor; // 500, sqrt(2*500^2) (cpp:440)
     int grad_adaptive;

@@ -221,16 +221,42 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 // whose result is discarded when -G/lamG < -17.5: then expf(-G/lamG) <= 2^-25 and
 // fl(t - e) == t for every t = fl(2 - e0) in [1, 2), so the reference's value is t itself.
 // The element loop is branch-free: out-of-range candidates (u - d < 0 or u + d >= W) read a
-// clamped, staged neighbour and select the reference's out-of-range cost afterwards; without
+// zero-filled staged record and select the reference's out-of-range cost afterwards; without
 // the adaptive weights the weights are 1, and 1 * x + 1 * y == x + y exactly.  lamG == 1 (the
 // default) skips the division, since -G / 1 == -G.
 // ---------------------------------------------------------------------------------------
-constexpr int COST_P = 64;
+#ifndef SM_COST_PROBE
+#define SM_COST_PROBE 0
+#endif
+#ifndef SM_COST_UNROLL
+#define SM_COST_UNROLL 1
+#endif
+// Pixels of a row segment per block: D <= 64 amortises the P + D - 1 moving-pixel staging over
+// 128 pixels (Teddy x16: 0.277 -> 0.255 ms); larger D gains nothing from it (full-res: 3.84 vs
+// 3.89 ms) and keeps 64.
+#ifndef SM_COST_P_ONE
+#define SM_COST_P_ONE 128
+#endif
+#ifndef SM_COST_P_MULTI
+#define SM_COST_P_MULTI 64
+#endif
+__host__ __device__ constexpr int cost_p(bool one) { return one ? SM_COST_P_ONE : SM_COST_P_MULTI; }
 constexpr int LUT_A_N = 129, LUT_B_N = 766;
 
-template <int METHOD, bool LAM1>
+// LDS layout of a cost block.  Moving pixel i (position mbase + i, every candidate of the
+// block's P pixels: q - mbase is in [0, P + D - 1) by construction) is a record of the CW
+// 32-bit census words in use (CW = ceil(bits / 32), at least 2) followed by gx | BGR and gy:
+// one 16-byte uint4 for CW = 2 (one ds_read_b128 per element), two for CW = 3, 4.  Positions
+// outside the image hold zeros (the out-of-range select discards them).  Focus-pixel values are
+// wave-uniform reads, once per pixel.
+template <int CW>
+__host__ __device__ constexpr int cost_rec_u4() { return CW <= 2 ? 1 : 2; }
+
+template <int METHOD, bool LAM1, int CW, bool ONE, bool OORZ>
 __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     extern __shared__ __align__(16) unsigned char cs_raw[];
+    constexpr int RW = cost_rec_u4<CW>();
+    constexpr int COST_P = cost_p(ONE);
     const int D = a.D, W = a.W, H = a.H;
     const int nbx = (W + COST_P - 1) / COST_P;
     const int blk = xcd_swizzle(blockIdx.x, gridDim.x);  // neighbouring segments share an XCD's L2
@@ -248,20 +274,16 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     constexpr bool CEN = METHOD != SM_M_AD;
     constexpr bool GRAD = METHOD == SM_M_CENSUS_GRAD;
     constexpr bool ADM = METHOD == SM_M_AD || METHOD == SM_M_AD_CENSUS;
-    // LDS carve-up (16-byte items first)
-    ulonglong2* fcode = (ulonglong2*)cs_raw;                 // [P]
-    ulonglong2* mcode = fcode + COST_P;                      // [P + D - 1]
-    uint64_t* etab = (uint64_t*)(mcode + (COST_P + D - 1));  // [32] 2^(i/32)
-    float* fgx = (float*)(etab + 32);                        // [P]
+    uint4* mrec = (uint4*)cs_raw;                                // [(P + D - 1) * RW]
+    ulonglong2* fcode = (ulonglong2*)(mrec + RW * (COST_P + D - 1));  // [P]
+    uint64_t* etab = (uint64_t*)(fcode + COST_P);               // [32] 2^(i/32)
+    float* fgx = (float*)(etab + 32);                            // [P]
     float* fgy = fgx + COST_P;
-    float* fwa = fgy + COST_P;                               // adaptive weight a (1 if off)
-    float* fwb = fwa + COST_P;                               // 1 - a (1 if off)
-    float* mgx = fwb + COST_P;                               // [P + D - 1]
-    float* mgy = mgx + (COST_P + D - 1);
-    uint32_t* fbgr = (uint32_t*)(mgy + (COST_P + D - 1));    // [P]
-    uint32_t* mbgr = fbgr + COST_P;                          // [P + D - 1]
-    float* luta = (float*)(mbgr + (COST_P + D - 1));         // [LUT_A_N]
-    float* lutb = luta + LUT_A_N;                            // [LUT_B_N]
+    float* fwa = fgy + COST_P;                                   // adaptive weight a (1 if off)
+    float* fwb = fwa + COST_P;                                   // 1 - a (1 if off)
+    uint32_t* fbgr = (uint32_t*)(fwb + COST_P);                  // [P]
+    float* luta = (float*)(fbgr + COST_P);                       // [LUT_A_N]
+    float* lutb = luta + LUT_A_N;                                // [LUT_B_N]
     const int tid = threadIdx.y * 64 + threadIdx.x;
     if (GRAD && tid < 32) etab[tid] = c_exp_tab[tid];
     if (CEN)
@@ -295,20 +317,37 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     }
     for (int i = tid; i < nm; i += 256) {
         const int q = mbase + i;
-        if (q < 0 || q >= W) continue;
-        if (CEN) mcode[i] = a.code[mrow + q];
-        if (GRAD) {
-            mgx[i] = a.gx[mrow + q];
-            mgy[i] = a.gy[mrow + q];
+        ulonglong2 c = make_ulonglong2(0, 0);
+        uint32_t w2 = 0, w3 = 0;
+        if (q >= 0 && q < W) {
+            if (CEN) c = a.code[mrow + q];
+            if (GRAD) {
+                w2 = __float_as_uint(a.gx[mrow + q]);
+                w3 = __float_as_uint(a.gy[mrow + q]);
+            }
+            if (ADM) {
+                const uint8_t* p = a.bgr + (mrow + q) * 3;
+                w2 = p[0] | (p[1] << 8) | (p[2] << 16);
+            }
         }
-        if (ADM) {
-            const uint8_t* p = a.bgr + (mrow + q) * 3;
-            mbgr[i] = p[0] | (p[1] << 8) | (p[2] << 16);
+        if (CW == 4) {
+            mrec[2 * i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, (uint32_t)(c.y >> 32));
+            mrec[2 * i + 1] = make_uint4(w2, w3, 0, 0);
+        } else if (CW == 3) {
+            mrec[2 * i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, w2);
+            mrec[2 * i + 1] = make_uint4(w3, 0, 0, 0);
+        } else {
+            mrec[i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), w2, w3);
         }
     }
     __syncthreads();
+    const int lane = threadIdx.x;
+    if (ONE && lane >= D) return;                   // D <= 64: one disparity per lane; no barrier follows
     const float cd = a.census_default;
-    float* out = a.vm + ((size_t)b * npix + (size_t)v * W + u0) * D;
+    const int icd = (int)cd;                        // (int)fminf(pc, cd) == min(pc, (int)cd) for integer pc >= 0
+    const float* out = a.vm + ((size_t)b * npix + (size_t)v * W + u0) * D;
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out, np * D * 4);
+#pragma unroll SM_COST_UNROLL
     for (int pl = threadIdx.y; pl < np; pl += 4) {
         const int u = u0 + pl;
         const ulonglong2 cf = CEN ? fcode[pl] : make_ulonglong2(0, 0);
@@ -321,53 +360,80 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
             wb = fwb[pl];
         }
         if (ADM) fc = fbgr[pl];
-        for (int d = threadIdx.x; d < D; d += 64) {
-            const int q = u - sgn * d;                 // moving position
+        auto elem = [&](int d, int q) {                // q = u - sgn * d, the moving position
             const bool oor = (unsigned)q >= (unsigned)W;
-            const int mi = min(max(q, 0), W - 1) - mbase;  // clamped, always a staged entry
-            float cen = 0.f;
+            const int mi = q - mbase;                  // staged record (zeros when out of range)
+            const uint4 r0 = mrec[RW * mi];
+            uint32_t w2 = r0.z, w3 = r0.w;
+            uint32_t pc = 0;
             if (CEN) {
-                const ulonglong2 cm = mcode[mi];
-                uint32_t pc = __popcll(cf.x ^ cm.x);
-                if (a.nwords > 1) pc += __popcll(cf.y ^ cm.y);
-                cen = oor ? cd : fminf((float)pc, cd);
+                pc = __popc((uint32_t)cf.x ^ r0.x) + __popc((uint32_t)(cf.x >> 32) ^ r0.y);
+                if (CW >= 3) pc += __popc((uint32_t)cf.y ^ r0.z);
+                if (CW == 4) pc += __popc((uint32_t)(cf.y >> 32) ^ r0.w);
+            }
+            if (CW == 3) {
+                w2 = r0.w;
+                w3 = ((const uint32_t*)mrec)[4 * (RW * mi + 1)];
+            } else if (CW == 4) {
+                const uint4 r1 = mrec[RW * mi + 1];
+                w2 = r1.x;
+                w3 = r1.y;
             }
             float res;
             if (METHOD == SM_M_CENSUS) {
-                res = cen;
+                res = oor ? cd : fminf((float)pc, cd);
             } else if (GRAD) {
-                const float dx = fminf(fabsf(fx - mgx[mi]), a.grad_trunc);
-                const float dy = fminf(fabsf(fy - mgy[mi]), a.grad_trunc);
+                const float dx = fminf(fabsf(fx - __uint_as_float(w2)), a.grad_trunc);
+                const float dy = fminf(fabsf(fy - __uint_as_float(w3)), a.grad_trunc);
                 const float t1 = wa * dx;
                 const float t2 = wb * dy;
-                const float g = oor ? a.grad_oor : t1 + t2;
-                const float e0 = luta[(int)cen];          // expf(-C / lamCen)
+                float g0 = t1 + t2;
+                asm volatile("" : "+v"(g0));              // keep the element loop branch-free
+                const float g = oor ? a.grad_oor : g0;
+                const int ci = oor ? icd : min((int)pc, icd);
+                const float e0 = luta[ci];                // expf(-C / lamCen)
                 const float xg = LAM1 ? -g : -g / a.lam2;
+#if SM_COST_PROBE == 1
+                const float ex = xg * 1e-3f;                 // timing probe: no exponential
+#else
                 const float ex = expf_glibc_core(xg, etab); // expf(-G / lamG)
+#endif
                 const float e1 = xg >= -17.5f ? ex : 0.f;
                 const float t = 2.0f - e0;
                 res = t - e1;
             } else {
-                const uint32_t y = mbgr[mi];
+                const uint32_t y = w2;
                 const int s3 = abs((int)(fc & 0xff) - (int)(y & 0xff)) +
                                abs((int)((fc >> 8) & 0xff) - (int)((y >> 8) & 0xff)) + abs((int)(fc >> 16) - (int)(y >> 16));
                 if (METHOD == SM_M_AD) {
                     res = oor ? a.ad_trunc : fminf((float)s3 / 3.0f, a.ad_trunc);
                 } else {
                     const float e0 = oor ? a.ad_oor_exp : lutb[s3];
-                    const float e1 = luta[(int)cen];
+                    const int ci = oor ? icd : min((int)pc, icd);
+                    const float e1 = luta[ci];
                     const float t = 2.0f - e0;
                     res = t - e1;
                 }
             }
-            out[(size_t)pl * D + d] = res;
+#if SM_COST_PROBE == 2
+            res = (float)d;                              // timing probe: stores only
+#endif
+            buf_st(ro, (uint32_t)((pl * D + d) * 4), 0, res);
+        };
+        if (ONE) {
+            elem(lane, u - sgn * lane);
+        } else {
+            const int qstep = sgn * 64;
+            int q = u - sgn * lane;
+            for (int d = lane; d < D; d += 64, q -= qstep) elem(d, q);
         }
     }
 }
 
-size_t cost_smem_bytes(int D) {
+size_t cost_smem_bytes(int D, int cwords) {
+    const int COST_P = cost_p(D <= 64);
     const size_t nm = COST_P + D - 1;
-    return 16 * (COST_P + nm) + 8 * 32 + 4 * (4 * COST_P + 2 * nm) + 4 * (COST_P + nm) + 4 * (LUT_A_N + LUT_B_N);
+    return 16 * (cwords > 2 ? 2 : 1) * nm + 16 * COST_P + 8 * 32 + 4 * 5 * COST_P + 4 * (LUT_A_N + LUT_B_N);
 }
 
 // SolveAll with PY_LVL = 1 as a standalone pass (used by the reference-ordered API):
@@ -436,20 +502,50 @@ hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st) {
     return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut_b), lut_b, sizeof(float) * 1024, 0, hipMemcpyHostToDevice, st);
 }
 
+template <int METHOD, bool LAM1, int CW, bool OORZ>
+static void launch_cost_z(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
+    if (a.D <= 64)
+        hipLaunchKernelGGL((k_cost<METHOD, LAM1, CW, true, OORZ>), grid, block, shm, st, a);
+    else
+        hipLaunchKernelGGL((k_cost<METHOD, LAM1, CW, false, OORZ>), grid, block, shm, st, a);
+}
+
+template <int METHOD, bool LAM1, int CW>
+static void launch_cost_nw(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
+    // the kernel's own expression for an out-of-range pair: xg = -G (lamG == 1) or -G / lamG
+    const float g = a.grad_oor;
+    const float xg = LAM1 ? -g : -g / a.lam2;
+    if constexpr (METHOD == SM_M_CENSUS_GRAD) {
+        if (xg < -17.5f) return launch_cost_z<METHOD, LAM1, CW, true>(a, grid, block, shm, st);
+    }
+    launch_cost_z<METHOD, LAM1, CW, false>(a, grid, block, shm, st);
+}
+
+template <int METHOD, bool LAM1>
+static void launch_cost_m(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
+    if (METHOD == SM_M_AD || a.cwords <= 2)
+        launch_cost_nw<METHOD, LAM1, 2>(a, grid, block, shm, st);
+    else if (a.cwords == 3)
+        launch_cost_nw<METHOD, LAM1, 3>(a, grid, block, shm, st);
+    else
+        launch_cost_nw<METHOD, LAM1, 4>(a, grid, block, shm, st);
+}
+
 void launch_cost(const CostArgs& a, int method, int n, hipStream_t st) {
-    dim3 grid((unsigned)((a.W + COST_P - 1) / COST_P * a.H * n));
+    const int P = cost_p(a.D <= 64);
+    dim3 grid((unsigned)((a.W + P - 1) / P * a.H * n));
     dim3 block(64, 4);
-    const size_t shm = cost_smem_bytes(a.D);
+    const size_t shm = cost_smem_bytes(a.D, method == SM_M_AD ? 2 : a.cwords);
     switch (method) {
         case SM_M_CENSUS_GRAD:
             if (a.lam2 == 1.0f)
-                hipLaunchKernelGGL((k_cost<SM_M_CENSUS_GRAD, true>), grid, block, shm, st, a);
+                launch_cost_m<SM_M_CENSUS_GRAD, true>(a, grid, block, shm, st);
             else
-                hipLaunchKernelGGL((k_cost<SM_M_CENSUS_GRAD, false>), grid, block, shm, st, a);
+                launch_cost_m<SM_M_CENSUS_GRAD, false>(a, grid, block, shm, st);
             break;
-        case SM_M_CENSUS: hipLaunchKernelGGL((k_cost<SM_M_CENSUS, false>), grid, block, shm, st, a); break;
-        case SM_M_AD_CENSUS: hipLaunchKernelGGL((k_cost<SM_M_AD_CENSUS, false>), grid, block, shm, st, a); break;
-        default: hipLaunchKernelGGL((k_cost<SM_M_AD, false>), grid, block, shm, st, a); break;
+        case SM_M_CENSUS: launch_cost_m<SM_M_CENSUS, false>(a, grid, block, shm, st); break;
+        case SM_M_AD_CENSUS: launch_cost_m<SM_M_AD_CENSUS, false>(a, grid, block, shm, st); break;
+        default: launch_cost_m<SM_M_AD, false>(a, grid, block, shm, st); break;
     }
 }
 

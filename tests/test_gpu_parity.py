@@ -78,6 +78,31 @@ def test_cost_volume_and_stages(oracle, cost):
     np.testing.assert_array_equal(dp, ref["disp"])
 
 
+@pytest.mark.parametrize("rv,ru,ring,cost,md", [(1, 1, 0, 1, 23), (2, 3, 1, 0, 99), (3, 4, 0, 2, 23),
+                                                 (4, 4, 1, 0, 23), (4, 5, 1, 0, 70), (4, 5, 1, 2, 99)])
+def test_census_windows(oracle, rv, ru, ring, cost, md):
+    """Census widths of 1-4 32-bit words (cost-kernel record layouts), D <= 64 and D > 64, both views."""
+    H, W = 23, 97
+    pair = S.make_pair(H, W, md + 1, 60 + rv * 7 + ru)
+    cfg = oracle.config(H, W, md, cost=cost, census_rv=rv, census_ru=ru, census_ring=ring)
+    lib = _capi.load()
+    p = _capi.default_params(md, H, W, aggregation=0, optimization=0, compute_right_view=1, cost_method=cost)
+    p.census_rv, p.census_ru, p.census_ring = rv, ru, ring
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        a = {k: np.ascontiguousarray(pair[k]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        _capi.check(lib, ctx, lib.sm_set_images(ctx, _capi.ptr(a["lbgr"]), _capi.ptr(a["rbgr"]), W * 3,
+                                                _capi.ptr(a["lgray"]), _capi.ptr(a["rgray"]), W))
+        _capi.check(lib, ctx, lib.sm_cost_calculate(ctx))
+        for view in (0, 1):
+            got = np.empty((H, W, md + 1), np.float32)
+            _capi.check(lib, ctx, lib.sm_get_volume(ctx, view, _capi.ptr(got)))
+            np.testing.assert_array_equal(bits(got), bits(oracle.cost_volume(pair, cfg, view=view)))
+    finally:
+        lib.sm_destroy(ctx)
+
+
 def test_right_view_volume(oracle):
     H, W, md = 33, 52, 19
     pair = S.make_pair(H, W, md + 1, 12)

@@ -22,7 +22,7 @@ def profile_name(sym: str, seen: dict) -> str:
         h = m.group(1) == "true"
         mode = {"0": "scan", "1": "norm", "2": "norm_scan"}[m.group(2)]
         return f"cbca_{'h' if h else 'v'}_{mode}"
-    m = re.search(r"k_sgm<\d+, (\d+),", sym)
+    m = re.search(r"k_sgm(?:_rows)?<\d+, (\d+),", sym)
     if m:
         mode = int(m.group(1))  # SGM_FIRST = 1, SGM_LAST = 2, SGM_KEEP = 4
         if mode & 2:

@@ -31,7 +31,17 @@ class Config(C.Structure):
         ("solve_all", C.c_int), ("reg_lambda", C.c_float), ("optimization", C.c_int),
         ("sgm_paths", C.c_int), ("sgm_p1", C.c_float), ("sgm_p2", C.c_float),
         ("sgm_cor_thres", C.c_int), ("sgm_redu", C.c_int),
+        ("do_refine", C.c_int), ("lr_max_diff", C.c_float), ("do_region_vote", C.c_int),
+        ("region_vote_nums", C.c_int), ("rv_ratio", C.c_float), ("rv_s", C.c_int),
+        ("do_proper_ipol", C.c_int), ("disp_occ", C.c_int), ("do_last_median", C.c_int),
     ]
+
+
+class Dumps(C.Structure):
+    """struct smo_dumps (oracle/sm_oracle.h)."""
+
+    _fields_ = [(k, C.c_void_p) for k in ("vol_cost", "vol_agg", "vol_final", "vol_right", "vol_agg_right",
+                                           "disp_left_raw", "disp_right", "stage_ms")]
 
 
 _lib = None
@@ -51,6 +61,13 @@ def load():
         lib.smo_default_config.argtypes = [C.POINTER(Config), C.c_int, C.c_int, C.c_int]
         lib.smo_run.argtypes = [C.POINTER(Config), P, P, P, P, P, P, P, P, P, P]
         lib.smo_run.restype = C.c_int
+        lib.smo_run_ex.argtypes = [C.POINTER(Config), P, P, P, P, P, C.POINTER(Dumps)]
+        lib.smo_run_ex.restype = C.c_int
+        lib.smo_lr_check.argtypes = [C.POINTER(Config), P, P]
+        lib.smo_region_vote.argtypes = [C.POINTER(Config), P, P, C.c_float, C.c_int]
+        lib.smo_proper_ipol.argtypes = [C.POINTER(Config), P, P]
+        lib.smo_median3.argtypes = [C.c_int, C.c_int, P]
+        lib.smo_refine.argtypes = [C.POINTER(Config), P, P, P, P]
         lib.smo_census.argtypes = [C.POINTER(Config), P, P]
         lib.smo_arms.argtypes = [C.POINTER(Config), P, P]
         lib.smo_cost_volume.argtypes = [C.POINTER(Config), P, P, P, P, C.c_int, P]
@@ -98,6 +115,60 @@ def run(pair: dict, cfg: Config, dumps: bool = False, right: bool = False):
         out.update(vols)
     if right:
         out["right"] = vr
+    return out
+
+
+def run_ex(pair: dict, cfg: Config, dumps=()):
+    """smo_run_ex: returns dict(disp, stage_ms, and each requested dump:
+    cost, agg, final, right, agg_right (H x W x D float32), disp_raw, disp_right (H x W int16))."""
+    lib = load()
+    H, W, D = cfg.H, cfg.W, cfg.D
+    arr = {k: np.ascontiguousarray(pair[k], np.uint8) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+    disp = np.empty((H, W), np.int16)
+    names = {"cost": "vol_cost", "agg": "vol_agg", "final": "vol_final", "right": "vol_right",
+             "agg_right": "vol_agg_right", "disp_raw": "disp_left_raw", "disp_right": "disp_right"}
+    bufs = {}
+    d = Dumps()
+    for k in dumps:
+        bufs[k] = np.empty((H, W), np.int16) if k.startswith("disp") else np.empty((H, W, D), np.float32)
+        setattr(d, names[k], bufs[k].ctypes.data)
+    ms = (C.c_double * 7)()
+    d.stage_ms = C.cast(ms, C.c_void_p).value
+    st = lib.smo_run_ex(C.byref(cfg), _p(arr["lbgr"]), _p(arr["rbgr"]), _p(arr["lgray"]), _p(arr["rgray"]),
+                        _p(disp), C.byref(d))
+    if st != 0:
+        raise ValueError("oracle rejected the configuration")
+    return {"disp": disp, "stage_ms": list(ms), **bufs}
+
+
+def lr_check(d0: np.ndarray, d1: np.ndarray, cfg: Config) -> np.ndarray:
+    out = np.ascontiguousarray(d0, np.int16).copy()
+    load().smo_lr_check(C.byref(cfg), _p(out), _p(np.ascontiguousarray(d1, np.int16)))
+    return out
+
+
+def region_vote(dp: np.ndarray, arms_l: np.ndarray, cfg: Config) -> np.ndarray:
+    out = np.ascontiguousarray(dp, np.int16).copy()
+    load().smo_region_vote(C.byref(cfg), _p(out), _p(np.ascontiguousarray(arms_l, np.uint16)), cfg.rv_ratio, cfg.rv_s)
+    return out
+
+
+def proper_ipol(dp: np.ndarray, bgr: np.ndarray, cfg: Config) -> np.ndarray:
+    out = np.ascontiguousarray(dp, np.int16).copy()
+    load().smo_proper_ipol(C.byref(cfg), _p(out), _p(np.ascontiguousarray(bgr, np.uint8)))
+    return out
+
+
+def median3(dp: np.ndarray) -> np.ndarray:
+    out = np.ascontiguousarray(dp, np.int16).copy()
+    load().smo_median3(out.shape[0], out.shape[1], _p(out))
+    return out
+
+
+def refine(d0, d1, arms_l, bgr, cfg: Config) -> np.ndarray:
+    out = np.ascontiguousarray(d0, np.int16).copy()
+    load().smo_refine(C.byref(cfg), _p(out), _p(np.ascontiguousarray(d1, np.int16)),
+                      _p(np.ascontiguousarray(arms_l, np.uint16)), _p(np.ascontiguousarray(bgr, np.uint8)))
     return out
 
 

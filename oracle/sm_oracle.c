@@ -61,6 +61,15 @@ void smo_default_config(smo_config* c, int maxdisp, int H, int W) {
     c->sgm_p2 = 3.0f;            /* updateCost P2 (h:2235) */
     c->sgm_cor_thres = 15;       /* sgm_corDifThres (h:239) */
     c->sgm_redu = 4;             /* sgm_reduCoeffi1 (h:240) */
+    c->do_refine = 0;            /* Do_refine (h:70) */
+    c->lr_max_diff = 0.0f;       /* LRmaxDiff (h:212) */
+    c->do_region_vote = 1;       /* Do_regionVote (h:75) */
+    c->region_vote_nums = 2;     /* region_vote_nums (h:306) */
+    c->rv_ratio = 0.4f;          /* rv_ratio[] (cpp:1400) */
+    c->rv_s = 20;                /* rv_s[] (cpp:1401) */
+    c->do_proper_ipol = 1;       /* Do_properIpol (h:76) */
+    c->disp_occ = -2 * 16;       /* DISP_OCC (h:216) */
+    c->do_last_median = 1;       /* Do_lastMedianBlur (h:80) */
 }
 
 /* OpenCV borderInterpolate, BORDER_REFLECT_101 (used by copyMakeBorder, h:870-871). */
@@ -340,11 +349,15 @@ void smo_cost_volume(const smo_config* c, const uint8_t* bgrL, const uint8_t* bg
     free(cR);
 }
 
-/* HVL_INTERSECTION[0] element k at (v,u,d) — genTrueHorVerArms (cpp:2794-2845), left view:
- * min(HVL[0](v,u)[k], HVL[1](v,u-d)[k]); zero (memset, cpp:2799-2800) once u-d < 0. */
-static inline int isect(const uint16_t* aL, const uint16_t* aR, int W, int v, int u, int d, int k) {
-    if (u - d < 0) return 0;
-    int a = aL[((size_t)v * W + u) * 4 + k], b = aR[((size_t)v * W + (u - d)) * 4 + k];
+/* HVL_INTERSECTION[num] element k at (v,u,d) — genTrueHorVerArms (cpp:2794-2845):
+ * num 0 (left view):  u_l = u,     u_r = u - d;
+ * num 1 (right view): u_l = u + d, u_r = u;
+ * value min(HVL[0](v,u_l)[k], HVL[1](v,u_r)[k]); zero (memset, cpp:2799-2800) once u_r < 0 or
+ * u_l >= w (the d loop breaks, cpp:2821-2822). */
+static inline int isect(const uint16_t* aL, const uint16_t* aR, int W, int v, int u, int d, int k, int view) {
+    const int ul = view ? u + d : u, ur = view ? u : u - d;
+    if (ur < 0 || ul >= W) return 0;
+    int a = aL[((size_t)v * W + ul) * 4 + k], b = aR[((size_t)v * W + ur) * 4 + k];
     return imin(a, b);
 }
 
@@ -369,7 +382,7 @@ static void cumu(const smo_config* c, float* vm, int32_t* area, int dv, int du) 
 
 /* cal1DCost (h:1643-1715) with cbca_intersect = 1; writes temps then copies back. */
 static void cost1d(const smo_config* c, float* vm, int32_t* area, float* vmT, int32_t* areaT,
-                   const uint16_t* aL, const uint16_t* aR, int dv, int du, int direc) {
+                   const uint16_t* aL, const uint16_t* aR, int dv, int du, int direc, int view) {
     const int H = c->H, W = c->W, n = c->D;
     const int head_num = direc * 2 + 1, tail_num = direc * 2;
     for (int v = 0; v < H; v++)
@@ -377,7 +390,7 @@ static void cost1d(const smo_config* c, float* vm, int32_t* area, float* vmT, in
             float* vT = vmT + ((size_t)v * W + u) * n;
             int32_t* aT = areaT + ((size_t)v * W + u) * n;
             for (int d = 0; d < n; d++) {
-                int tailL = isect(aL, aR, W, v, u, d, tail_num), headL = isect(aL, aR, W, v, u, d, head_num);
+                int tailL = isect(aL, aR, W, v, u, d, tail_num, view), headL = isect(aL, aR, W, v, u, d, head_num, view);
                 int tail_u = u + du * tailL, tail_v = v + dv * tailL;
                 int head_u = u - du * headL, head_v = v - dv * headL;
                 int pre_tailU = tail_u + du, pre_tailV = tail_v + dv;
@@ -397,8 +410,10 @@ static void cost1d(const smo_config* c, float* vm, int32_t* area, float* vmT, in
     memcpy(area, areaT, (size_t)H * W * n * 4);
 }
 
-/* cbca_core (cpp:5585-5666) for LOR = 0 only (imgNum = Do_refine && Do_LRConsis ? 2 : 1). */
-void smo_cbca(const smo_config* c, float* vm, const uint16_t* aL, const uint16_t* aR) {
+/* cbca_core (cpp:5585-5666) for one LOR (imgNum = Do_refine && Do_LRConsis ? 2 : 1). */
+void smo_cbca(const smo_config* c, float* vm, const uint16_t* aL, const uint16_t* aR) { smo_cbca_view(c, vm, aL, aR, 0); }
+
+void smo_cbca_view(const smo_config* c, float* vm, const uint16_t* aL, const uint16_t* aR, int view) {
     const size_t nvol = (size_t)c->H * c->W * c->D;
     const int du[2] = {-1, 0}, dv[2] = {0, -1};
     int32_t* area = (int32_t*)malloc(nvol * 4);
@@ -408,14 +423,14 @@ void smo_cbca(const smo_config* c, float* vm, const uint16_t* aL, const uint16_t
         for (size_t i = 0; i < nvol; i++) area[i] = 1;  /* Scalar::all(1) (cpp:5604) */
         if (it % 2 == 0) {
             cumu(c, vm, area, dv[0], du[0]);
-            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[0], du[0], 0);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[0], du[0], 0, view);
             cumu(c, vm, area, dv[1], du[1]);
-            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[1], du[1], 1);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[1], du[1], 1, view);
         } else {
             cumu(c, vm, area, dv[1], du[1]);
-            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[1], du[1], 1);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[1], du[1], 1, view);
             cumu(c, vm, area, dv[0], du[0]);
-            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[0], du[0], 0);
+            cost1d(c, vm, area, vmT, areaT, aL, aR, dv[0], du[0], 0, view);
         }
         for (size_t i = 0; i < nvol; i++) vm[i] /= area[i];  /* genfinalVm_cbca (cpp:3969-3992) */
     }
@@ -441,8 +456,9 @@ void smo_solve_all(const smo_config* c, float* vm) {
     }
 }
 
-/* updateCost<float> (h:2206-2280) for one pixel, leftFirst = true (D2 is computed there
- * but never used, so it is omitted). */
+/* updateCost<float> (h:2206-2280) for one pixel.  D1 compares I_c[0] when leftFirst, I_c[1]
+ * otherwise (h:2219-2224): the caller passes that view's colour image.  D2 is computed there but
+ * never used, so it is omitted. */
 static void update_cost(const smo_config* c, float* Lr, const float* vm, const uint8_t* Ic, int v, int u,
                         int rv, int ru, int preIsInner) {
     const int W = c->W, n = c->D;
@@ -474,7 +490,8 @@ static void update_cost(const smo_config* c, float* Lr, const float* vm, const u
     }
 }
 
-/* sgm (cpp:6204-6224) + costScan (cpp:1983-2029) + gen_sgm_vm (cpp:2031-2056). */
+/* sgm (cpp:6204-6224) + costScan (cpp:1983-2029) + gen_sgm_vm (cpp:2031-2056).  Ic = I_c[0] for
+ * vm[0] (leftFirst = true), I_c[1] for vm[1] (dispOptimize, cpp:1057-1059). */
 void smo_sgm(const smo_config* c, float* vm, const uint8_t* Ic) {
     static const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};  /* cpp:6207 */
     static const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};  /* cpp:6208 */
@@ -517,41 +534,255 @@ void smo_wta(const smo_config* c, const float* vm, int16_t* disp) {
     }
 }
 
+/* LRConsistencyCheck_normal (cpp:2262-2282), LOR = 0: a left disparity survives only if the
+ * right map at u - d agrees within LRmaxDiff; otherwise -1. */
+void smo_lr_check(const smo_config* c, int16_t* disp0, const int16_t* disp1) {
+    const int H = c->H, W = c->W;
+    for (int v = 0; v < H; v++) {
+        int16_t* D1 = disp0 + (size_t)v * W;
+        const int16_t* D2 = disp1 + (size_t)v * W;
+        for (int u = 0; u < W; u++) {
+            const int16_t d = D1[u];
+            /* abs(int) > float: the int difference converts to float (exact for |x| < 2^24) */
+            if (d < 0 || u - d < 0 || (float)abs(d - D2[u - d]) > c->lr_max_diff) D1[u] = -1;
+        }
+    }
+}
+
+/* regionVote_my (cpp:7219-7277): every invalid pixel collects the valid disparities of its
+ * cross region (rows v-U..v+D of its own column, each row spanning that row's L/R arms at the
+ * column, HVL[0]); with more than rv_s of them the most frequent one (first maximum) replaces it
+ * when hist[most] / validNum >= rv_ratio — an INTEGER division (cpp:7270).  Reads Dp, writes a
+ * copy (dp_res). */
+void smo_region_vote(const smo_config* c, int16_t* disp, const uint16_t* armsL, float rv_ratio, int rv_s) {
+    const int H = c->H, W = c->W, n = c->D;
+    int16_t* res = (int16_t*)malloc((size_t)H * W * 2);
+    int* hist = (int*)malloc((size_t)n * sizeof(int));
+    memcpy(res, disp, (size_t)H * W * 2);
+    for (int v = 0; v < H; v++)
+        for (int u = 0; u < W; u++) {
+            if (disp[(size_t)v * W + u] >= 0) continue;
+            for (int d = 0; d < n; d++) hist[d] = 0;
+            int validNum = 0;
+            const uint16_t* a = armsL + ((size_t)v * W + u) * 4;
+            const int v_begin = v - a[2], v_end = v + a[3];
+            for (int vn = v_begin; vn <= v_end; vn++) {
+                const uint16_t* an = armsL + ((size_t)vn * W + u) * 4;
+                const int u_begin = u - an[0], u_end = u + an[1];
+                const int16_t* dp = disp + (size_t)vn * W;
+                for (int un = u_begin; un <= u_end; un++)
+                    if (dp[un] >= 0) {
+                        validNum++;
+                        hist[dp[un]]++;
+                    }
+            }
+            if (validNum <= rv_s) continue;
+            int most = 0;
+            for (int d = 1; d < n; d++)
+                if (hist[d] > hist[most]) most = d;
+            if ((float)(hist[most] / validNum) >= rv_ratio) res[(size_t)v * W + u] = (int16_t)most;
+        }
+    memcpy(disp, res, (size_t)H * W * 2);
+    free(res);
+    free(hist);
+}
+
+/* properIpol (cpp:7395-7490): each invalid pixel searches 16 directions up to 20 steps for the
+ * first valid disparity (steps alternate pw/2 and pw - pw/2, C truncating division); DISP_OCC
+ * pixels take the smallest found disparity, others the one whose colour (max channel |diff| of
+ * I_c[0]) is closest, first strict minimum below 255.  Reads Dp, writes a copy. */
+void smo_proper_ipol(const smo_config* c, int16_t* disp, const uint8_t* bgrL) {
+    static const int DW[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -2, -1};
+    static const int DH[16] = {2, 2, 0, -2, -2, -2, 0, 2, 2, 1, -1, -2, -2, -1, 1, 2};
+    const int h = c->H, w = c->W, searchDepth = 20;
+    int16_t* cp = (int16_t*)malloc((size_t)h * w * 2);
+    for (int v = 0; v < h; v++)
+        for (int u = 0; u < w; u++) {
+            const int16_t dv = disp[(size_t)v * w + u];
+            if (dv >= 0) {
+                cp[(size_t)v * w + u] = dv;
+                continue;
+            }
+            int dDisp[16], dDiff[16];
+            for (int k = 0; k < 16; k++) {
+                dDisp[k] = -1;
+                dDiff[k] = -1;
+                const int ph = DH[k], pw = DW[k];
+                int posw = u, posh = v;
+                for (int dep = 0; dep < searchDepth; dep++) {
+                    if (dep % 2 == 0) {
+                        posw += pw / 2;
+                        posh += ph / 2;
+                    } else {
+                        posw += pw - pw / 2;
+                        posh += ph - ph / 2;
+                    }
+                    if (!(posw >= 0 && posw < w && posh >= 0 && posh < h)) break;
+                    const int16_t q = disp[(size_t)posh * w + posw];
+                    if (q >= 0) {
+                        dDisp[k] = q;
+                        int cd = 0;
+                        for (int ch = 0; ch < 3; ch++) {
+                            int x = abs((int)bgrL[((size_t)v * w + u) * 3 + ch] - (int)bgrL[((size_t)posh * w + posw) * 3 + ch]);
+                            if (x > cd) cd = x;
+                        }
+                        dDiff[k] = cd;
+                        break;
+                    }
+                }
+            }
+            if (dv == c->disp_occ) {
+                int minDisp = 2147483647;
+                for (int k = 0; k < 16; k++)
+                    if (dDisp[k] >= 0 && minDisp > dDisp[k]) minDisp = dDisp[k];
+                cp[(size_t)v * w + u] = minDisp != 2147483647 ? (int16_t)minDisp : dv;
+            } else {
+                int minDif = 255, best = -1;
+                for (int k = 0; k < 16; k++)
+                    if (dDiff[k] >= 0 && minDif > dDiff[k]) {
+                        minDif = dDiff[k];
+                        best = dDisp[k];
+                    }
+                cp[(size_t)v * w + u] = best >= 0 ? (int16_t)best : dv;
+            }
+        }
+    memcpy(disp, cp, (size_t)h * w * 2);
+    free(cp);
+}
+
+/* cv::medianBlur(DP[0], DP[0], 3) (cpp:1497-1505) on CV_16S: the 3x3 sorting-network path, rows
+ * and columns clamped at the border (replicate); in place means the source is copied first. */
+static int16_t med3(int16_t a, int16_t b, int16_t c) {
+    int16_t t;
+    if (a > b) { t = a; a = b; b = t; }
+    if (b > c) { t = b; b = c; c = t; }
+    if (a > b) { t = a; a = b; b = t; }
+    return b;
+}
+void smo_median3(int H, int W, int16_t* disp) {
+    int16_t* src = (int16_t*)malloc((size_t)H * W * 2);
+    memcpy(src, disp, (size_t)H * W * 2);
+    if (H == 1 || W == 1) {
+        const int len = H * W;
+        for (int i = 0; i < len; i++)
+            disp[i] = med3(src[i > 0 ? i - 1 : 0], src[i], src[i < len - 1 ? i + 1 : len - 1]);
+    } else {
+        int16_t p[9];
+        for (int v = 0; v < H; v++)
+            for (int u = 0; u < W; u++) {
+                int k = 0;
+                for (int dv = -1; dv <= 1; dv++)
+                    for (int du = -1; du <= 1; du++) {
+                        int vv = imin(imax(v + dv, 0), H - 1), uu = imin(imax(u + du, 0), W - 1);
+                        p[k++] = src[(size_t)vv * W + uu];
+                    }
+                for (int i = 1; i < 9; i++)  /* insertion sort; the median of 9 is unique */
+                    for (int j = i; j > 0 && p[j - 1] > p[j]; j--) {
+                        int16_t t = p[j];
+                        p[j] = p[j - 1];
+                        p[j - 1] = t;
+                    }
+                disp[(size_t)v * W + u] = p[4];
+            }
+    }
+    free(src);
+}
+
+/* refine(), non-USE_RECONCV branch (cpp:1347-1510) with the default stage switches (h:72-81):
+ * LR check, region_vote_nums x regionVote_my(0.4, 20), region_vote_nums x properIpol, 3x3 median. */
+void smo_refine(const smo_config* c, int16_t* disp0, const int16_t* disp1, const uint16_t* armsL, const uint8_t* bgrL) {
+    smo_lr_check(c, disp0, disp1);                                     /* Do_LRConsis (cpp:1364-1375) */
+    if (c->do_region_vote)
+        for (int i = 0; i < c->region_vote_nums; i++) smo_region_vote(c, disp0, armsL, c->rv_ratio, c->rv_s);  /* cpp:1390-1422 */
+    if (c->do_proper_ipol)
+        for (int i = 0; i < c->region_vote_nums; i++) smo_proper_ipol(c, disp0, bgrL);   /* cpp:1437-1451 */
+    if (c->do_last_median) smo_median3(c->H, c->W, disp0);                              /* cpp:1497-1505 */
+}
+
+/* main:138-166 for one pair: costCalculate, SolveAll(PY_LVL = 1), dispOptimize, [refine]. */
+int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR, const uint8_t* grayL,
+               const uint8_t* grayR, int16_t* disp, const smo_dumps* dd) {
+    if (c->H < 2 || c->W < 2 || c->D < 1) return -1;
+    smo_dumps none;
+    memset(&none, 0, sizeof(none));
+    const smo_dumps* d = dd ? dd : &none;
+    const int refine = c->do_refine;
+    const int views = refine ? 2 : 1;
+    const size_t npix = (size_t)c->H * c->W, nvol = npix * c->D;
+    double t0 = now_ms(), t;
+    double ms[7] = {0, 0, 0, 0, 0, 0, 0};
+    float* vm[2] = {NULL, NULL};
+    int16_t* dp1 = NULL;
+    uint16_t *aL = NULL, *aR = NULL;
+    int rc = -1;
+    vm[0] = (float*)malloc(nvol * 4);
+    if (!vm[0]) goto done;
+    if (refine && !(vm[1] = (float*)malloc(nvol * 4))) goto done;
+    smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 0, vm[0]);
+    if (refine) smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 1, vm[1]);
+    else if (d->vol_right) smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 1, d->vol_right);
+    if (refine && d->vol_right) memcpy(d->vol_right, vm[1], nvol * 4);
+    if (d->vol_cost) memcpy(d->vol_cost, vm[0], nvol * 4);
+    t = now_ms(); ms[0] = t - t0; t0 = t;
+    if (c->aggregation == 1 || refine) {
+        aL = (uint16_t*)malloc(npix * 8);
+        aR = (uint16_t*)malloc(npix * 8);
+        if (!aL || !aR) goto done;
+        smo_arms(c, bgrL, aL);                   /* calArms for both images (cpp:5358-5385) */
+        smo_arms(c, bgrR, aR);
+    }
+    if (c->aggregation == 1)
+        for (int i = 0; i < views; i++) smo_cbca_view(c, vm[i], aL, aR, i);   /* cbca_core LOR loop (cpp:5598) */
+    if (d->vol_agg) memcpy(d->vol_agg, vm[0], nvol * 4);
+    if (refine && d->vol_agg_right) memcpy(d->vol_agg_right, vm[1], nvol * 4);
+    t = now_ms(); ms[1] = t - t0; t0 = t;
+    if (c->solve_all)
+        for (int i = 0; i < views; i++) smo_solve_all(c, vm[i]);               /* img_n (cpp:2178) */
+    t = now_ms(); ms[2] = t - t0; t0 = t;
+    if (c->optimization == 1)
+        for (int i = 0; i < views; i++) smo_sgm(c, vm[i], i == 0 ? bgrL : bgrR);  /* cpp:1053-1060 */
+    if (d->vol_final) memcpy(d->vol_final, vm[0], nvol * 4);
+    t = now_ms(); ms[3] = t - t0; t0 = t;
+    smo_wta(c, vm[0], disp);
+    if (refine) {
+        if (!(dp1 = (int16_t*)malloc(npix * 2))) goto done;
+        smo_wta(c, vm[1], dp1);                                                /* cpp:1110-1127 */
+        if (d->disp_left_raw) memcpy(d->disp_left_raw, disp, npix * 2);
+        if (d->disp_right) memcpy(d->disp_right, dp1, npix * 2);
+    }
+    t = now_ms(); ms[4] = t - t0; t0 = t;
+    if (refine) smo_refine(c, disp, dp1, aL, bgrL);                           /* main:165-166 */
+    t = now_ms(); ms[5] = t - t0;
+    ms[6] = ms[0] + ms[1] + ms[2] + ms[3] + ms[4] + ms[5];
+    if (d->stage_ms) memcpy(d->stage_ms, ms, sizeof(ms));
+    rc = 0;
+done:
+    free(vm[0]);
+    free(vm[1]);
+    free(dp1);
+    free(aL);
+    free(aR);
+    return rc;
+}
+
 int smo_run(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
             const uint8_t* grayL, const uint8_t* grayR, int16_t* disp,
             float* vol_cost, float* vol_agg, float* vol_final, float* vol_right, double* stage_ms) {
-    if (c->H < 2 || c->W < 2 || c->D < 1) return -1;
-    const size_t npix = (size_t)c->H * c->W, nvol = npix * c->D;
-    double t0 = now_ms(), t;
-    float* vm = (float*)malloc(nvol * 4);
-    if (!vm) return -1;
-    double ms[6] = {0, 0, 0, 0, 0, 0};
-    smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 0, vm);
-    if (vol_right) smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 1, vol_right);
-    if (vol_cost) memcpy(vol_cost, vm, nvol * 4);
-    t = now_ms(); ms[0] = t - t0; t0 = t;
-    if (c->aggregation == 1) {
-        uint16_t* aL = (uint16_t*)malloc(npix * 8);
-        uint16_t* aR = (uint16_t*)malloc(npix * 8);
-        smo_arms(c, bgrL, aL);                   /* calArms for both images (cpp:5358-5385) */
-        smo_arms(c, bgrR, aR);
-        smo_cbca(c, vm, aL, aR);
-        free(aL);
-        free(aR);
+    double ms[7];
+    smo_dumps d;
+    memset(&d, 0, sizeof(d));
+    d.vol_cost = vol_cost;
+    d.vol_agg = vol_agg;
+    d.vol_final = vol_final;
+    d.vol_right = vol_right;
+    d.stage_ms = ms;
+    int rc = smo_run_ex(c, bgrL, bgrR, grayL, grayR, disp, &d);
+    if (rc == 0 && stage_ms) {   /* legacy layout: cost, cbca, solveall, sgm, wta (+refine), total */
+        memcpy(stage_ms, ms, 4 * sizeof(double));
+        stage_ms[4] = ms[4] + ms[5];
+        stage_ms[5] = ms[6];
     }
-    if (vol_agg) memcpy(vol_agg, vm, nvol * 4);
-    t = now_ms(); ms[1] = t - t0; t0 = t;
-    if (c->solve_all) smo_solve_all(c, vm);
-    t = now_ms(); ms[2] = t - t0; t0 = t;
-    if (c->optimization == 1) smo_sgm(c, vm, bgrL);
-    if (vol_final) memcpy(vol_final, vm, nvol * 4);
-    t = now_ms(); ms[3] = t - t0; t0 = t;
-    smo_wta(c, vm, disp);
-    t = now_ms(); ms[4] = t - t0;
-    ms[5] = ms[0] + ms[1] + ms[2] + ms[3] + ms[4];
-    if (stage_ms) memcpy(stage_ms, ms, sizeof(ms));
-    free(vm);
-    return 0;
+    return rc;
 }
 
 /* calErr (h:1748-1825): bad pixel ratio over mask == 255 with threshold `thres`. */

@@ -48,6 +48,16 @@ typedef struct smo_config {
     float sgm_p1, sgm_p2;        /* 1.0, 3.0 hard-coded in updateCost (h:2234-2235) */
     int sgm_cor_thres;           /* sgm_corDifThres = 15 (h:239) */
     int sgm_redu;                /* sgm_reduCoeffi1 = 4 (h:240) */
+    /* refinement (refine(), cpp:1138-1511, non-USE_RECONCV branch cpp:1347-1510) */
+    int do_refine;               /* Do_refine (h:70; default 0): both views through CBCA/SGM + refine() */
+    float lr_max_diff;           /* LRmaxDiff = 0 (h:212) */
+    int do_region_vote;          /* Do_regionVote = 1 (h:75) */
+    int region_vote_nums;        /* region_vote_nums = 2 (h:306) */
+    float rv_ratio;              /* rv_ratio[i] = 0.4 (cpp:1400) */
+    int rv_s;                    /* rv_s[i] = 20 (cpp:1401) */
+    int do_proper_ipol;          /* Do_properIpol = 1 (h:76) */
+    int disp_occ;                /* DISP_OCC = -2 * 16 (h:216) */
+    int do_last_median;          /* Do_lastMedianBlur = 1 (h:80) */
 } smo_config;
 
 void smo_default_config(smo_config* c, int maxdisp, int H, int W);
@@ -64,11 +74,36 @@ void smo_arms(const smo_config* c, const uint8_t* bgr, uint16_t* arms /* H*W*4 *
 /* Cost volume for one view (0 = left reference, 1 = right), H*W*D floats. */
 void smo_cost_volume(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
                      const uint8_t* grayL, const uint8_t* grayR, int view, float* vm);
+/* view 0: intersection min(armsL(u), armsR(u-d)); view 1: min(armsL(u+d), armsR(u)) (cpp:2794-2845) */
 void smo_cbca(const smo_config* c, float* vm, const uint16_t* armsL, const uint16_t* armsR);
+void smo_cbca_view(const smo_config* c, float* vm, const uint16_t* armsL, const uint16_t* armsR, int view);
 float smo_solve_all_weight(float reg_lambda);
 void smo_solve_all(const smo_config* c, float* vm);
 void smo_sgm(const smo_config* c, float* vm, const uint8_t* bgrL);
 void smo_wta(const smo_config* c, const float* vm, int16_t* disp);
+
+/* refine() stages (cpp:1364-1506); all act in place on an H*W int16 map. */
+void smo_lr_check(const smo_config* c, int16_t* disp0, const int16_t* disp1);          /* cpp:2262-2282 */
+void smo_region_vote(const smo_config* c, int16_t* disp, const uint16_t* armsL,
+                     float rv_ratio, int rv_s);                                      /* cpp:7219-7277 */
+void smo_proper_ipol(const smo_config* c, int16_t* disp, const uint8_t* bgrL);        /* cpp:7395-7490 */
+void smo_median3(int H, int W, int16_t* disp);                                        /* cv::medianBlur(.,.,3) */
+void smo_refine(const smo_config* c, int16_t* disp0, const int16_t* disp1, const uint16_t* armsL,
+                const uint8_t* bgrL);                                                  /* cpp:1347-1510 */
+
+/* Optional intermediate outputs of smo_run_ex (any may be NULL). */
+typedef struct smo_dumps {
+    float* vol_cost;             /* vm[0] after the cost stage */
+    float* vol_agg;              /* vm[0] after CBCA */
+    float* vol_final;            /* vm[0] after the SGM path sum */
+    float* vol_right;            /* vm[1] cost volume */
+    float* vol_agg_right;        /* vm[1] after CBCA (do_refine) */
+    int16_t* disp_left_raw;      /* DP[0] after WTA, before refine() (do_refine) */
+    int16_t* disp_right;         /* DP[1] after WTA (do_refine) */
+    double* stage_ms;            /* [7]: cost, cbca, solveall, sgm, wta, refine, total */
+} smo_dumps;
+int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
+               const uint8_t* grayL, const uint8_t* grayR, int16_t* disp, const smo_dumps* d);
 
 /* Whole default pipeline for one pair (main:138-163 call order).  Optional dumps may be NULL:
  * vol_cost = vm[0] after the cost stage, vol_agg = after CBCA, vol_final = after SGM sum,

@@ -171,18 +171,23 @@ def fuse(vm0, vm1, lam0, lam1):
     return ((f32(2) - e0).astype(f32) - e1).astype(f32)
 
 
-def isect(aL, aR, D):
+def isect(aL, aR, D, view=0):
+    """HVL_INTERSECTION[view] (cpp:2794-2845): view 0 pairs left u with right u - d, view 1 left
+    u + d with right u; pairs falling outside the image stay 0 (memset)."""
     H, W, _ = aL.shape
     out = np.zeros((H, W, D, 4), np.int32)
     for d in range(D):
         if d < W:
-            out[:, d:, d, :] = np.minimum(aL[:, d:, :], aR[:, :W - d, :])
+            if view == 0:
+                out[:, d:, d, :] = np.minimum(aL[:, d:, :], aR[:, :W - d, :])
+            else:
+                out[:, :W - d, d, :] = np.minimum(aL[:, d:, :], aR[:, :W - d, :])
     return out
 
 
-def cbca(vm, aL, aR, iters=2):
+def cbca(vm, aL, aR, iters=2, view=0):
     H, W, D = vm.shape
-    A = isect(aL, aR, D)
+    A = isect(aL, aR, D, view)
     vm = vm.copy()
     vv, uu, dd = np.meshgrid(np.arange(H), np.arange(W), np.arange(D), indexing="ij")
 
@@ -270,8 +275,103 @@ def wta(vm):
     return out
 
 
-def pipeline(pair, max_disp, cost="censusGrad", aggregate=True, solve=True, optimize=True, paths=4):
-    """Default main_.cpp sequence; returns dict of stage volumes and the disparity map."""
+def lr_check(d0, d1, maxdiff=f32(0)):
+    """LRConsistencyCheck_normal (cpp:2262-2282)."""
+    H, W = d0.shape
+    out = d0.copy()
+    uu = np.broadcast_to(np.arange(W), (H, W))
+    d = d0.astype(np.int64)
+    src = uu - d
+    ok = (d >= 0) & (src >= 0)
+    partner = np.where(ok, np.take_along_axis(d1.astype(np.int64), np.clip(src, 0, W - 1), axis=1), 0)
+    bad = ~ok | (np.abs(d - partner).astype(f32) > f32(maxdiff))
+    out[bad] = -1
+    return out
+
+
+def region_vote(dp, aL, D, ratio=f32(0.4), s=20):
+    """regionVote_my (cpp:7219-7277): histogram of the valid disparities in the cross region,
+    first maximum, integer hist/validNum compared with the float ratio (cpp:7270)."""
+    H, W = dp.shape
+    res = dp.copy()
+    for v in range(H):
+        for u in range(W):
+            if dp[v, u] >= 0:
+                continue
+            vals = []
+            for vn in range(v - int(aL[v, u, 2]), v + int(aL[v, u, 3]) + 1):
+                row = dp[vn, u - int(aL[vn, u, 0]): u + int(aL[vn, u, 1]) + 1]
+                vals.append(row[row >= 0])
+            vals = np.concatenate(vals).astype(np.int64)
+            if vals.size <= s:
+                continue
+            hist = np.bincount(vals, minlength=D)
+            most = int(np.argmax(hist))   # first maximum
+            if f32(int(hist[most]) // int(vals.size)) >= f32(ratio):
+                res[v, u] = most
+    return res
+
+
+def proper_ipol(dp, bgr, occ=-32, depth=20):
+    """properIpol (cpp:7395-7490)."""
+    DW = [0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -2, -1]
+    DH = [2, 2, 0, -2, -2, -2, 0, 2, 2, 1, -1, -2, -2, -1, 1, 2]
+    tdiv = lambda a, b: int(a / b)   # C truncating division
+    H, W = dp.shape
+    I = bgr.astype(np.int64)
+    out = dp.copy()
+    for v in range(H):
+        for u in range(W):
+            if dp[v, u] >= 0:
+                continue
+            found = []   # (direction order) disparity, colour difference
+            for k in range(16):
+                pv, pu = v, u
+                for dep in range(depth):
+                    if dep % 2 == 0:
+                        pu += tdiv(DW[k], 2)
+                        pv += tdiv(DH[k], 2)
+                    else:
+                        pu += DW[k] - tdiv(DW[k], 2)
+                        pv += DH[k] - tdiv(DH[k], 2)
+                    if not (0 <= pu < W and 0 <= pv < H):
+                        break
+                    if dp[pv, pu] >= 0:
+                        found.append((int(dp[pv, pu]), int(np.max(np.abs(I[v, u] - I[pv, pu])))))
+                        break
+            if dp[v, u] == occ:
+                if found:
+                    out[v, u] = min(f[0] for f in found)
+            else:
+                cand = [f for f in found if f[1] < 255]
+                if cand:
+                    best = min(range(len(cand)), key=lambda i: (cand[i][1], i))
+                    out[v, u] = cand[best][0]
+    return out
+
+
+def median3(dp):
+    """cv::medianBlur(src, dst, 3) with replicated borders."""
+    H, W = dp.shape
+    P = np.pad(dp, 1, mode="edge")
+    stack = np.stack([P[i:i + H, j:j + W] for i in range(3) for j in range(3)])
+    return np.sort(stack, axis=0)[4].astype(np.int16)
+
+
+def refine(d0, d1, aL, bgrL, D, nums=2):
+    """refine(), cpp:1347-1510 with the default stage switches (h:72-81)."""
+    d = lr_check(d0, d1)
+    for _ in range(nums):
+        d = region_vote(d, aL, D)
+    for _ in range(nums):
+        d = proper_ipol(d, bgrL)
+    return median3(d)
+
+
+def pipeline(pair, max_disp, cost="censusGrad", aggregate=True, solve=True, optimize=True, paths=4,
+             refine_on=False):
+    """Default main_.cpp sequence; returns dict of stage volumes and the disparity map.
+    refine_on: Do_refine = 1 (both views through CBCA / SolveAll / SGM / WTA, then refine())."""
     D = max_disp + 1
     lb, rb, lg, rg = pair["lbgr"], pair["rbgr"], pair["lgray"], pair["rgray"]
     out = {}
@@ -299,4 +399,20 @@ def pipeline(pair, max_disp, cost="censusGrad", aggregate=True, solve=True, opti
         vm = sgm(vm, lb, paths=paths)
     out["final"] = vm
     out["disp"] = wta(vm)
+    if refine_on:
+        assert cost == "censusGrad"
+        gx0, gy0 = grads(lg)
+        gx1, gy1 = grads(rg)
+        v1 = fuse(census_cost(census(lg), census(rg), D, view=1),
+                  grad_cost(gx0, gx1, gy0, gy1, arms(rb), D, view=1), 13, 1)
+        if aggregate:
+            v1 = cbca(v1, arms(lb), arms(rb), view=1)
+        out["agg_right"] = v1
+        if solve:
+            v1 = solve_all(v1)
+        if optimize:
+            v1 = sgm(v1, rb, paths=paths)
+        out["disp_right"] = wta(v1)
+        out["disp_raw"] = out["disp"]
+        out["disp"] = refine(out["disp"], out["disp_right"], arms(lb), lb, D)
     return out

@@ -84,3 +84,74 @@ def test_reflect101(oracle):
     for n in (1, 2, 3, 5):
         for p in range(-9, 14):
             assert lib.smo_reflect101(p, n) == pyref.reflect101(p, n)
+
+
+# ---- refine() path (Do_refine = 1): right-view CBCA/SGM and the refinement stages ----------
+
+@pytest.mark.parametrize("H,W,D,idx,smooth", [(10, 15, 6, 7, True), (12, 16, 8, 8, False)])
+def test_refine_pipeline_bitexact(oracle, H, W, D, idx, smooth):
+    p = tiny_pair(H, W, D, idx, smooth)
+    cfg = oracle.config(H, W, D - 1, do_refine=1)
+    got = oracle.run_ex(p, cfg, dumps=("agg", "agg_right", "disp_raw", "disp_right"))
+    ref = pyref.pipeline(p, D - 1, refine_on=True)
+    np.testing.assert_array_equal(got["agg"].view(np.uint32), ref["agg"].view(np.uint32))
+    np.testing.assert_array_equal(got["agg_right"].view(np.uint32), ref["agg_right"].view(np.uint32))
+    np.testing.assert_array_equal(got["disp_raw"], ref["disp_raw"])
+    np.testing.assert_array_equal(got["disp_right"], ref["disp_right"])
+    np.testing.assert_array_equal(got["disp"], ref["disp"])
+
+
+def _noisy_map(H, W, D, seed, invalid=0.3, occ=False):
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, D, size=(H // 4 + 1, W // 4 + 1))
+    dp = np.kron(base, np.ones((4, 4), np.int64))[:H, :W]
+    dp = np.where(rng.random((H, W)) < invalid, -32 if occ else -1, dp)
+    if occ:
+        dp = np.where(rng.random((H, W)) < 0.1, -1, dp)
+    return dp.astype(np.int16)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_refine_stages_vs_pyref(oracle, seed):
+    H, W, D = 23, 31, 9
+    p = tiny_pair(H, W, D, 20 + seed, smooth=True)
+    cfg = oracle.config(H, W, D - 1)
+    aL = oracle.arms(p["lbgr"], cfg)
+    d0, d1 = _noisy_map(H, W, D, seed, 0.1), _noisy_map(H, W, D, seed + 100, 0.1)
+    np.testing.assert_array_equal(oracle.lr_check(d0, d1, cfg), pyref.lr_check(d0, d1))
+    dm = _noisy_map(H, W, D, seed + 7, 0.4)
+    np.testing.assert_array_equal(oracle.region_vote(dm, aL, cfg), pyref.region_vote(dm, aL, D))
+    # uniform colour => long arms: the vote fills a hole only where every valid neighbour agrees
+    # (hist / validNum is an integer division, cpp:7270)
+    aU = oracle.arms(np.full((H, W, 3), 90, np.uint8), cfg)
+    flat = np.full((H, W), 3, np.int16)
+    flat[::5, ::3] = -1
+    got = oracle.region_vote(flat, aU, cfg)
+    np.testing.assert_array_equal(got, pyref.region_vote(flat, aU, D))
+    assert (got == 3).all()
+    mixed = flat.copy()
+    mixed[0, 1] = 5          # one dissenting neighbour in every region: no hole is filled
+    got = oracle.region_vote(mixed, aU, cfg)
+    np.testing.assert_array_equal(got, pyref.region_vote(mixed, aU, D))
+    np.testing.assert_array_equal(got, mixed)
+    for occ in (False, True):
+        dq = _noisy_map(H, W, D, seed + 11, 0.5, occ)
+        np.testing.assert_array_equal(oracle.proper_ipol(dq, p["lbgr"], cfg), pyref.proper_ipol(dq, p["lbgr"]))
+    dq = _noisy_map(H, W, D, seed + 13, 0.2)
+    np.testing.assert_array_equal(oracle.median3(dq), pyref.median3(dq))
+    np.testing.assert_array_equal(oracle.refine(d0, d1, aL, p["lbgr"], cfg),
+                                  pyref.refine(d0, d1, aL, p["lbgr"], D))
+
+
+def test_proper_ipol_colour_255_never_wins(oracle):
+    # minDifColor starts at 255 with a strict '>' (cpp:7470-7477): a neighbour whose colour
+    # differs by exactly 255 is never taken, so the pixel keeps its invalid value.
+    H, W, D = 5, 6, 4
+    bgr = np.zeros((H, W, 3), np.uint8)
+    bgr[2, 2] = 255
+    dp = np.full((H, W), 2, np.int16)
+    dp[2, 2] = -1
+    cfg = oracle.config(H, W, D - 1)
+    out = oracle.proper_ipol(dp, bgr, cfg)
+    assert out[2, 2] == -1
+    np.testing.assert_array_equal(out, pyref.proper_ipol(dp, bgr))

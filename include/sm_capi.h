@@ -13,6 +13,8 @@
  *   sm_cost_calculate  <- StereoMatching::costCalculate              stereoMatching.cpp:945-1021
  *   sm_solve_all       <- SolveAll(StereoMatching**&, PY_LVL, REG_LAMBDA)  stereoMatching.cpp:2142-2208
  *   sm_disp_optimize   <- StereoMatching::dispOptimize + DP[0]       stereoMatching.cpp:1046-1136, h:2724
+ *   sm_refine          <- StereoMatching::refine (Do_refine)         stereoMatching.cpp:1138-1511, main_.cpp:165-166
+ *   sm_get_disp / sm_set_disp <- public member DP[view]              stereoMatching.h:2724
  *   sm_get_volume      <- public member vm[view]                     stereoMatching.h:2720
  *   sm_get_arms        <- public member HVL[view]                    stereoMatching.h:2717
  *   sm_destroy         <- delete smPsy[p]                            main_.cpp:173-178
@@ -88,6 +90,18 @@ typedef struct sm_params {
     int32_t compute_right_view;  /* build vm[1] too (Do_LRConsis, h:72); 0 = skip (unused downstream) */
     int32_t keep_final_volume;   /* write the SGM path-sum back into vm[0] (reference does); 0 = fuse into WTA */
     int32_t batch_capacity;      /* max pairs per sm_run call (device buffers sized for it) */
+    /* refinement: Do_refine (h:70) = 1 runs vm[1] through CBCA / SolveAll / SGM / WTA as well
+     * (cbca_core cpp:5592, SolveAll cpp:2178, dispOptimize cpp:1054) and refine() afterwards
+     * (sm_refine; sm_run does both).  Stage switches and constants as in the reference. */
+    int32_t do_refine;           /* Do_refine = 0 (h:70) */
+    float lr_max_diff;           /* LRmaxDiff = 0 (h:212) */
+    int32_t do_region_vote;      /* Do_regionVote = 1 (h:75) */
+    int32_t region_vote_nums;    /* region_vote_nums = 2 (h:306): rounds of region vote and of properIpol */
+    float rv_ratio;              /* rv_ratio[i] = 0.4 (cpp:1400); must be > 0 */
+    int32_t rv_s;                /* rv_s[i] = 20 (cpp:1401) */
+    int32_t do_proper_ipol;      /* Do_properIpol = 1 (h:76) */
+    int32_t disp_occ;            /* DISP_OCC = -2 * 16 (h:216) */
+    int32_t do_last_median_blur; /* Do_lastMedianBlur = 1 (h:80) */
 } sm_params;
 
 typedef struct sm_ctx sm_ctx;
@@ -105,6 +119,11 @@ SM_API sm_status sm_set_images(sm_ctx* ctx, const uint8_t* lbgr, const uint8_t* 
 SM_API sm_status sm_cost_calculate(sm_ctx* ctx);
 SM_API sm_status sm_solve_all(sm_ctx* ctx, int32_t py_lev, float reg_lambda);
 SM_API sm_status sm_disp_optimize(sm_ctx* ctx, int16_t* disp_out);
+/* refine() on DP[0] (needs do_refine = 1 at sm_create and a preceding sm_disp_optimize). */
+SM_API sm_status sm_refine(sm_ctx* ctx, int16_t* disp_out);
+SM_API sm_status sm_get_disp(sm_ctx* ctx, int32_t view, int16_t* dst);  /* DP[view], H*W int16 */
+/* Overwrite DP[view] (the reference's DP is a public member, h:2724); after sm_disp_optimize. */
+SM_API sm_status sm_set_disp(sm_ctx* ctx, int32_t view, const int16_t* src);
 SM_API sm_status sm_get_volume(sm_ctx* ctx, int32_t view, float* dst);   /* H*W*D floats */
 SM_API sm_status sm_get_arms(sm_ctx* ctx, int32_t view, uint16_t* dst);  /* H*W*4 (L,R,U,D) */
 
@@ -113,7 +132,7 @@ SM_API sm_status sm_get_arms(sm_ctx* ctx, int32_t view, uint16_t* dst);  /* H*W*
  * device-to-device).  A device source must be complete before the call (its stream synchronized). */
 SM_API sm_status sm_upload_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
                                  const uint8_t* lgray, const uint8_t* rgray);
-/* Run cost -> CBCA -> SolveAll(py_lev=1, reg_lambda) -> SGM -> WTA on the n uploaded pairs.
+/* Run cost -> CBCA -> SolveAll(py_lev=1, reg_lambda) -> SGM -> WTA [-> refine] on the n uploaded pairs.
  * Asynchronous on the ctx stream.  disp_out: host or device [n][H][W] int16 (synchronous copy) or
  * NULL to leave the maps on the device (read them with sm_download_disp). */
 SM_API sm_status sm_run(sm_ctx* ctx, int32_t n, float reg_lambda, int16_t* disp_out);

@@ -35,8 +35,12 @@ class StereoMatching {
     inline static std::string costcalculation = "censusGrad";
     inline static std::string aggregation = "CBCA";
     inline static std::string optimization = "sgm";
-    static constexpr bool Do_refine = false;   // h:70
+    // h:70-80 are static const in the reference (compile-time); here they are read at construction
+    inline static bool Do_refine = false;      // h:70
     static constexpr bool Do_LRConsis = true;  // h:72
+    inline static bool Do_regionVote = true;   // h:75
+    inline static bool Do_properIpol = true;   // h:76
+    inline static bool Do_lastMedianBlur = true;  // h:80
 
     struct Parameters {  // StereoMatching::Parameters (h:85-351), the fields the hot path reads
         int numDisparities, rows, cols;
@@ -46,6 +50,9 @@ class StereoMatching {
         int cbca_crossL0 = 17, cbca_crossL_out0 = 34, cbca_cTresh0 = 20, cbca_cTresh_out0 = 6;
         int sgm_scanNum = 4, sgm_corDifThres = 15, sgm_reduCoeffi1 = 4;
         int errorThreshold = 1;
+        float LRmaxDiff = 0;                  // h:212
+        int DISP_OCC = -2 * 16;               // h:216
+        int region_vote_nums = 2;             // h:306
         Parameters(int maxDisp, int h, int w, int lamCen_ = 13, int lamG_ = 1, int /*M*/ = 2, int /*lamc*/ = 109,
                    int /*ts*/ = 10, const std::string& /*errCsvName*/ = "", int disSc_ = 1)
             : numDisparities(maxDisp + 1), rows(h), cols(w), lamCen(lamCen_), lamG(lamG_), disSc(disSc_) {}
@@ -79,6 +86,13 @@ class StereoMatching {
         p.sgm_paths = param.sgm_scanNum;
         p.sgm_cor_dif_thres = param.sgm_corDifThres;
         p.sgm_redu_coeff = param.sgm_reduCoeffi1;
+        p.do_refine = Do_refine ? 1 : 0;
+        p.lr_max_diff = param.LRmaxDiff;
+        p.disp_occ = param.DISP_OCC;
+        p.region_vote_nums = param.region_vote_nums;
+        p.do_region_vote = Do_regionVote ? 1 : 0;
+        p.do_proper_ipol = Do_properIpol ? 1 : 0;
+        p.do_last_median_blur = Do_lastMedianBlur ? 1 : 0;
         check(sm_create(&ctx_, &p, hip_device), "sm_create");
         if (I1_c.channels != 3 || I2_c.channels != 3 || I1_g.channels != 1 || I2_g.channels != 1)
             throw std::invalid_argument("expected BGR colour and single-channel gray images");
@@ -89,11 +103,18 @@ class StereoMatching {
     StereoMatching& operator=(const StereoMatching&) = delete;
 
     void costCalculate() { check(sm_cost_calculate(ctx_), "costCalculate"); }
-    void dispOptimize() {
+    void dispOptimize() {  // DP[0] (and DP[1] when Do_refine), cpp:1046-1136
         DP[0].resize((size_t)h_ * w_);
         check(sm_disp_optimize(ctx_, DP[0].data()), "dispOptimize");
+        if (Do_refine) {
+            DP[1].resize((size_t)h_ * w_);
+            check(sm_get_disp(ctx_, 1, DP[1].data()), "DP[1]");
+        }
     }
-    void refine() { throw std::logic_error("refine(): Do_refine = 0 in the reference (h:70); not built"); }
+    void refine() {  // cpp:1138-1511; needs Do_refine at construction
+        DP[0].resize((size_t)h_ * w_);
+        check(sm_refine(ctx_, DP[0].data()), "refine");
+    }
     std::vector<float> volume(int view = 0) {
         std::vector<float> v((size_t)h_ * w_ * d_);
         check(sm_get_volume(ctx_, view, v.data()), "vm");

@@ -35,6 +35,9 @@ class sm_params(C.Structure):
         ("sgm_cor_dif_thres", C.c_int32), ("sgm_redu_coeff", C.c_int32),
         ("compute_right_view", C.c_int32), ("keep_final_volume", C.c_int32),
         ("batch_capacity", C.c_int32),
+        ("do_refine", C.c_int32), ("lr_max_diff", C.c_float), ("do_region_vote", C.c_int32),
+        ("region_vote_nums", C.c_int32), ("rv_ratio", C.c_float), ("rv_s", C.c_int32),
+        ("do_proper_ipol", C.c_int32), ("disp_occ", C.c_int32), ("do_last_median_blur", C.c_int32),
     ]
 
 
@@ -51,6 +54,9 @@ SIGNATURES = [
     ("sm_cost_calculate", C.c_int, [_P]),
     ("sm_solve_all", C.c_int, [_P, C.c_int32, C.c_float]),
     ("sm_disp_optimize", C.c_int, [_P, _P]),
+    ("sm_refine", C.c_int, [_P, _P]),
+    ("sm_get_disp", C.c_int, [_P, C.c_int32, _P]),
+    ("sm_set_disp", C.c_int, [_P, C.c_int32, _P]),
     ("sm_get_volume", C.c_int, [_P, C.c_int32, _P]),
     ("sm_get_arms", C.c_int, [_P, C.c_int32, _P]),
     ("sm_upload_batch", C.c_int, [_P, C.c_int32, _P, _P, _P, _P]),

@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <new>
 #include <string>
@@ -49,12 +50,15 @@ struct sm_ctx {
     float* vm0 = nullptr;       // [cap][npix][D]
     float* vm1 = nullptr;       // [cap][npix][D] (right view, optional)
     float* acc = nullptr;       // [cap][npix][D]
-    int16_t* disp = nullptr;    // [cap][npix]
+    int16_t* disp = nullptr;    // [cap][npix] DP[0]
+    int16_t* disp1 = nullptr;   // [cap][npix] DP[1] (do_refine)
+    int16_t* disp_tmp = nullptr;// [cap][npix] refine ping-pong (do_refine)
     float* dummy = nullptr;     // 64 floats written by lanes past D
-    uint8_t* flags = nullptr;   // [cap][npix] SGM colour-difference penalty bits
+    uint8_t* flags = nullptr;   // [cap][npix] SGM colour-difference penalty bits, left image
+    uint8_t* flags1 = nullptr;  // [cap][npix] same for the right image (do_refine)
     uint32_t* px = nullptr;     // [cap][2][npix] packed BGR
     int n_loaded = 0;
-    int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized
+    int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized, 5 refined
     float lut_a[1024], lut_b[1024];
     float ad_oor_exp = 0;
     bool fuse_norm_scan = false;
@@ -134,7 +138,11 @@ sm_status timed(sm_ctx* c, const char* name, double bytes, F&& launch) {
 int census_len(const sm_params& p) { return (2 * p.census_rv + 1) * (2 * p.census_ru + 1) + (p.census_ring ? 8 : 0); }
 
 bool needs_census(const sm_params& p) { return p.cost_method != SM_COST_AD; }
-bool needs_arms(const sm_params& p) { return p.cost_method == SM_COST_CENSUS_GRAD || p.aggregation == SM_AGG_CBCA; }
+bool needs_arms(const sm_params& p) {
+    return p.cost_method == SM_COST_CENSUS_GRAD || p.aggregation == SM_AGG_CBCA || p.do_refine;  // + regionVote (cpp:1393-1396)
+}
+bool right_view(const sm_params& p) { return p.compute_right_view || p.do_refine; }
+int n_views(const sm_params& p) { return p.do_refine ? 2 : 1; }   // imgNum = Do_refine && Do_LRConsis ? 2 : 1
 
 int cbca_lag(const sm_params& p) { return p.arm_l_out > p.arm_min_l ? p.arm_l_out : p.arm_min_l; }
 
@@ -155,6 +163,10 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (p.sgm_redu_coeff == 0) return bad("sgm_redu_coeff must be non-zero");
     if (p.batch_capacity < 1) return bad("batch_capacity must be >= 1");
     if (p.lam_cen == 0 || p.lam_g == 0 || p.lam_ad == 0 || p.lam_cen_adc == 0) return bad("fusion lambdas must be non-zero");
+    if (p.do_refine) {
+        if (!(p.rv_ratio > 0)) return bad("rv_ratio must be > 0");
+        if (p.region_vote_nums < 0 || p.region_vote_nums > 64) return bad("region_vote_nums must be in [0, 64]");
+    }
     return SM_OK;
 }
 
@@ -189,7 +201,8 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 }
 
 void free_all(sm_ctx* c) {
-    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp, c->dummy, c->flags, c->px};
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
+                    c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px};
     for (void* q : ptrs)
         if (q) hipFree(q);
     for (auto& r : c->recs) {
@@ -216,7 +229,10 @@ struct Bufs {
     float* vm1;
     float* acc;
     int16_t* disp;
+    int16_t* disp1;
+    int16_t* disp_tmp;
     uint8_t* flags;
+    uint8_t* flags1;
     uint32_t* px;
 };
 
@@ -233,7 +249,10 @@ Bufs at(const sm_ctx* c, int off) {
     b.vm1 = c->vm1 ? c->vm1 + o * nv : nullptr;
     b.acc = c->acc ? c->acc + o * nv : nullptr;
     b.disp = c->disp + o * np;
+    b.disp1 = c->disp1 ? c->disp1 + o * np : nullptr;
+    b.disp_tmp = c->disp_tmp ? c->disp_tmp + o * np : nullptr;
     b.flags = c->flags + o * np;
+    b.flags1 = c->flags1 ? c->flags1 + o * np : nullptr;
     b.px = c->px + o * 2 * np;
     return b;
 }
@@ -253,6 +272,7 @@ sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
         a.gy = B.gy;
         a.arms = B.arms;
         a.flags = B.flags;
+        a.flags1 = flags && p.do_refine ? B.flags1 : nullptr;
         a.H = H;
         a.W = W;
         a.rv = p.census_rv;
@@ -269,7 +289,7 @@ sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
         a.do_arms = arms;
         a.do_flags = flags;
         return timed(c, "prep", (double)n * 2 * c->npix * (1 + 3 + (census ? 16 : 0) + (grad ? 8 : 0) + (arms ? 4 : 0)) +
-                                    (flags ? (double)n * c->npix : 0),
+                                    (flags ? (double)n * c->npix * n_views(p) : 0),
                      [&] { sm::launch_prep(a, n, c->st); });
     }
 }
@@ -304,7 +324,7 @@ sm_status run_cost(sm_ctx* c, int n, int view, const Bufs& B) {
                  [&] { sm::launch_cost(a, m, n, c->st); });
 }
 
-sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w, const Bufs& B) {
+sm_status run_cbca(sm_ctx* c, int n, int view, bool fuse_scale, float w, const Bufs& B) {
     // cbca_core (cpp:5585-5666): iteration k runs H then V for even k, V then H for odd k.
     // The last pass of iteration k and the first pass of iteration k+1 share a direction and
     // are fused into one CB_NORM_SCAN sweep, so N iterations take N + 1 sweeps.
@@ -312,34 +332,38 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w, const Bufs& B) {
     const int N = p.cbca_iterations;
     if (N <= 0) return SM_OK;
     sm::CbcaArgs a{};
-    a.vm = B.vm0;
+    a.vm = view == 0 ? B.vm0 : B.vm1;
+    a.view = view;
     a.dummy = c->dummy;
     a.arms = (const uint32_t*)B.arms;
     a.H = p.rows;
     a.W = p.cols;
     a.D = p.num_disparities;
     a.lag = cbca_lag(p);
-    a.vm_end = c->vm0 + (size_t)c->cap * c->nvol;
+    a.vm_end = (view == 0 ? c->vm0 : c->vm1) + (size_t)c->cap * c->nvol;
     a.arms_end = (const uint32_t*)(c->arms + c->arms_bytes);
     a.scale = w;
     a.apply_scale = 0;
     const double bytes = (double)n * c->nvol * 8.0;
-    sm_status s = timed(c, "cbca_h_scan", bytes, [&] { sm::launch_cbca(a, true, sm::CB_SCAN, n, c->st); });
+    // profile names: "cbca_h_scan" etc. for vm[0], "cbca_h_scan_r" etc. for vm[1]
+    std::string sfx = view == 0 ? "" : "_r";
+    auto nm = [&](const char* base) { static thread_local std::string t; t = std::string(base) + sfx; return t.c_str(); };
+    sm_status s = timed(c, nm("cbca_h_scan"), bytes, [&] { sm::launch_cbca(a, true, sm::CB_SCAN, n, c->st); });
     if (s) return s;
     for (int k = 0; k < N; k++) {
         const bool dir_h = (k % 2 == 1);  // direction of iteration k's second pass
         if (k + 1 < N && c->fuse_norm_scan) {
-            s = timed(c, dir_h ? "cbca_h_norm_scan" : "cbca_v_norm_scan", bytes,
+            s = timed(c, nm(dir_h ? "cbca_h_norm_scan" : "cbca_v_norm_scan"), bytes,
                       [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM_SCAN, n, c->st); });
         } else if (k + 1 < N) {
-            s = timed(c, dir_h ? "cbca_h_norm" : "cbca_v_norm", bytes,
+            s = timed(c, nm(dir_h ? "cbca_h_norm" : "cbca_v_norm"), bytes,
                       [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM, n, c->st); });
             if (s) return s;
-            s = timed(c, dir_h ? "cbca_h_scan" : "cbca_v_scan", bytes,
+            s = timed(c, nm(dir_h ? "cbca_h_scan" : "cbca_v_scan"), bytes,
                       [&] { sm::launch_cbca(a, dir_h, sm::CB_SCAN, n, c->st); });
         } else {
             a.apply_scale = fuse_scale ? 1 : 0;
-            s = timed(c, dir_h ? "cbca_h_norm" : "cbca_v_norm", bytes,
+            s = timed(c, nm(dir_h ? "cbca_h_norm" : "cbca_v_norm"), bytes,
                       [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM, n, c->st); });
         }
         if (s) return s;
@@ -347,25 +371,30 @@ sm_status run_cbca(sm_ctx* c, int n, bool fuse_scale, float w, const Bufs& B) {
     return SM_OK;
 }
 
-sm_status run_scale(sm_ctx* c, int n, float w, const Bufs& B) {
-    return timed(c, "solve_all_scale", (double)n * c->nvol * 8.0,
-                 [&] { sm::launch_scale(B.vm0, (size_t)n * c->nvol, w, c->st); });
+sm_status run_scale(sm_ctx* c, int n, int view, float w, const Bufs& B) {
+    return timed(c, view == 0 ? "solve_all_scale" : "solve_all_scale_r", (double)n * c->nvol * 8.0,
+                 [&] { sm::launch_scale(view == 0 ? B.vm0 : B.vm1, (size_t)n * c->nvol, w, c->st); });
 }
 
-sm_status run_optimize(sm_ctx* c, int n, const Bufs& B) {
+// dispOptimize (cpp:1046-1136) for one view: vm[0] with the left image's penalty flags
+// (leftFirst = true) -> DP[0]; vm[1] with the right image's (leftFirst = false) -> DP[1].
+sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
     const sm_params& p = c->p;
+    float* vm = view == 0 ? B.vm0 : B.vm1;
+    int16_t* disp = view == 0 ? B.disp : B.disp1;
+    const char* sfx = view == 0 ? "" : "_r";
     if (p.optimization == SM_OPT_SGM) {
         static const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};  // cpp:6207
         static const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};  // cpp:6208
         static const char* NAMES[8] = {"sgm_path0", "sgm_path1", "sgm_path2", "sgm_path3",
                                        "sgm_path4", "sgm_path5", "sgm_path6", "sgm_path7"};
         sm::SgmArgs a{};
-        a.flags = B.flags;
+        a.flags = view == 0 ? B.flags : B.flags1;
         a.dummy = c->dummy;
-        a.vm = B.vm0;
+        a.vm = vm;
         a.acc = B.acc;
         a.bgr = B.bgr;
-        a.disp = B.disp;
+        a.disp = disp;
         a.H = p.rows;
         a.W = p.cols;
         a.D = p.num_disparities;
@@ -382,15 +411,50 @@ sm_status run_optimize(sm_ctx* c, int n, const Bufs& B) {
             // algorithmic bytes per element: read C (+ read acc) (+ write acc | write final)
             double per = 4.0 + ((mode & sm::SGM_FIRST) ? 0 : 4.0) + ((mode & sm::SGM_LAST) ? (p.keep_final_volume ? 4.0 : 0) : 4.0);
             double bytes = (double)n * c->nvol * per + ((mode & sm::SGM_LAST) ? (double)n * c->npix * 2 : 0);
-            sm_status s = timed(c, (mode & sm::SGM_LAST) ? "sgm_last_wta" : NAMES[i], bytes,
-                                [&] { sm::launch_sgm_path(a, mode, n, c->st); });
+            const std::string name = std::string((mode & sm::SGM_LAST) ? "sgm_last_wta" : NAMES[i]) + sfx;
+            sm_status s = timed(c, name.c_str(), bytes, [&] { sm::launch_sgm_path(a, mode, n, c->st); });
             if (s) return s;
         }
     } else {
-        sm_status s = timed(c, "wta", (double)n * c->nvol * 4.0 + (double)n * c->npix * 2,
-                            [&] { sm::launch_wta(B.vm0, B.disp, n, p.rows, p.cols, p.num_disparities, c->st); });
+        const std::string name = std::string("wta") + sfx;
+        sm_status s = timed(c, name.c_str(), (double)n * c->nvol * 4.0 + (double)n * c->npix * 2,
+                            [&] { sm::launch_wta(vm, disp, n, p.rows, p.cols, p.num_disparities, c->st); });
         if (s) return s;
     }
+    return SM_OK;
+}
+
+// refine(), non-USE_RECONCV branch (cpp:1347-1510), on DP[0] of n pairs: LR check (in place),
+// region votes and proper interpolations (Jacobi, ping-pong with disp_tmp), 3x3 median.
+sm_status run_refine(sm_ctx* c, int n, const Bufs& B) {
+    const sm_params& p = c->p;
+    const int H = p.rows, W = p.cols;
+    const double map = (double)n * c->npix * 2;
+    sm_status s = timed(c, "refine_lr_check", 3 * map,
+                        [&] { sm::launch_lr_check(B.disp, B.disp1, n, H, W, p.lr_max_diff, c->st); });
+    if (s) return s;
+    int16_t* cur = B.disp;
+    int16_t* nxt = B.disp_tmp;
+    const uint32_t* arms = (const uint32_t*)B.arms;
+    if (p.do_region_vote)
+        for (int i = 0; i < p.region_vote_nums; i++) {
+            if ((s = timed(c, "refine_region_vote", 2 * map,
+                           [&] { sm::launch_region_vote(cur, nxt, arms, n, H, W, p.rv_s, p.rv_ratio, c->st); })))
+                return s;
+            std::swap(cur, nxt);
+        }
+    if (p.do_proper_ipol)
+        for (int i = 0; i < p.region_vote_nums; i++) {
+            if ((s = timed(c, "refine_proper_ipol", 2 * map,
+                           [&] { sm::launch_proper_ipol(cur, nxt, B.px, n, H, W, p.disp_occ, c->st); })))
+                return s;
+            std::swap(cur, nxt);
+        }
+    if (p.do_last_median_blur) {
+        if ((s = timed(c, "refine_median3", 2 * map, [&] { sm::launch_median3(cur, nxt, n, H, W, c->st); }))) return s;
+        std::swap(cur, nxt);
+    }
+    if (cur != B.disp) HIP_TRY(c, hipMemcpyAsync(B.disp, cur, (size_t)map, hipMemcpyDeviceToDevice, c->st));
     return SM_OK;
 }
 
@@ -461,6 +525,15 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->compute_right_view = 0;
     p->keep_final_volume = 0;
     p->batch_capacity = 1;
+    p->do_refine = 0;           // h:70
+    p->lr_max_diff = 0.0f;      // h:212
+    p->do_region_vote = 1;      // h:75
+    p->region_vote_nums = 2;    // h:306
+    p->rv_ratio = 0.4f;         // cpp:1400
+    p->rv_s = 20;               // cpp:1401
+    p->do_proper_ipol = 1;      // h:76
+    p->disp_occ = -2 * 16;      // h:216
+    p->do_last_median_blur = 1; // h:80
 }
 
 const char* sm_status_string(sm_status s) {
@@ -508,13 +581,18 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     // volumes carry a 4 KiB tail: vectorised SGM lanes past D read (never write) into it
     const size_t vpad = 1024;
     if ((s = dalloc(c, &c->vm0, cap * c->nvol + vpad))) return s;
-    if (p->compute_right_view)
+    if (right_view(*p))
         if ((s = dalloc(c, &c->vm1, cap * c->nvol + vpad))) return s;
     if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
         if ((s = dalloc(c, &c->acc, cap * c->nvol + vpad))) return s;
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
     if ((s = dalloc(c, &c->dummy, 64))) return s;
     if ((s = dalloc(c, &c->flags, cap * c->npix))) return s;
+    if (p->do_refine) {
+        if ((s = dalloc(c, &c->flags1, cap * c->npix))) return s;
+        if ((s = dalloc(c, &c->disp1, cap * c->npix))) return s;
+        if ((s = dalloc(c, &c->disp_tmp, cap * c->npix))) return s;
+    }
     if ((s = dalloc(c, &c->px, cap * 2 * c->npix))) return s;
     build_luts(c);
     {
@@ -556,8 +634,10 @@ sm_status sm_cost_calculate(sm_ctx* c) {
     const Bufs B = at(c, 0);
     if ((s = run_prep(c, n, B))) return s;
     if ((s = run_cost(c, n, 0, B))) return s;
-    if (c->p.compute_right_view && (s = run_cost(c, n, 1, B))) return s;
-    if (c->p.aggregation == SM_AGG_CBCA && (s = run_cbca(c, n, false, 1.0f, B))) return s;
+    if (right_view(c->p) && (s = run_cost(c, n, 1, B))) return s;
+    if (c->p.aggregation == SM_AGG_CBCA)
+        for (int v = 0; v < n_views(c->p); v++)
+            if ((s = run_cbca(c, n, v, false, 1.0f, B))) return s;
     c->stage = 2;
     return SM_OK;
 }
@@ -569,7 +649,8 @@ sm_status sm_solve_all(sm_ctx* c, int32_t py_lev, float reg_lambda) {
     if (py_lev != 1) return fail(c, SM_EINVAL, "only PY_LEV = 1 is supported (main_.cpp:131)");
     const float m = 1 + reg_lambda;
     const float w = (float)(1. / (double)m);  // Mat::inv of the 1x1 regMat (cpp:2164)
-    if ((s = run_scale(c, c->n_loaded, w, at(c, 0)))) return s;
+    for (int v = 0; v < n_views(c->p); v++)   // img_n = Do_refine ? 2 : 1 (cpp:2178)
+        if ((s = run_scale(c, c->n_loaded, v, w, at(c, 0)))) return s;
     c->stage = 3;
     return SM_OK;
 }
@@ -578,9 +659,46 @@ sm_status sm_disp_optimize(sm_ctx* c, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
     if (c->stage < 2 || c->stage > 3) return fail(c, SM_ESTATE, "sm_disp_optimize must follow sm_cost_calculate / sm_solve_all");
-    if ((s = run_optimize(c, c->n_loaded, at(c, 0)))) return s;
+    for (int v = 0; v < n_views(c->p); v++)   // num = Do_refine && Do_LRConsis ? 2 : 1 (cpp:1054, 1110)
+        if ((s = run_optimize(c, c->n_loaded, v, at(c, 0)))) return s;
     c->stage = 4;
     if (disp_out) return sm_download_disp(c, 1, disp_out);
+    return SM_OK;
+}
+
+sm_status sm_refine(sm_ctx* c, int16_t* disp_out) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!c->p.do_refine) return fail(c, SM_ESTATE, "sm_refine needs do_refine = 1 at sm_create (DP[1] is not computed otherwise)");
+    if (c->stage != 4) return fail(c, SM_ESTATE, "sm_refine must follow sm_disp_optimize");
+    if ((s = run_refine(c, c->n_loaded, at(c, 0)))) return s;
+    c->stage = 5;
+    if (disp_out) return sm_download_disp(c, 1, disp_out);
+    return SM_OK;
+}
+
+sm_status sm_get_disp(sm_ctx* c, int32_t view, int16_t* dst) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!dst || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
+    if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
+    const int16_t* src = view == 0 ? c->disp : c->disp1;
+    if (!src) return fail(c, SM_EINVAL, "DP[1] is only computed with do_refine = 1");
+    HIP_TRY(c, hipMemcpyAsync(dst, src, c->npix * 2, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    return SM_OK;
+}
+
+sm_status sm_set_disp(sm_ctx* c, int32_t view, const int16_t* src) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!src || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
+    if (c->stage < 4) return fail(c, SM_ESTATE, "sm_set_disp must follow sm_disp_optimize");
+    int16_t* dst = view == 0 ? c->disp : c->disp1;
+    if (!dst) return fail(c, SM_EINVAL, "DP[1] is only allocated with do_refine = 1");
+    HIP_TRY(c, hipMemcpyAsync(dst, src, c->npix * 2, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    c->stage = 4;   // refine() may run (again) on the new maps
     return SM_OK;
 }
 
@@ -591,8 +709,8 @@ sm_status sm_get_volume(sm_ctx* c, int32_t view, float* dst) {
     if (c->stage < 2) return fail(c, SM_ESTATE, "no volume yet");
     float* src = view == 0 ? c->vm0 : (view == 1 ? c->vm1 : nullptr);
     if (!src) return fail(c, SM_EINVAL, view == 1 ? "right view not computed (compute_right_view = 0)" : "bad view");
-    if (view == 0 && c->stage == 4 && !c->p.keep_final_volume && c->p.optimization == SM_OPT_SGM)
-        return fail(c, SM_ESTATE, "vm[0] after SGM is only kept with keep_final_volume = 1");
+    if (c->stage >= 4 && !c->p.keep_final_volume && c->p.optimization == SM_OPT_SGM)
+        return fail(c, SM_ESTATE, "vm[view] after SGM is only kept with keep_final_volume = 1");
     HIP_TRY(c, hipMemcpyAsync(dst, src, c->nvol * 4, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     return SM_OK;
@@ -649,15 +767,19 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
         const Bufs B = at(c, off);
         if ((s = run_prep(c, m2, B))) return s;
         if ((s = run_cost(c, m2, 0, B))) return s;
-        if (c->p.compute_right_view && (s = run_cost(c, m2, 1, B))) return s;
-        if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0) {
-            if ((s = run_cbca(c, m2, true, w, B))) return s;   // SolveAll fused into the last pass
-        } else {
-            if ((s = run_scale(c, m2, w, B))) return s;
+        if (right_view(c->p) && (s = run_cost(c, m2, 1, B))) return s;
+        for (int v = 0; v < n_views(c->p); v++) {
+            if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0) {
+                if ((s = run_cbca(c, m2, v, true, w, B))) return s;   // SolveAll fused into the last pass
+            } else {
+                if ((s = run_scale(c, m2, v, w, B))) return s;
+            }
         }
-        if ((s = run_optimize(c, m2, B))) return s;
+        for (int v = 0; v < n_views(c->p); v++)
+            if ((s = run_optimize(c, m2, v, B))) return s;
+        if (c->p.do_refine && (s = run_refine(c, m2, B))) return s;
     }
-    c->stage = 4;
+    c->stage = c->p.do_refine ? 5 : 4;
     if (disp_out) return sm_download_disp(c, n, disp_out);
     return SM_OK;
 }
@@ -666,7 +788,7 @@ sm_status sm_download_disp(sm_ctx* c, int32_t n, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
     if (!disp_out || n < 1 || n > c->cap) return fail(c, SM_EINVAL, "bad arguments");
-    if (c->stage != 4) return fail(c, SM_ESTATE, "no disparity map yet");
+    if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
     HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDefault, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     return SM_OK;

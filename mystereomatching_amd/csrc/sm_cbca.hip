@@ -46,6 +46,9 @@ __device__ __forceinline__ uint32_t pkmin(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t shr1_in(uint32_t v, uint32_t in) {  // lane l <- lane l-1, lane 0 <- in
     return (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
 }
+__device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane l <- lane l+1, lane 63 <- in
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)v, DPP_WAVE_SHL1, 0xF, 0xF, false);
+}
 
 // Positions per tile and tiles prefetched ahead: the sweeps are bound by memory latency at the
 // 5-6 waves per CU the LDS rings allow, so PF tiles of loads are kept in flight; the loads of PF
@@ -112,7 +115,10 @@ struct CbTile {
     uint32_t a1[HORIZ ? 1 : NSETS][T];   // V: right arm pair at (row j0 + k - off, u - d)
 };
 
-template <bool HORIZ, int MODE, bool FULL, bool SCALE>
+// RV: the right view's volume vm[1] (cbca_core's LOR = 1, run when Do_refine): the pixel's own
+// arms are the right image's, and lane d pairs them with the LEFT image's arms at u + d
+// (HVL_INTERSECTION[1], cpp:2794-2845) — zero once u + d >= W.
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV>
 struct CbLine {
     static constexpr int T = CbCfg<HORIZ, MODE>::T;
     static constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
@@ -182,7 +188,9 @@ struct CbLine {
             const int p0 = base + lane;
             t.a0[s] = buf_ld_u32(A0r[s], (lane < T && (unsigned)p0 < (unsigned)len) ? (uint32_t)(p0 * pstride) * 4u : 0x80000000u, 0);
             if (HORIZ) {
-                const int q = base + lane - c64;  // right pixel of lane 0 at position base + lane
+                // H window input at position base + lane: left view — the right pixel of lane 0
+                // (shifted in at lane 0); right view — the left pixel of lane 63 (shifted in there)
+                const int q = RV ? base + lane + c64 + 63 : base + lane - c64;
                 t.a1v[s] = buf_ld_u32(A1r[s], (lane < T && (unsigned)q < (unsigned)len) ? (uint32_t)q * 4u : 0x80000000u, 0);
             } else {
                 const __amdgpu_buffer_rsrc_t ra1 = bounded_rsrc(A1v[s] + (long)base * (long)(pstride * 4), aend);
@@ -196,7 +204,10 @@ struct CbLine {
     __device__ __forceinline__ void advance(const Tile& t, int k, int /*j*/) {
         if (HORIZ) {
 #pragma unroll
-            for (int s = 0; s < NSETS; s++) sh[s] = shr1_in(sh[s], (uint32_t)__builtin_amdgcn_readlane((int)t.a1v[s], k));
+            for (int s = 0; s < NSETS; s++) {
+                const uint32_t in = (uint32_t)__builtin_amdgcn_readlane((int)t.a1v[s], k);
+                sh[s] = RV ? shl1_in(sh[s], in) : shr1_in(sh[s], in);
+            }
         }
     }
 
@@ -329,10 +340,10 @@ struct CbLine {
     }
 };
 
-template <bool HORIZ, int MODE, bool FULL, bool SCALE>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV>
 __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     extern __shared__ float smem[];
-    CbLine<HORIZ, MODE, FULL, SCALE> L;
+    CbLine<HORIZ, MODE, FULL, SCALE, RV> L;
     constexpr int T = CbCfg<HORIZ, MODE>::T;
     constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
     L.lane = threadIdx.x;
@@ -358,23 +369,33 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.xend = (const char*)a.vm_end;
     L.aend = (const char*)a.arms_end;
     // arm planes: [b][view][plane][npix]; plane 0 = (L | R<<16), plane 1 = (U | D<<16)
+    // own = this view's image, other = the image it is matched against
     const int pass_plane = HORIZ ? 0 : 1, perp_plane = HORIZ ? 1 : 0;
+    const int own = RV ? 2 : 0, other = RV ? 0 : 2;
     const uint32_t* planeL = a.arms + ((size_t)b * 4) * npix + first_pix;
+    const int line_bytes = (((HORIZ ? a.W : a.H) - 1) * L.pstride + 1) * 4;
 #pragma unroll
     for (int s = 0; s < NSETS; s++) {
         const int pl = (s == 1) ? perp_plane : pass_plane;
-        const int line_bytes = (((HORIZ ? a.W : a.H) - 1) * L.pstride + 1) * 4;
-        L.A0r[s] = buf_rsrc(planeL + (size_t)pl * npix, line_bytes);
-        L.A1r[s] = buf_rsrc(planeL + (size_t)(2 + pl) * npix, line_bytes);
-        L.A1v[s] = (const char*)(a.arms + ((size_t)b * 4 + 2 + pl) * npix);
+        L.A0r[s] = buf_rsrc(planeL + (size_t)(own + pl) * npix, line_bytes);
+        L.A1r[s] = buf_rsrc(planeL + (size_t)(other + pl) * npix, line_bytes);
+        L.A1v[s] = (const char*)(a.arms + ((size_t)b * 4 + other + pl) * npix);
         L.sh[s] = 0u;
+        if (HORIZ && RV) {
+            // the window before the set's first position p0 = -off: lane l holds the left
+            // image's arm pair at p0 - 1 + c64 + l (0 outside the line)
+            const int q = -L.set_off(s) - 1 + chunk * 64 + L.lane;
+            L.sh[s] = buf_ld_u32(L.A1r[s], (unsigned)q < (unsigned)a.W ? (uint32_t)q * 4u : 0x80000000u, 0);
+        }
     }
     if (!HORIZ) {
-        const uint32_t col = (uint32_t)(L.line - min(dl, L.line)) * 4u;  // u - d, clamped (vmask zeroes)
+        // other image's column: u - d (left view) or u + d (right view), clamped; vmask zeroes
+        // the pairs outside the image
+        const uint32_t col = RV ? (uint32_t)min(L.line + dl, a.W - 1) * 4u : (uint32_t)(L.line - min(dl, L.line)) * 4u;
 #pragma unroll
         for (int k = 0; k < (HORIZ ? 1 : T); k++) L.ao[k] = col + (uint32_t)(k * a.W * 4);
     }
-    L.vmask = (!HORIZ && L.line - dl < 0) ? 0u : 0xffffffffu;
+    L.vmask = (!HORIZ && (RV ? L.line + dl >= a.W : L.line - dl < 0)) ? 0u : 0xffffffffu;
     L.c64 = chunk * 64;
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
@@ -392,7 +413,7 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.Acc = 0;
     L.ws = 0;
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    typename CbLine<HORIZ, MODE, FULL, SCALE>::Tile ta, tb, tc;
+    typename CbLine<HORIZ, MODE, FULL, SCALE, RV>::Tile ta, tb, tc;
     if constexpr (CbCfg<HORIZ, MODE>::PF == 2) {
         L.load(ta, 0);
         L.load(tb, T);
@@ -424,10 +445,14 @@ static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
     const int lines = HORIZ ? a.H : a.W;
     dim3 grid(lines * nchunks * n);
     const size_t shm = 4 * (size_t)cbca_smem_words(a.lag, HORIZ, MODE);
-    if (a.D % 64 == 0)
-        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE>), grid, dim3(64), shm, st, a);
-    else
-        hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE>), grid, dim3(64), shm, st, a);
+    const bool full = a.D % 64 == 0;
+    if (a.view == 0) {
+        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, false>), grid, dim3(64), shm, st, a);
+        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, false>), grid, dim3(64), shm, st, a);
+    } else {
+        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, true>), grid, dim3(64), shm, st, a);
+        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, true>), grid, dim3(64), shm, st, a);
+    }
 }
 
 template <bool HORIZ, int MODE>

@@ -19,7 +19,8 @@ struct PrepArgs {
     float* gx;
     float* gy;
     uint8_t* arms;              // [n][view][plane][H][W] u32: plane 0 = L | R<<16, plane 1 = U | D<<16
-    uint8_t* flags;             // [n][H][W] (left view only)
+    uint8_t* flags;             // [n][H][W] left image
+    uint8_t* flags1;            // [n][H][W] right image (nullptr: not needed)
     int H, W, rv, ru, ring;
     int L, L_out, C_D, C_D_out, minL, cor_thres;
     int do_census, do_grad, do_arms, do_flags;
@@ -52,6 +53,7 @@ struct CbcaArgs {
     int lag;                    // max arm length (the ring size is derived in sm_cbca.hip)
     int apply_scale;
     float scale;                // SolveAll weight (fused into the last normalising pass)
+    int view;                   // 0: vm[0] (left reference), 1: vm[1] (right reference, Do_refine)
 };
 
 struct SgmArgs {
@@ -78,6 +80,13 @@ void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipS
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);
 void launch_div_check(int exp2, int bmax, unsigned long long* bad, hipStream_t st);
 float expf_host(float x);
+// refinement (sm_refine.hip)
+void launch_lr_check(int16_t* d0, const int16_t* d1, int n, int H, int W, float maxdiff, hipStream_t st);
+void launch_region_vote(const int16_t* src, int16_t* dst, const uint32_t* arms, int n, int H, int W, int rv_s,
+                        float rv_ratio, hipStream_t st);
+void launch_proper_ipol(const int16_t* src, int16_t* dst, const uint32_t* px, int n, int H, int W, int disp_occ,
+                        hipStream_t st);
+void launch_median3(const int16_t* src, int16_t* dst, int n, int H, int W, hipStream_t st);
 int sgm_k_for(int D);
 
 }  // namespace sm

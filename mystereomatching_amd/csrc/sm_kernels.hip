@@ -176,8 +176,9 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
             planes[0] = (packed & 0xffu) | ((packed >> 8 & 0xffu) << 16);
             planes[npix] = (packed >> 16 & 0xffu) | ((packed >> 24) << 16);
         }
-        // SGM penalty flags of the left image (updateCost, h:2223-2229)
-        if (a.do_flags && view == 0) {
+        // SGM penalty flags of the left image (updateCost, h:2223-2229), and of the right image
+        // when vm[1] is optimised too (leftFirst = false compares I_c[1], h:2224)
+        if (a.do_flags && (view == 0 || a.flags1)) {
             const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};
             const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};
             const uint32_t c0 = pc[0];
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
                 if (vv < 0 || vv >= H || uu < 0 || uu >= W) continue;
                 if (color_d1(c0, pc[RV[i] * W + RU[i]]) > a.cor_thres) f |= 1u << i;
             }
-            a.flags[(size_t)b * npix + (size_t)v * W + u] = (uint8_t)f;
+            (view == 0 ? a.flags : a.flags1)[(size_t)b * npix + (size_t)v * W + u] = (uint8_t)f;
         }
     }
 }

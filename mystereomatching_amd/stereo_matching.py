@@ -8,6 +8,7 @@ Same names, argument meaning and call order as ``main_.cpp`` uses them (main_.cp
     sm.costCalculate()                                  # cost + CBCA (cpp:945-1021)
     SolveAll([sm], 1, 0.3)                              # cpp:2142-2208
     sm.dispOptimize()                                   # SGM + WTA (cpp:1046-1136)
+    if StereoMatching.Do_refine: sm.refine()            # cpp:1138-1511 (main:165-166)
     disparity = sm.DP[0]                                # int16 H x W, -1 = invalid
 
 All compute runs in libsm_hip.so on the GPU (no CPU fallback).  Errors are raised as
@@ -31,9 +32,13 @@ class StereoMatching:
     optimization: str = "sgm"
     object: str = ""
 
-    # compile-time switches the hot path reads (h:57-83)
+    # compile-time switches the hot path reads (h:57-83); like the reference's static consts they
+    # are read when an object is constructed (set StereoMatching.Do_refine = True before it)
     Do_refine = False
     Do_LRConsis = True
+    Do_regionVote = True
+    Do_properIpol = True
+    Do_lastMedianBlur = True
 
     class Parameters:
         """StereoMatching::Parameters (h:85-351): the fields the hot path reads."""
@@ -64,11 +69,16 @@ class StereoMatching:
             self.vmTop_Num = M
             self.vmTop_thres = lamc * 0.01
             self.rows, self.cols = h, w
+            self.LRmaxDiff = 0.0                       # h:212
+            self.DISP_OCC = -2 * 16                    # h:216
+            self.region_vote_nums = 2                  # h:306
+            self.rv_ratio, self.rv_s = 0.4, 20         # refine(): rv_ratio[] / rv_s[] (cpp:1400-1401)
             if disSc != 1:
                 raise ValueError("pyramid levels > 0 (disSc > 1) are not supported; PY_LEV = 1")
 
         def to_c(self, cost: str, aggregation: str, optimization: str, batch: int = 1,
-                 compute_right_view: bool = False, keep_final_volume: bool = False) -> _capi.sm_params:
+                 compute_right_view: bool = False, keep_final_volume: bool = False,
+                 do_refine: bool = False, switches=(True, True, True)) -> _capi.sm_params:
             if self.censusFunc not in (0, 3):
                 raise ValueError("censusFunc must be 0 (plain census) or 3 (census + ring bits)")
             p = _capi.default_params(self.numDisparities - 1, self.rows, self.cols)
@@ -88,6 +98,12 @@ class StereoMatching:
             p.batch_capacity = batch
             p.compute_right_view = int(compute_right_view)
             p.keep_final_volume = int(keep_final_volume)
+            p.do_refine = int(do_refine)
+            p.lr_max_diff = float(self.LRmaxDiff)
+            p.disp_occ = int(self.DISP_OCC)
+            p.region_vote_nums = int(self.region_vote_nums)
+            p.rv_ratio, p.rv_s = float(self.rv_ratio), int(self.rv_s)
+            p.do_region_vote, p.do_proper_ipol, p.do_last_median_blur = (int(x) for x in switches)
             return p
 
     def __init__(self, I1_c, I2_c, I1_g, I2_g, DT=None, all_mask=None, nonocc_mask=None, disc_mask=None,
@@ -110,9 +126,13 @@ class StereoMatching:
         self.I_c, self.I_g = [I1_c, I2_c], [I1_g, I2_g]
         self.DP: List[Optional[np.ndarray]] = [None, None]
         self._lib = _capi.load()
+        if self.Do_refine and not self.Do_LRConsis:
+            raise ValueError("Do_refine needs Do_LRConsis (refine() starts with the LR check, cpp:1364)")
         p = param.to_c(self.costcalculation, self.aggregation, self.optimization,
                        compute_right_view=self.Do_LRConsis and self.Do_refine,
-                       keep_final_volume=keep_final_volume)
+                       keep_final_volume=keep_final_volume, do_refine=self.Do_refine,
+                       switches=(self.Do_regionVote, self.Do_properIpol, self.Do_lastMedianBlur))
+        self._refine_on = bool(self.Do_refine)
         p.rows, p.cols = h, w
         ctx = C.c_void_p()
         st = self._lib.sm_create(C.byref(ctx), C.byref(p), device)
@@ -134,15 +154,23 @@ class StereoMatching:
         _capi.check(self._lib, self._ctx, self._lib.sm_cost_calculate(self._ctx), "costCalculate")
 
     def dispOptimize(self):
-        """SGM (or WTA only) -> DP[0] (cpp:1046-1136)."""
+        """SGM (or WTA only) -> DP[0], and DP[1] when Do_refine (cpp:1046-1136)."""
         dp = np.empty((self.h_, self.w_), np.int16)
         _capi.check(self._lib, self._ctx, self._lib.sm_disp_optimize(self._ctx, _capi.ptr(dp)), "dispOptimize")
         self.DP[0] = dp
+        if self._refine_on:
+            d1 = np.empty((self.h_, self.w_), np.int16)
+            _capi.check(self._lib, self._ctx, self._lib.sm_get_disp(self._ctx, 1, _capi.ptr(d1)), "DP[1]")
+            self.DP[1] = d1
         return dp
 
     def refine(self):
-        raise NotImplementedError("refine() is off in the reference default (Do_refine = 0, h:70); "
-                                  "it is the next row of SURVEY.md §8f")
+        """refine() (cpp:1138-1511): LR check against DP[1], region votes, proper interpolation,
+        3x3 median -> DP[0].  Needs Do_refine = True when the object was constructed."""
+        dp = np.empty((self.h_, self.w_), np.int16)
+        _capi.check(self._lib, self._ctx, self._lib.sm_refine(self._ctx, _capi.ptr(dp)), "refine")
+        self.DP[0] = dp
+        return dp
 
     def pipeline(self):
         """pipeline() (cpp:1950-1981): costCalculate -> dispOptimize (no SolveAll)."""

@@ -36,7 +36,8 @@ def test_params_struct_layout_and_defaults():
     # every field of struct sm_params is 4 bytes; the header's field count must match ctypes
     txt = open(os.path.join(ROOT, "include", "sm_capi.h")).read()
     body = txt[txt.index("typedef struct sm_params {"):txt.index("} sm_params;")]
-    nfields = sum(len(re.findall(r"\b\w+\s*(?:,|;)", ln.split("/*")[0])) for ln in body.splitlines()[1:])
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    nfields = sum(len(re.findall(r"\b\w+\s*(?:,|;)", ln)) for ln in body.splitlines()[1:])
     assert C.sizeof(_capi.sm_params) == 4 * nfields
     p = _capi.default_params(59, 375, 450)
     assert p.num_disparities == 60
@@ -44,6 +45,10 @@ def test_params_struct_layout_and_defaults():
     assert (p.arm_l, p.arm_l_out, p.arm_c_thresh, p.arm_c_thresh_out, p.arm_min_l) == (17, 34, 20, 6, 1)
     assert (p.cbca_iterations, p.sgm_paths, p.sgm_cor_dif_thres, p.sgm_redu_coeff) == (2, 4, 15, 4)
     assert (p.lam_cen, p.lam_g, p.grad_trunc, p.sgm_p1, p.sgm_p2) == (13.0, 1.0, 500.0, 1.0, 3.0)
+    # refine() switches and constants (h:70-80, 212, 216, 306; cpp:1400-1401)
+    assert (p.do_refine, p.lr_max_diff, p.do_region_vote, p.region_vote_nums, p.rv_s) == (0, 0.0, 1, 2, 20)
+    assert (p.do_proper_ipol, p.disp_occ, p.do_last_median_blur) == (1, -32, 1)
+    assert np.float32(p.rv_ratio) == np.float32(0.4)
 
 
 @pytest.mark.parametrize("field,value,msg", [
@@ -90,3 +95,17 @@ def test_host_expf_matches_libm_sample(oracle):
     got2 = np.array([lib.sm_expf_host(float(x)) for x in xs2], np.float32)
     ref2 = np.concatenate([oracle.expf_range(int(b), 1) for b in xs2.view(np.uint32)])
     assert np.array_equal(got2.view(np.uint32), ref2.view(np.uint32))
+
+
+@pytest.mark.parametrize("field,value,msg", [("rv_ratio", 0.0, b"rv_ratio"), ("region_vote_nums", -1, b"region_vote_nums")])
+def test_refine_validation(field, value, msg):
+    lib = _capi.load()
+    p = _capi.default_params(63, 32, 32, do_refine=1)
+    setattr(p, field, value)
+    ctx = C.c_void_p()
+    st = lib.sm_create(C.byref(ctx), C.byref(p), 0)
+    try:
+        assert st == _capi.SM_EINVAL
+        assert msg in lib.sm_last_error(ctx)
+    finally:
+        lib.sm_destroy(ctx)

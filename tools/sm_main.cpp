@@ -25,7 +25,7 @@ static bool read_ppm(const char* path, int& w, int& h, std::vector<uint8_t>& rgb
 
 int main(int argc, char** argv) {
     if (argc < 5) {
-        std::fprintf(stderr, "usage: %s left.ppm right.ppm max_disp out.pgm [device]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s left.ppm right.ppm max_disp out.pgm [device] [refine]\n", argv[0]);
         return 2;
     }
     int w, h, w2, h2;
@@ -36,6 +36,7 @@ int main(int argc, char** argv) {
     }
     const int maxDisp = std::atoi(argv[3]);
     const int dev = argc > 5 ? std::atoi(argv[5]) : 0;
+    smamd::StereoMatching::Do_refine = argc > 6 && std::atoi(argv[6]) != 0;
     std::vector<uint8_t> lb(l.size()), rb(r.size()), lg((size_t)w * h), rg((size_t)w * h);
     for (size_t i = 0; i < (size_t)w * h; i++) {
         for (int c = 0; c < 3; c++) {
@@ -57,6 +58,7 @@ int main(int argc, char** argv) {
         sm->costCalculate();
         smamd::SolveAll(&sm, 1, 0.3f);
         sm->dispOptimize();
+        if (smamd::StereoMatching::Do_refine) sm->refine();  // main_.cpp:165-166
         auto t1 = std::chrono::steady_clock::now();
         std::printf("all Time: %.3f ms\n", std::chrono::duration<double, std::milli>(t1 - t0).count());
         std::ofstream o(argv[4], std::ios::binary);

@@ -381,12 +381,6 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
         L.A1r[s] = buf_rsrc(planeL + (size_t)(other + pl) * npix, line_bytes);
         L.A1v[s] = (const char*)(a.arms + ((size_t)b * 4 + other + pl) * npix);
         L.sh[s] = 0u;
-        if (HORIZ && RV) {
-            // the window before the set's first position p0 = -off: lane l holds the left
-            // image's arm pair at p0 - 1 + c64 + l (0 outside the line)
-            const int q = -L.set_off(s) - 1 + chunk * 64 + L.lane;
-            L.sh[s] = buf_ld_u32(L.A1r[s], (unsigned)q < (unsigned)a.W ? (uint32_t)q * 4u : 0x80000000u, 0);
-        }
     }
     if (!HORIZ) {
         // other image's column: u - d (left view) or u + d (right view), clamped; vmask zeroes
@@ -400,6 +394,15 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
     L.ring = cbca_ring(a.lag, HORIZ, MODE);
+    if (HORIZ && RV) {
+        // right view: the window before each set's first position p0 = -off holds, in lane l, the
+        // left image's arm pair at p0 - 1 + c64 + l (0 outside the line)
+#pragma unroll
+        for (int s = 0; s < NSETS; s++) {
+            const int q = -L.set_off(s) - 1 + chunk * 64 + L.lane;
+            L.sh[s] = buf_ld_u32(L.A1r[s], (unsigned)q < (unsigned)a.W ? (uint32_t)q * 4u : 0x80000000u, 0);
+        }
+    }
     L.r1 = smem;
     L.r2 = smem + (size_t)L.ring * 64;
     L.ra = (uint16_t*)(smem + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));

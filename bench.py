@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
+    ap.add_argument("--refine", action="store_true",
+                    help="Do_refine = 1 (h:70): both views through CBCA/SolveAll/SGM/WTA, then refine() "
+                         "(LR check, 2x region vote, 2x proper interpolation, 3x3 median)")
     return ap.parse_args()
 
 
@@ -77,7 +80,9 @@ def main():
     D = md + 1
     # this rank's shard of the global batch: pair indices [rank*B, rank*B + B)
     batch = S.make_batch(B, H, W, D, first_index=rank * B)
-    sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths)
+    sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine))
+    if args.refine:
+        desc = desc + " + Do_refine (right view CBCA/SGM, LR check, region vote, proper ipol, median)"
     sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
 
     def barrier():
@@ -130,7 +135,7 @@ def main():
                               "GB_s": round(gbs, 1), "bytes_per_launch": k["bytes_per_launch"]}
         dom = max(kern_out, key=lambda n: kernels[n]["total_ms"])
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_b{B}.json")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}{'_refine' if args.refine else ''}_b{B}.json")
         if os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
@@ -144,12 +149,12 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
-        cfg = O.config(H, W, md, sgm_paths=paths)
+        cfg = O.config(H, W, md, sgm_paths=paths, do_refine=int(args.refine))
         n, t_cpu = 0, 0.0
         while n == 0 or (t_cpu < args.cpu_seconds and n < B):
             pair = {k: batch[k][n] for k in ("lbgr", "rbgr", "lgray", "rgray")}
             t = time.perf_counter()
-            r = O.run(pair, cfg)
+            r = O.run_ex(pair, cfg)
             t_cpu += time.perf_counter() - t
             if not np.array_equal(r["disp"], disp[n]):
                 raise SystemExit(f"bench: GPU disparity of pair {n} differs from the CPU restatement")
@@ -165,7 +170,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded piecewise-planar pairs, mystereomatching_amd/synthetic.py)",
             "config": {"workload": desc, "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": B * world,
-                       "sgm_paths": paths, "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
+                       "sgm_paths": paths, "refine": bool(args.refine),
+                       "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
             "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kern_out,
         }

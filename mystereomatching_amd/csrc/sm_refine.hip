@@ -104,54 +104,87 @@ __global__ __launch_bounds__(256) void k_region_vote(const int16_t* __restrict__
 // properIpol (cpp:7395-7490).  A hole searches 16 directions, up to 20 steps each, for the first
 // valid disparity; steps alternate pw / 2 and pw - pw / 2 (C truncating division).  DISP_OCC
 // holes take the smallest disparity found; other holes the disparity whose pixel's colour is
-// closest (max channel |diff| of I_c[0]), first strict minimum below 255.
+// closest (max channel |diff| of I_c[0]), first strict minimum below 255 in direction order.
+//
+// Holes are sparse and scattered, so a block first compacts the holes of its 64 x 4 tile into an
+// LDS list; then 16 lanes serve one hole, lane k walking direction k (positions move
+// monotonically, so leaving the image ends the walk exactly like the reference's break), 5
+// speculative loads per round to hide the L2 latency of the dependent walk; the group's result
+// is a 16-lane min of (colour difference, direction) or of the disparity.
+constexpr int PI_DEPTH = 20, PI_CHUNK = 5;
 __global__ __launch_bounds__(256) void k_proper_ipol(const int16_t* __restrict__ src, int16_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ px, int H, int W, int disp_occ) {
+    __shared__ uint32_t holes[TX * TY];
+    __shared__ int nholes;
     const Pix p = pixel_of(H, W);
-    if (!p.ok) return;
     const size_t npix = (size_t)H * W;
     const int16_t* dp = src + (size_t)p.b * npix;
+    if (threadIdx.x == 0) nholes = 0;
+    __syncthreads();
+    if (p.ok) {
+        const size_t o = (size_t)p.v * W + p.u;
+        const int cur = dp[o];
+        if (cur >= 0)
+            dst[(size_t)p.b * npix + o] = (int16_t)cur;
+        else
+            holes[atomicAdd(&nholes, 1)] = (uint32_t)threadIdx.x;
+    }
+    __syncthreads();
+    const int n = nholes;
     const uint32_t* col = px + (size_t)p.b * 2 * npix;  // left view's packed BGR
-    const size_t o = (size_t)p.v * W + p.u;
-    const int cur = dp[o];
-    int out = cur;
-    if (cur < 0) {
-        const int DW[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -2, -1};
-        const int DH[16] = {2, 2, 0, -2, -2, -2, 0, 2, 2, 1, -1, -2, -2, -1, 1, 2};
-        const uint32_t c0 = col[o];
-        const bool occ = cur == disp_occ;
-        int minDisp = 0x7fffffff, minDif = 255, best = -1;
+    const int k = threadIdx.x & 15;
+    const int DW[16] = {0, 2, 2, 2, 0, -2, -2, -2, 1, 2, 2, 1, -1, -2, -2, -1};
+    const int DH[16] = {2, 2, 0, -2, -2, -2, 0, 2, 2, 1, -1, -2, -2, -1, 1, 2};
+    const int pw = DW[k], ph = DH[k];
+    const int sw0 = pw / 2, sh0 = ph / 2, sw1 = pw - pw / 2, sh1 = ph - ph / 2;
+    // tile origin of this block (pixel_of maps threadIdx -> (u, v) inside it)
+    const int u_org = p.u - (int)(threadIdx.x & (TX - 1)), v_org = p.v - (int)(threadIdx.x / TX);
+    for (int base = 0; base < n; base += 16) {   // uniform trip count: every lane joins the shuffles
+        const int hi = base + (int)(threadIdx.x >> 4);
+        const bool act = hi < n;
+        const uint32_t t = act ? holes[hi] : 0u;
+        const int u = u_org + (int)(t & (TX - 1)), v = v_org + (int)(t / TX);
+        const int cur = act ? (int)dp[(size_t)v * W + u] : 0;
+        int found = -1, fu = 0, fv = 0;
+        for (int t0 = 0; act && t0 < PI_DEPTH && found < 0; t0 += PI_CHUNK) {
+            int q[PI_CHUNK], qu[PI_CHUNK], qv[PI_CHUNK];
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int pw = DW[k], ph = DH[k];
-            const int sw0 = pw / 2, sh0 = ph / 2, sw1 = pw - pw / 2, sh1 = ph - ph / 2;
-            int pu = p.u, pv = p.v;
-            for (int dep = 0; dep < 20; dep++) {
-                pu += (dep & 1) ? sw1 : sw0;
-                pv += (dep & 1) ? sh1 : sh0;
-                if (pu < 0 || pu >= W || pv < 0 || pv >= H) break;
-                const size_t q = (size_t)pv * W + pu;
-                const int dq = dp[q];
-                if (dq >= 0) {
-                    if (occ) {
-                        minDisp = min(minDisp, dq);
-                    } else {
-                        const int cd = colour_dif(c0, col[q]);
-                        if (minDif > cd) {  // directions in order: first strict minimum
-                            minDif = cd;
-                            best = dq;
-                        }
-                    }
-                    break;
+            for (int j = 0; j < PI_CHUNK; j++) {
+                const int st = t0 + j;
+                const int n0 = (st + 2) >> 1, n1 = (st + 1) >> 1;   // even / odd steps taken
+                qu[j] = u + n0 * sw0 + n1 * sw1;
+                qv[j] = v + n0 * sh0 + n1 * sh1;
+                const bool in = qu[j] >= 0 && qu[j] < W && qv[j] >= 0 && qv[j] < H;
+                q[j] = in ? (int)dp[(size_t)qv[j] * W + qu[j]] : -2;   // -2: outside (ends the walk)
+            }
+#pragma unroll
+            for (int j = PI_CHUNK - 1; j >= 0; j--)   // first valid step of the chunk before any exit
+                if (q[j] >= 0) {
+                    found = q[j];
+                    fu = qu[j];
+                    fv = qv[j];
                 }
+            // positions are monotone: after the first outside step every later one is outside, so
+            // a valid step of the chunk always precedes the exit
+            if (q[PI_CHUNK - 1] == -2) break;
+        }
+        const bool occ = cur == disp_occ;
+        // keys: occ -> the disparity; else (colour diff < 255) -> diff * 16 + direction
+        uint32_t key = 0xffffffffu;
+        if (found >= 0) {
+            if (occ) {
+                key = (uint32_t)found;
+            } else {
+                const int cd = colour_dif(col[(size_t)v * W + u], col[(size_t)fv * W + fu]);
+                if (cd < 255) key = (uint32_t)(cd * 16 + k);
             }
         }
-        if (occ)
-            out = minDisp != 0x7fffffff ? minDisp : cur;
-        else
-            out = best >= 0 ? best : cur;
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) key = min(key, (uint32_t)__shfl_xor((int)key, m, 16));
+        const int fsel = __shfl(found, (int)(key & 15), 16);   // all lanes take part
+        const int res = key == 0xffffffffu ? cur : (occ ? (int)key : fsel);
+        if (act && k == 0) dst[(size_t)p.b * npix + (size_t)v * W + u] = (int16_t)res;
     }
-    dst[(size_t)p.b * npix + o] = (int16_t)out;
 }
 
 __device__ __forceinline__ void cswap(int& a, int& b) {

@@ -62,7 +62,10 @@ struct sm_ctx {
     float lut_a[1024], lut_b[1024];
     float ad_oor_exp = 0;
     bool fuse_norm_scan = false;
-    int sub_batch = 0;             // SM_SUB_BATCH=k: run sm_run in groups of k pairs (0 = all)   // SM_FUSE_NORM_SCAN=1: one sweep for norm(k) + scan(k+1)
+    int sub_batch = 0;          // SM_SUB_BATCH=k: run sm_run in groups of k pairs (0 = all)
+    int nstreams = 1;           // SM_STREAMS=s: groups alternate over s streams (staggered, see sm_run)
+    hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
+    std::vector<hipEvent_t> xev;                        // stagger / join events
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
@@ -210,6 +213,13 @@ void free_all(sm_ctx* c) {
         if (r.stop) hipEventDestroy(r.stop);
     }
     for (auto e : c->free_events) hipEventDestroy(e);
+    for (auto e : c->xev) hipEventDestroy(e);
+    c->xev.clear();
+    for (auto& x : c->xst)
+        if (x) {
+            hipStreamDestroy(x);
+            x = nullptr;
+        }
     c->recs.clear();
     c->free_events.clear();
     if (c->st) hipStreamDestroy(c->st);
@@ -600,6 +610,16 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         c->fuse_norm_scan = e && e[0] == '1';
         const char* sb = getenv("SM_SUB_BATCH");
         c->sub_batch = sb ? atoi(sb) : 0;
+        const char* ns = getenv("SM_STREAMS");
+        c->nstreams = ns ? atoi(ns) : 1;
+        if (c->nstreams < 1) c->nstreams = 1;
+        if (c->nstreams > 4) c->nstreams = 4;
+        for (int i = 0; i + 1 < c->nstreams; i++) HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking));
+        for (int i = 0; i < 16; i++) {
+            hipEvent_t e;
+            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->xev.push_back(e);
+        }
     }
     HIP_TRY(c, sm::upload_luts(c->lut_a, c->lut_b, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
@@ -760,25 +780,47 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     const float m = 1 + reg_lambda;
     const float w = (float)(1. / (double)m);
     // Sub-batches: all stages of a group of pairs run back to back so that one pass's output is
-    // still in the 256 MB Infinity Cache when the next pass reads it.
+    // still in the 256 MB Infinity Cache when the next pass reads it.  With SM_STREAMS = s > 1 the
+    // groups alternate over s streams and group k + 1 starts once group k has finished its CBCA,
+    // so the LDS-bound aggregation sweeps of one group share the CUs with the SGM paths of the
+    // previous one; the main stream joins every stream at the end.
     const int g = c->sub_batch > 0 ? c->sub_batch : n;
-    for (int off = 0; off < n; off += g) {
+    const int ns = c->nstreams;
+    hipStream_t main_st = c->st;
+    int k = 0;
+    sm_status s_out = SM_OK;
+    if (ns > 1) {   // the side streams start after everything queued so far on the main stream
+        HIP_TRY(c, hipEventRecord(c->xev[0], main_st));
+        for (int i = 0; i + 1 < ns; i++) HIP_TRY(c, hipStreamWaitEvent(c->xst[i], c->xev[0], 0));
+    }
+    for (int off = 0; off < n; off += g, k++) {
         const int m2 = n - off < g ? n - off : g;
         const Bufs B = at(c, off);
-        if ((s = run_prep(c, m2, B))) return s;
-        if ((s = run_cost(c, m2, 0, B))) return s;
-        if (right_view(c->p) && (s = run_cost(c, m2, 1, B))) return s;
-        for (int v = 0; v < n_views(c->p); v++) {
-            if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0) {
-                if ((s = run_cbca(c, m2, v, true, w, B))) return s;   // SolveAll fused into the last pass
-            } else {
-                if ((s = run_scale(c, m2, v, w, B))) return s;
-            }
+        c->st = (ns > 1 && k % ns) ? c->xst[k % ns - 1] : main_st;
+        if (ns > 1 && k > 0) hipStreamWaitEvent(c->st, c->xev[1 + (k - 1) % 8], 0);
+        if ((s_out = run_prep(c, m2, B))) break;
+        if ((s_out = run_cost(c, m2, 0, B))) break;
+        if (right_view(c->p) && (s_out = run_cost(c, m2, 1, B))) break;
+        for (int v = 0; v < n_views(c->p) && !s_out; v++) {
+            if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0)
+                s_out = run_cbca(c, m2, v, true, w, B);   // SolveAll fused into the last pass
+            else
+                s_out = run_scale(c, m2, v, w, B);
         }
-        for (int v = 0; v < n_views(c->p); v++)
-            if ((s = run_optimize(c, m2, v, B))) return s;
-        if (c->p.do_refine && (s = run_refine(c, m2, B))) return s;
+        if (s_out) break;
+        if (ns > 1) hipEventRecord(c->xev[1 + k % 8], c->st);
+        for (int v = 0; v < n_views(c->p) && !s_out; v++) s_out = run_optimize(c, m2, v, B);
+        if (s_out) break;
+        if (c->p.do_refine && (s_out = run_refine(c, m2, B))) break;
     }
+    c->st = main_st;
+    if (ns > 1) {
+        for (int i = 0; i + 1 < ns; i++) {
+            hipEventRecord(c->xev[9 + i], c->xst[i]);
+            hipStreamWaitEvent(main_st, c->xev[9 + i], 0);
+        }
+    }
+    if (s_out) return s_out;
     c->stage = c->p.do_refine ? 5 : 4;
     if (disp_out) return sm_download_disp(c, n, disp_out);
     return SM_OK;

@@ -12,6 +12,8 @@
  *   sm_set_images      <- ctor image arguments I1_c,I2_c,I1_g,I2_g   stereoMatching.cpp:2063-2071
  *   sm_cost_calculate  <- StereoMatching::costCalculate              stereoMatching.cpp:945-1021
  *   sm_solve_all       <- SolveAll(StereoMatching**&, PY_LVL, REG_LAMBDA)  stereoMatching.cpp:2142-2208
+ *   sm_solve_all_pyr   <- the same with PY_LVL > 1 (one ctx per level)     stereoMatching.cpp:2142-2208
+ *   sm_pyr_down        <- cv::pyrDown on the inputs                     main_.cpp:145-148
  *   sm_disp_optimize   <- StereoMatching::dispOptimize + DP[0]       stereoMatching.cpp:1046-1136, h:2724
  *   sm_refine          <- StereoMatching::refine (Do_refine)         stereoMatching.cpp:1138-1511, main_.cpp:165-166
  *   sm_get_disp / sm_set_disp <- public member DP[view]              stereoMatching.h:2724
@@ -119,6 +121,15 @@ SM_API sm_status sm_set_images(sm_ctx* ctx, const uint8_t* lbgr, const uint8_t* 
 SM_API sm_status sm_cost_calculate(sm_ctx* ctx);
 SM_API sm_status sm_solve_all(sm_ctx* ctx, int32_t py_lev, float reg_lambda);
 SM_API sm_status sm_disp_optimize(sm_ctx* ctx, int16_t* disp_out);
+/* SolveAll(smPyr, PY_LVL, REG_LAMBDA) over PY_LVL in [1, 3] contexts, one per pyramid level
+ * (main_.cpp:131-158): level s has rows (rows_{s-1} + 1) / 2, cols likewise, num_disparities
+ * >= num_disparities_{s-1} / 2 + 1, the same pair count and device, and sm_cost_calculate done.
+ * levels[0]'s volume(s) receive the cross-scale sum; the coarser levels are only read. */
+SM_API sm_status sm_solve_all_pyr(sm_ctx* const* levels, int32_t py_lvl, float reg_lambda);
+/* cv::pyrDown (u8, 1 or 3 channels, BORDER_REFLECT_101) on `hip_device`; src rows x cols, dst
+ * ((rows + 1) / 2) x ((cols + 1) / 2); host or device pointers, synchronous.  (main_.cpp:145-148) */
+SM_API sm_status sm_pyr_down(int32_t hip_device, const uint8_t* src, int32_t rows, int32_t cols, int32_t channels,
+                             uint8_t* dst);
 /* refine() on DP[0] (needs do_refine = 1 at sm_create and a preceding sm_disp_optimize). */
 SM_API sm_status sm_refine(sm_ctx* ctx, int16_t* disp_out);
 SM_API sm_status sm_get_disp(sm_ctx* ctx, int32_t view, int16_t* dst);  /* DP[view], H*W int16 */

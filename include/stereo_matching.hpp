@@ -15,6 +15,7 @@
 // m.channels(), m.step, m.data}.  Non-OK statuses become std::runtime_error (the reference threw
 // cv::Exception from CV_Assert).
 #pragma once
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -61,7 +62,6 @@ class StereoMatching {
     StereoMatching(const Mat& I1_c, const Mat& I2_c, const Mat& I1_g, const Mat& I2_g, const Parameters& param,
                    int hip_device = 0)
         : h_(I1_c.rows), w_(I1_c.cols), d_(param.numDisparities) {
-        if (param.disSc != 1) throw std::invalid_argument("only PY_LEV = 1 (disSc = 1) is supported");
         sm_params p;
         sm_params_default(&p, param.numDisparities - 1, I1_c.rows, I1_c.cols);
         p.cost_method = costcalculation == "censusGrad" ? SM_COST_CENSUS_GRAD
@@ -77,8 +77,9 @@ class StereoMatching {
         p.census_ring = param.censusFunc == 3;
         p.lam_cen = (float)param.lamCen;
         p.lam_g = (float)param.lamG;
-        p.arm_l = param.cbca_crossL0;
-        p.arm_l_out = param.cbca_crossL_out0;
+        const int sc = param.disSc > 1 ? param.disSc : 1;   // calArms: L / scale (cpp:5367-5371)
+        p.arm_l = param.cbca_crossL0 / sc;
+        p.arm_l_out = param.cbca_crossL_out0 / sc;
         p.arm_c_thresh = param.cbca_cTresh0;
         p.arm_c_thresh_out = param.cbca_cTresh_out0;
         p.arm_min_l = param.cbca_minArmL;
@@ -132,8 +133,28 @@ class StereoMatching {
     friend void SolveAll(StereoMatching** smPyr, int PY_LVL, float REG_LAMBDA);
 };
 
+// SolveAll (cpp:2142-2208): PY_LVL = 1 scales vm[0]; PY_LVL in [2, 3] combines the levels
+// smPyr[0..PY_LVL-1] of main_.cpp:134-156's pyramid into smPyr[0].
 inline void SolveAll(StereoMatching** smPyr, int PY_LVL, float REG_LAMBDA) {
-    smPyr[0]->check(sm_solve_all(smPyr[0]->ctx_, PY_LVL, REG_LAMBDA), "SolveAll");
+    if (PY_LVL == 1) {
+        smPyr[0]->check(sm_solve_all(smPyr[0]->ctx_, PY_LVL, REG_LAMBDA), "SolveAll");
+        return;
+    }
+    std::vector<sm_ctx*> lv;
+    for (int i = 0; i < PY_LVL; i++) lv.push_back(smPyr[i]->ctx_);
+    smPyr[0]->check(sm_solve_all_pyr(lv.data(), PY_LVL, REG_LAMBDA), "SolveAll");
+}
+
+// cv::pyrDown for u8 images (main_.cpp:145-148) on the GPU; returns the (rows+1)/2 x (cols+1)/2 image.
+inline std::vector<uint8_t> pyrDown(const Mat& src, int hip_device = 0) {
+    std::vector<uint8_t> in((size_t)src.rows * src.cols * src.channels);
+    for (int r = 0; r < src.rows; r++)
+        std::copy(src.data + (size_t)r * src.step, src.data + (size_t)r * src.step + (size_t)src.cols * src.channels,
+                  in.begin() + (size_t)r * src.cols * src.channels);
+    std::vector<uint8_t> out((size_t)((src.rows + 1) / 2) * ((src.cols + 1) / 2) * src.channels);
+    if (sm_pyr_down(hip_device, in.data(), src.rows, src.cols, src.channels, out.data()) != SM_OK)
+        throw std::runtime_error("pyrDown failed");
+    return out;
 }
 
 }  // namespace smamd

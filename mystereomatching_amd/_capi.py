@@ -54,6 +54,8 @@ SIGNATURES = [
     ("sm_cost_calculate", C.c_int, [_P]),
     ("sm_solve_all", C.c_int, [_P, C.c_int32, C.c_float]),
     ("sm_disp_optimize", C.c_int, [_P, _P]),
+    ("sm_solve_all_pyr", C.c_int, [C.POINTER(_P), C.c_int32, C.c_float]),
+    ("sm_pyr_down", C.c_int, [C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32, _P]),
     ("sm_refine", C.c_int, [_P, _P]),
     ("sm_get_disp", C.c_int, [_P, C.c_int32, _P]),
     ("sm_set_disp", C.c_int, [_P, C.c_int32, _P]),

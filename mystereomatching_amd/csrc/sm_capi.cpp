@@ -666,13 +666,113 @@ sm_status sm_solve_all(sm_ctx* c, int32_t py_lev, float reg_lambda) {
     sm_status s = check(c);
     if (s) return s;
     if (c->stage != 2) return fail(c, SM_ESTATE, "sm_solve_all must follow sm_cost_calculate");
-    if (py_lev != 1) return fail(c, SM_EINVAL, "only PY_LEV = 1 is supported (main_.cpp:131)");
+    if (py_lev != 1) return fail(c, SM_EINVAL, "PY_LVL > 1 needs every level's context: use sm_solve_all_pyr");
     const float m = 1 + reg_lambda;
     const float w = (float)(1. / (double)m);  // Mat::inv of the 1x1 regMat (cpp:2164)
     for (int v = 0; v < n_views(c->p); v++)   // img_n = Do_refine ? 2 : 1 (cpp:2178)
         if ((s = run_scale(c, c->n_loaded, v, w, at(c, 0)))) return s;
     c->stage = 3;
     return SM_OK;
+}
+
+// invWgt = row 0 of regMat.inv() (cpp:2147-2168): OpenCV's invert for a CV_32F matrix of order
+// n <= 3 evaluates the adjugate over the determinant in double and rounds each entry to float.
+static bool pyr_weights(int L, float lam, float* w) {
+    float M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int s = 0; s < L; s++) {
+        if (s == 0) {
+            M[s][s] = 1 + lam;
+            if (L > 1) M[s][s + 1] = -lam;
+        } else if (s == L - 1) {
+            M[s][s] = 1 + lam;
+            M[s][s - 1] = -lam;
+        } else {
+            M[s][s] = 1 + 2 * lam;
+            M[s][s - 1] = -lam;
+            M[s][s + 1] = -lam;
+        }
+    }
+    if (L == 1) {
+        w[0] = (float)(1. / (double)M[0][0]);
+        return true;
+    }
+    if (L == 2) {
+        double d = (double)M[0][0] * M[1][1] - (double)M[0][1] * M[1][0];
+        if (d == 0.) return false;
+        d = 1. / d;
+        w[0] = (float)(M[1][1] * d);
+        w[1] = (float)(-M[0][1] * d);
+        return true;
+    }
+    double d = M[0][0] * ((double)M[1][1] * M[2][2] - (double)M[1][2] * M[2][1]) -
+               M[0][1] * ((double)M[1][0] * M[2][2] - (double)M[1][2] * M[2][0]) +
+               M[0][2] * ((double)M[1][0] * M[2][1] - (double)M[1][1] * M[2][0]);
+    if (d == 0.) return false;
+    d = 1. / d;
+    w[0] = (float)(((double)M[1][1] * M[2][2] - (double)M[1][2] * M[2][1]) * d);
+    w[1] = (float)(((double)M[0][2] * M[2][1] - (double)M[0][1] * M[2][2]) * d);
+    w[2] = (float)(((double)M[0][1] * M[1][2] - (double)M[0][2] * M[1][1]) * d);
+    return true;
+}
+
+sm_status sm_solve_all_pyr(sm_ctx* const* levels, int32_t py_lvl, float reg_lambda) {
+    if (!levels || !levels[0]) return SM_EINVAL;
+    sm_ctx* c = levels[0];
+    sm_status s = check(c);
+    if (s) return s;
+    if (py_lvl < 1 || py_lvl > 3)
+        return fail(c, SM_EINVAL, "PY_LVL must be in [1, 3] (OpenCV's closed-form small-matrix invert)");
+    if (py_lvl == 1) return sm_solve_all(c, 1, reg_lambda);
+    sm::PyrArgs a{};
+    a.levels = py_lvl;
+    a.n = c->n_loaded;
+    for (int l = 0; l < py_lvl; l++) {
+        sm_ctx* q = levels[l];
+        if (!q) return fail(c, SM_EINVAL, "null level context");
+        if (q->device != c->device) return fail(c, SM_EINVAL, "pyramid levels must share one device");
+        if (q->stage != 2) return fail(c, SM_ESTATE, "every level needs sm_cost_calculate (and no SolveAll yet)");
+        if (q->n_loaded != c->n_loaded) return fail(c, SM_EINVAL, "pyramid levels must hold the same number of pairs");
+        if (n_views(q->p) < n_views(c->p)) return fail(c, SM_EINVAL, "coarser levels need do_refine like level 0");
+        if (l > 0) {
+            const sm_params& pp = levels[l - 1]->p;
+            if (q->p.rows != (pp.rows + 1) / 2 || q->p.cols != (pp.cols + 1) / 2)
+                return fail(c, SM_EINVAL, "level sizes must follow pyrDown: ((rows + 1) / 2, (cols + 1) / 2)");
+            if (q->p.num_disparities < pp.num_disparities / 2 + 1)
+                return fail(c, SM_EINVAL, "level num_disparities too small for curD = (curD + 1) / 2");
+        }
+        a.H[l] = q->p.rows;
+        a.W[l] = q->p.cols;
+        a.D[l] = q->p.num_disparities;
+        if (l > 0) HIP_TRY(c, hipStreamSynchronize(q->st));   // coarse volumes complete
+    }
+    if (!pyr_weights(py_lvl, reg_lambda, a.w)) return fail(c, SM_EINVAL, "singular regularisation matrix");
+    for (int v = 0; v < n_views(c->p); v++) {
+        for (int l = 0; l < py_lvl; l++) a.vm[l] = v == 0 ? levels[l]->vm0 : levels[l]->vm1;
+        const double bytes = (double)a.n * c->nvol * 8.0;
+        if ((s = timed(c, v == 0 ? "solve_all_pyr" : "solve_all_pyr_r", bytes, [&] { sm::launch_solve_all_pyr(a, c->st); })))
+            return s;
+    }
+    c->stage = 3;
+    for (int l = 1; l < py_lvl; l++) levels[l]->stage = 3;
+    return SM_OK;
+}
+
+sm_status sm_pyr_down(int32_t dev, const uint8_t* src, int32_t rows, int32_t cols, int32_t ch, uint8_t* dst) {
+    if (!src || !dst || rows < 1 || cols < 1 || (ch != 1 && ch != 3)) return SM_EINVAL;
+    if (hipSetDevice(dev) != hipSuccess) return SM_EHIP;
+    const size_t in = (size_t)rows * cols * ch, out = (size_t)((rows + 1) / 2) * ((cols + 1) / 2) * ch;
+    uint8_t *dsrc = nullptr, *ddst = nullptr;
+    hipError_t e = hipMalloc((void**)&dsrc, in);
+    if (e == hipSuccess) e = hipMalloc((void**)&ddst, out);
+    if (e == hipSuccess) e = hipMemcpy(dsrc, src, in, hipMemcpyDefault);
+    if (e == hipSuccess) {
+        sm::launch_pyr_down(dsrc, ddst, rows, cols, ch, nullptr);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(dst, ddst, out, hipMemcpyDefault);
+    if (dsrc) hipFree(dsrc);
+    if (ddst) hipFree(ddst);
+    return e == hipSuccess ? SM_OK : SM_EHIP;
 }
 
 sm_status sm_disp_optimize(sm_ctx* c, int16_t* disp_out) {

@@ -69,6 +69,13 @@ struct SgmArgs {
     int n;                      // pairs in the launch
 };
 
+struct PyrArgs {                // SolveAll over PY_LVL pyramid levels (sm_pyramid.hip)
+    float* vm[3];               // level s volume [n][H_s][W_s][D_s]; vm[0] is updated in place
+    int H[3], W[3], D[3];
+    float w[3];                 // invWgt[s] = regInv(0, s)
+    int levels, n;
+};
+
 hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st);
 void launch_cost(const CostArgs& a, int method, int n, hipStream_t st);
 void launch_prep(const PrepArgs& a, int n, hipStream_t st);
@@ -86,6 +93,8 @@ void launch_region_vote(const int16_t* src, int16_t* dst, const uint32_t* arms, 
                         float rv_ratio, hipStream_t st);
 void launch_proper_ipol(const int16_t* src, int16_t* dst, const uint32_t* px, int n, int H, int W, int disp_occ,
                         hipStream_t st);
+void launch_pyr_down(const uint8_t* src, uint8_t* dst, int rows, int cols, int ch, hipStream_t st);
+void launch_solve_all_pyr(const PyrArgs& a, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int n, int H, int W, hipStream_t st);
 int sgm_k_for(int D);
 

@@ -73,8 +73,6 @@ class StereoMatching:
             self.DISP_OCC = -2 * 16                    # h:216
             self.region_vote_nums = 2                  # h:306
             self.rv_ratio, self.rv_s = 0.4, 20         # refine(): rv_ratio[] / rv_s[] (cpp:1400-1401)
-            if disSc != 1:
-                raise ValueError("pyramid levels > 0 (disSc > 1) are not supported; PY_LEV = 1")
 
         def to_c(self, cost: str, aggregation: str, optimization: str, batch: int = 1,
                  compute_right_view: bool = False, keep_final_volume: bool = False,
@@ -88,7 +86,9 @@ class StereoMatching:
             p.census_ring = 1 if self.censusFunc == 3 else 0
             p.lam_cen, p.lam_g = float(self.lamCen), float(self.lamG)
             p.grad_adaptive = int(self.gradFuse_adpWgt)
-            p.arm_l, p.arm_l_out = self.cbca_crossL[0], self.cbca_crossL_out[0]
+            # calArms divides the arm limits by the level's scale (cpp:5367-5371)
+            sc = self.disSc if self.disSc > 1 else 1
+            p.arm_l, p.arm_l_out = int(self.cbca_crossL[0] / sc), int(self.cbca_crossL_out[0] / sc)
             p.arm_c_thresh, p.arm_c_thresh_out = self.cbca_cTresh[0], self.cbca_cTresh_out[0]
             p.arm_min_l = self.cbca_minArmL
             p.cbca_iterations = self.cbca_iterationNum
@@ -216,9 +216,27 @@ class StereoMatching:
 
 
 def SolveAll(smPyr: Sequence[StereoMatching], PY_LVL: int, REG_LAMBDA: float):
-    """SolveAll (cpp:2142-2208); PY_LVL must be 1 (main_.cpp:131)."""
+    """SolveAll (cpp:2142-2208).  PY_LVL = 1 (main_.cpp:131) scales vm; PY_LVL in [2, 3] combines
+    the pyramid levels smPyr[0..PY_LVL-1] (built with pyrDown, main_.cpp:134-156) into smPyr[0]."""
     sm = smPyr[0]
-    _capi.check(sm._lib, sm._ctx, sm._lib.sm_solve_all(sm._ctx, int(PY_LVL), float(REG_LAMBDA)), "SolveAll")
+    if int(PY_LVL) == 1:
+        st = sm._lib.sm_solve_all(sm._ctx, 1, float(REG_LAMBDA))
+    else:
+        arr = (C.c_void_p * int(PY_LVL))(*[s._ctx.value for s in smPyr[:int(PY_LVL)]])
+        st = sm._lib.sm_solve_all_pyr(arr, int(PY_LVL), float(REG_LAMBDA))
+    _capi.check(sm._lib, sm._ctx, st, "SolveAll")
+
+
+def pyrDown(img, device: int = 0) -> np.ndarray:
+    """cv::pyrDown for u8 H x W or H x W x 3 images (main_.cpp:145-148), on the GPU."""
+    a = np.ascontiguousarray(img, np.uint8)
+    rows, cols = a.shape[:2]
+    ch = 1 if a.ndim == 2 else a.shape[2]
+    out = np.empty(((rows + 1) // 2, (cols + 1) // 2) + a.shape[2:], np.uint8)
+    lib = _capi.load()
+    st = lib.sm_pyr_down(device, _capi.ptr(a), rows, cols, ch, _capi.ptr(out))
+    _capi.check(lib, None, st, "pyrDown")
+    return out
 
 
 def _is_device_tensor(a) -> bool:

@@ -68,6 +68,13 @@ def load():
         lib.smo_proper_ipol.argtypes = [C.POINTER(Config), P, P]
         lib.smo_median3.argtypes = [C.c_int, C.c_int, P]
         lib.smo_refine.argtypes = [C.POINTER(Config), P, P, P, P]
+        lib.smo_pyr_down_u8.argtypes = [P, C.c_int, C.c_int, C.c_int, P]
+        lib.smo_pyr_weights.argtypes = [C.c_int, C.c_float, P]
+        lib.smo_pyr_weights.restype = C.c_int
+        lib.smo_solve_all_pyr.argtypes = [P, P, C.c_int, C.c_float]
+        lib.smo_solve_all_pyr.restype = C.c_int
+        lib.smo_run_pyr.argtypes = [C.POINTER(Config), C.c_int, P, P, P, P, P]
+        lib.smo_run_pyr.restype = C.c_int
         lib.smo_census.argtypes = [C.POINTER(Config), P, P]
         lib.smo_arms.argtypes = [C.POINTER(Config), P, P]
         lib.smo_cost_volume.argtypes = [C.POINTER(Config), P, P, P, P, C.c_int, P]
@@ -170,6 +177,34 @@ def refine(d0, d1, arms_l, bgr, cfg: Config) -> np.ndarray:
     load().smo_refine(C.byref(cfg), _p(out), _p(np.ascontiguousarray(d1, np.int16)),
                       _p(np.ascontiguousarray(arms_l, np.uint16)), _p(np.ascontiguousarray(bgr, np.uint8)))
     return out
+
+
+def pyr_down(img: np.ndarray) -> np.ndarray:
+    """cv::pyrDown of a u8 H x W or H x W x C image (smo_pyr_down_u8)."""
+    a = np.ascontiguousarray(img, np.uint8)
+    rows, cols = a.shape[:2]
+    ch = 1 if a.ndim == 2 else a.shape[2]
+    out = np.empty(((rows + 1) // 2, (cols + 1) // 2) + a.shape[2:], np.uint8)
+    load().smo_pyr_down_u8(_p(a), rows, cols, ch, _p(out))
+    return out
+
+
+def pyr_weights(py_lvl: int, reg_lambda: float = 0.3) -> np.ndarray:
+    w = np.zeros(3, np.float32)
+    if load().smo_pyr_weights(py_lvl, reg_lambda, _p(w)) != 0:
+        raise ValueError("PY_LVL must be in [1, 3]")
+    return w[:py_lvl]
+
+
+def run_pyr(pair: dict, cfg: Config, py_lvl: int) -> np.ndarray:
+    """smo_run_pyr: main_.cpp:131-166 with PY_LEV = py_lvl; returns DP[0]."""
+    arr = {k: np.ascontiguousarray(pair[k], np.uint8) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+    disp = np.empty((cfg.H, cfg.W), np.int16)
+    st = load().smo_run_pyr(C.byref(cfg), py_lvl, _p(arr["lbgr"]), _p(arr["rbgr"]), _p(arr["lgray"]),
+                            _p(arr["rgray"]), _p(disp))
+    if st != 0:
+        raise ValueError("oracle rejected the pyramid configuration")
+    return disp
 
 
 def census(gray: np.ndarray, cfg: Config) -> np.ndarray:

@@ -785,6 +785,166 @@ int smo_run(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
     return rc;
 }
 
+/* cv::pyrDown, 8-bit, BORDER_DEFAULT = BORDER_REFLECT_101: the separable 1-4-6-4-1 integer
+ * filter, (sum + 128) >> 8 (FixPtCast<uchar, 8>); intermediate row sums are exact ints. */
+void smo_pyr_down_u8(const uint8_t* src, int rows, int cols, int ch, uint8_t* dst) {
+    static const int k[5] = {1, 4, 6, 4, 1};
+    const int dr = (rows + 1) / 2, dc = (cols + 1) / 2;
+    for (int y = 0; y < dr; y++)
+        for (int x = 0; x < dc; x++)
+            for (int c = 0; c < ch; c++) {
+                int sum = 0;
+                for (int i = 0; i < 5; i++) {
+                    const int sy = smo_reflect101(2 * y + i - 2, rows);
+                    int row = 0;
+                    for (int j = 0; j < 5; j++) row += k[j] * src[((size_t)sy * cols + smo_reflect101(2 * x + j - 2, cols)) * ch + c];
+                    sum += k[i] * row;
+                }
+                dst[((size_t)y * dc + x) * ch + c] = (uint8_t)((sum + 128) >> 8);
+            }
+}
+
+/* SolveAll's regMat (cpp:2147-2163) and regInv = regMat.inv() (cpp:2164): OpenCV's invert for
+ * CV_32F with n <= 3 evaluates the adjugate / determinant in double and rounds each entry to
+ * float (n = 1: (float)(1. / a); n = 2: d = 1 / det2, Df(0,j) = (float)(+-S * d); n = 3: the
+ * t[0..2] cofactor row times 1 / det3).  invWgt[s] = regInv(0, s) (cpp:2165-2168). */
+int smo_pyr_weights(int L, float lam, float* w) {
+    if (L < 1 || L > 3) return -1;
+    float M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int s = 0; s < L; s++) {
+        if (s == 0) {
+            M[s][s] = 1 + lam;
+            if (L > 1) M[s][s + 1] = -lam;
+        } else if (s == L - 1) {
+            M[s][s] = 1 + lam;
+            M[s][s - 1] = -lam;
+        } else {
+            M[s][s] = 1 + 2 * lam;
+            M[s][s - 1] = -lam;
+            M[s][s + 1] = -lam;
+        }
+    }
+    if (L == 1) {
+        w[0] = (float)(1. / (double)M[0][0]);
+    } else if (L == 2) {
+        double d = (double)M[0][0] * M[1][1] - (double)M[0][1] * M[1][0];
+        if (d == 0.) return -1;
+        d = 1. / d;
+        w[0] = (float)(M[1][1] * d);
+        w[1] = (float)(-M[0][1] * d);
+    } else {
+        double d = M[0][0] * ((double)M[1][1] * M[2][2] - (double)M[1][2] * M[2][1]) -
+                   M[0][1] * ((double)M[1][0] * M[2][2] - (double)M[1][2] * M[2][0]) +
+                   M[0][2] * ((double)M[1][0] * M[2][1] - (double)M[1][1] * M[2][0]);
+        if (d == 0.) return -1;
+        d = 1. / d;
+        w[0] = (float)(((double)M[1][1] * M[2][2] - (double)M[1][2] * M[2][1]) * d);
+        w[1] = (float)(((double)M[0][2] * M[2][1] - (double)M[0][1] * M[2][2]) * d);
+        w[2] = (float)(((double)M[0][1] * M[1][2] - (double)M[0][2] * M[1][1]) * d);
+    }
+    return 0;
+}
+
+/* SolveAll (cpp:2169-2205) for PY_LVL levels, one view: sum += invWgt[s] * vm_s[curY][curX][curD]
+ * in level order, then curY /= 2, curX /= 2, curD = (curD + 1) / 2. */
+int smo_solve_all_pyr(const smo_config* cfgs, float* const* vms, int L, float lam) {
+    float w[3];
+    if (smo_pyr_weights(L, lam, w)) return -1;
+    const smo_config* c0 = &cfgs[0];
+    for (int y = 0; y < c0->H; y++)
+        for (int x = 0; x < c0->W; x++)
+            for (int d = 0; d < c0->D; d++) {
+                int cy = y, cx = x, cd = d;
+                float sum = 0;
+                for (int s = 0; s < L; s++) {
+                    const smo_config* c = &cfgs[s];
+                    if (cy >= c->H || cx >= c->W || cd >= c->D) return -1;
+                    const float cur = vms[s][((size_t)cy * c->W + cx) * c->D + cd];
+                    sum += w[s] * cur;
+                    cy /= 2;
+                    cx /= 2;
+                    cd = (cd + 1) / 2;
+                }
+                vms[0][((size_t)y * c0->W + x) * c0->D + d] = sum;
+            }
+    return 0;
+}
+
+int smo_run_pyr(const smo_config* c0, int L, const uint8_t* bgrL, const uint8_t* bgrR, const uint8_t* grayL,
+                const uint8_t* grayR, int16_t* disp) {
+    if (L < 1 || L > 3 || c0->H < 2 || c0->W < 2) return -1;
+    smo_config cfg[3];
+    uint8_t* img[3][4] = {{NULL}};            /* per level: bgrL, bgrR, grayL, grayR */
+    float* vm[3][2] = {{NULL}};
+    uint16_t* arms[3][2] = {{NULL}};
+    const int views = c0->do_refine ? 2 : 1;
+    int rc = -1, maxdisp = c0->D - 1, disSc = 1;
+    for (int p = 0; p < L; p++) {
+        smo_config* c = &cfg[p];
+        *c = *c0;
+        if (p > 0) {
+            c->H = (cfg[p - 1].H + 1) / 2;
+            c->W = (cfg[p - 1].W + 1) / 2;
+            if (c->H < 2 || c->W < 2) goto done;
+            const size_t np = (size_t)c->H * c->W;
+            for (int k = 0; k < 4; k++) {
+                const int ch = k < 2 ? 3 : 1;
+                img[p][k] = (uint8_t*)malloc(np * ch);
+                if (!img[p][k]) goto done;
+                const uint8_t* src = p == 1 ? (k == 0 ? bgrL : k == 1 ? bgrR : k == 2 ? grayL : grayR) : img[p - 1][k];
+                smo_pyr_down_u8(src, cfg[p - 1].H, cfg[p - 1].W, ch, img[p][k]);   /* main:145-148 */
+            }
+        }
+        c->D = maxdisp + 1;
+        c->arm_L = c0->arm_L / disSc;          /* calArms: L / scale (cpp:5369-5371) */
+        c->arm_L_out = c0->arm_L_out / disSc;
+        const uint8_t* bL = p ? img[p][0] : bgrL;
+        const uint8_t* bR = p ? img[p][1] : bgrR;
+        const uint8_t* gL = p ? img[p][2] : grayL;
+        const uint8_t* gR = p ? img[p][3] : grayR;
+        const size_t np = (size_t)c->H * c->W, nv = np * c->D;
+        for (int v = 0; v < views; v++) {
+            vm[p][v] = (float*)malloc(nv * 4);
+            if (!vm[p][v]) goto done;
+            smo_cost_volume(c, bL, bR, gL, gR, v, vm[p][v]);
+        }
+        for (int k = 0; k < 2; k++) {
+            arms[p][k] = (uint16_t*)malloc(np * 8);
+            if (!arms[p][k]) goto done;
+            smo_arms(c, k ? bR : bL, arms[p][k]);
+        }
+        if (c->aggregation == 1)
+            for (int v = 0; v < views; v++) smo_cbca_view(c, vm[p][v], arms[p][0], arms[p][1], v);
+        maxdisp = maxdisp / 2 + 1;             /* main:143 */
+        disSc *= 2;
+    }
+    for (int v = 0; v < views; v++) {          /* SolveAll(smPsy, PY_LEV, REG_LAMBDA) (main:158) */
+        float* vv[3] = {vm[0][v], vm[1][v], vm[2][v]};
+        if (c0->solve_all && smo_solve_all_pyr(cfg, vv, L, c0->reg_lambda)) goto done;
+    }
+    {
+        const smo_config* c = &cfg[0];
+        if (c->optimization == 1)
+            for (int v = 0; v < views; v++) smo_sgm(c, vm[0][v], v == 0 ? bgrL : bgrR);
+        smo_wta(c, vm[0][0], disp);
+        if (c->do_refine) {
+            int16_t* d1 = (int16_t*)malloc((size_t)c->H * c->W * 2);
+            if (!d1) goto done;
+            smo_wta(c, vm[0][1], d1);
+            smo_refine(c, disp, d1, arms[0][0], bgrL);
+            free(d1);
+        }
+    }
+    rc = 0;
+done:
+    for (int p = 0; p < 3; p++) {
+        for (int k = 0; k < 4; k++) free(img[p][k]);
+        for (int v = 0; v < 2; v++) free(vm[p][v]);
+        for (int k = 0; k < 2; k++) free(arms[p][k]);
+    }
+    return rc;
+}
+
 /* calErr (h:1748-1825): bad pixel ratio over mask == 255 with threshold `thres`. */
 float smo_bad_ratio(int H, int W, const int16_t* DP, const float* DT, const uint8_t* mask, float thres, float* rms_out) {
     int sumNum = 0, errorNumer = 0;

@@ -105,6 +105,22 @@ typedef struct smo_dumps {
 int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
                const uint8_t* grayL, const uint8_t* grayR, int16_t* disp, const smo_dumps* d);
 
+/* Cross-scale pyramid (main:131-158, SolveAll cpp:2142-2208 with PY_LVL > 1).
+ * cv::pyrDown for u8 images (BORDER_REFLECT_101): dst is ((rows+1)/2) x ((cols+1)/2),
+ * dst = (sum_ij k_i k_j src(2y+i-2, 2x+j-2) + 128) >> 8 with k = {1, 4, 6, 4, 1}. */
+void smo_pyr_down_u8(const uint8_t* src, int rows, int cols, int channels, uint8_t* dst);
+/* invWgt[s] = regInv(0, s) of SolveAll's regularisation matrix (cpp:2147-2167), OpenCV's float
+ * Mat::inv small-matrix path (n <= 3).  Returns 0, or -1 for PY_LVL outside [1, 3]. */
+int smo_pyr_weights(int py_lvl, float reg_lambda, float* w);
+/* SolveAll's cross-scale sum for one view: vms[s] is level s's volume (cfgs[s] its shape);
+ * vms[0] receives sum_s invWgt[s] * vm_s(y >> s, x >> s, d_s) with d_s = (d_{s-1} + 1) / 2. */
+int smo_solve_all_pyr(const smo_config* cfgs, float* const* vms, int py_lvl, float reg_lambda);
+/* main:131-166 with PY_LEV levels: per-level images by pyrDown, per-level Parameters
+ * (maxdisp_{p+1} = maxdisp_p / 2 + 1, disSc = 2^p: arm lengths L / disSc, L_out / disSc,
+ * cpp:5369-5371), costCalculate per level, SolveAll(PY_LEV), dispOptimize [+ refine] at level 0. */
+int smo_run_pyr(const smo_config* c0, int py_lvl, const uint8_t* bgrL, const uint8_t* bgrR,
+                const uint8_t* grayL, const uint8_t* grayR, int16_t* disp);
+
 /* Whole default pipeline for one pair (main:138-163 call order).  Optional dumps may be NULL:
  * vol_cost = vm[0] after the cost stage, vol_agg = after CBCA, vol_final = after SGM sum,
  * vol_right = vm[1] cost volume.  stage_ms[6] (optional): cost, cbca, solveall, sgm, wta, total.

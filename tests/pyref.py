@@ -416,3 +416,81 @@ def pipeline(pair, max_disp, cost="censusGrad", aggregate=True, solve=True, opti
         out["disp_raw"] = out["disp"]
         out["disp"] = refine(out["disp"], out["disp_right"], arms(lb), lb, D)
     return out
+
+
+# ---- cross-scale pyramid (main_.cpp:131-158, SolveAll cpp:2142-2208 with PY_LVL > 1) ----------
+
+def pyr_down(img):
+    """cv::pyrDown (u8, BORDER_REFLECT_101): separable 1-4-6-4-1, (sum + 128) >> 8."""
+    a = img.astype(np.int64)
+    rows, cols = a.shape[:2]
+    pad = [(2, 2), (2, 2)] + [(0, 0)] * (a.ndim - 2)
+    P = np.pad(a, pad, mode="reflect")          # numpy 'reflect' == REFLECT_101
+    k = [1, 4, 6, 4, 1]
+    dr, dc = (rows + 1) // 2, (cols + 1) // 2
+    rowsum = sum(k[j] * P[:, j:j + 2 * dc:2] for j in range(5))      # columns 2x + j - 2
+    tot = sum(k[i] * rowsum[i:i + 2 * dr:2] for i in range(5))       # rows 2y + i - 2
+    return ((tot + 128) >> 8).astype(np.uint8)
+
+
+def pyr_weights(L, lam=f32(0.3)):
+    """regInv(0, :) of SolveAll's float regularisation matrix via OpenCV's small-matrix invert."""
+    lam = f32(lam)
+    M = np.zeros((L, L), np.float32)
+    for s in range(L):
+        if s == 0:
+            M[s, s] = f32(1) + lam
+            if L > 1:
+                M[s, s + 1] = -lam
+        elif s == L - 1:
+            M[s, s] = f32(1) + lam
+            M[s, s - 1] = -lam
+        else:
+            M[s, s] = f32(1) + f32(f32(2) * lam)
+            M[s, s - 1] = -lam
+            M[s, s + 1] = -lam
+    m = M.astype(np.float64)
+    if L == 1:
+        return np.array([f32(1.0 / m[0, 0])], np.float32)
+    if L == 2:
+        d = 1.0 / (m[0, 0] * m[1, 1] - m[0, 1] * m[1, 0])
+        return np.array([m[1, 1] * d, -m[0, 1] * d]).astype(np.float32)
+    det = (m[0, 0] * (m[1, 1] * m[2, 2] - m[1, 2] * m[2, 1]) - m[0, 1] * (m[1, 0] * m[2, 2] - m[1, 2] * m[2, 0])
+           + m[0, 2] * (m[1, 0] * m[2, 1] - m[1, 1] * m[2, 0]))
+    d = 1.0 / det
+    return np.array([(m[1, 1] * m[2, 2] - m[1, 2] * m[2, 1]) * d, (m[0, 2] * m[2, 1] - m[0, 1] * m[2, 2]) * d,
+                     (m[0, 1] * m[1, 2] - m[0, 2] * m[1, 1]) * d]).astype(np.float32)
+
+
+def solve_all_pyr(vms, lam=f32(0.3)):
+    """vms[s]: level-s volume; returns the new level-0 volume."""
+    L = len(vms)
+    w = pyr_weights(L, lam)
+    H, W, D = vms[0].shape
+    yy, xx, dd = np.meshgrid(np.arange(H), np.arange(W), np.arange(D), indexing="ij")
+    acc = np.zeros((H, W, D), np.float32)
+    for s in range(L):
+        acc = (acc + (w[s] * vms[s][yy, xx, dd]).astype(np.float32)).astype(np.float32)
+        yy, xx, dd = yy // 2, xx // 2, (dd + 1) // 2
+    return acc
+
+
+def pipeline_pyr(pair, max_disp, L, paths=4):
+    """main_.cpp:131-163 with PY_LEV = L (censusGrad + CBCA, no refine)."""
+    lv = [dict(pair)]
+    for _ in range(1, L):
+        lv.append({k: pyr_down(v) for k, v in lv[-1].items() if k in ("lbgr", "rbgr", "lgray", "rgray")})
+    vms, md, sc = [], max_disp, 1
+    for p in lv:
+        D = md + 1
+        lb, rb, lg, rg = p["lbgr"], p["rbgr"], p["lgray"], p["rgray"]
+        gx0, gy0 = grads(lg)
+        gx1, gy1 = grads(rg)
+        aL = arms(lb, L=17 // sc, L_out=34 // sc)
+        aR = arms(rb, L=17 // sc, L_out=34 // sc)
+        vm = fuse(census_cost(census(lg), census(rg), D), grad_cost(gx0, gx1, gy0, gy1, aL, D), 13, 1)
+        vms.append(cbca(vm, aL, aR))
+        md, sc = md // 2 + 1, sc * 2
+    vm = solve_all_pyr(vms)
+    vm = sgm(vm, pair["lbgr"], paths=paths)
+    return wta(vm)

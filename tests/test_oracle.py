@@ -155,3 +155,35 @@ def test_proper_ipol_colour_255_never_wins(oracle):
     out = oracle.proper_ipol(dp, bgr, cfg)
     assert out[2, 2] == -1
     np.testing.assert_array_equal(out, pyref.proper_ipol(dp, bgr))
+
+
+# ---- cross-scale pyramid (PY_LEV > 1): pyrDown, SolveAll weights, whole pipeline -------------
+
+@pytest.mark.parametrize("shape", [(9, 13, 3), (10, 14), (2, 3, 3), (3, 2), (17, 8, 3), (5, 5)])
+def test_pyr_down(oracle, shape):
+    img = np.random.default_rng(sum(shape)).integers(0, 256, size=shape, dtype=np.uint8)
+    np.testing.assert_array_equal(oracle.pyr_down(img), pyref.pyr_down(img))
+
+
+def test_pyr_down_constant_and_ramp(oracle):
+    flat = np.full((7, 11, 3), 200, np.uint8)
+    np.testing.assert_array_equal(oracle.pyr_down(flat), np.full((4, 6, 3), 200, np.uint8))
+    ramp = np.tile(np.arange(16, dtype=np.uint8) * 10, (6, 1))
+    np.testing.assert_array_equal(oracle.pyr_down(ramp), pyref.pyr_down(ramp))
+
+
+@pytest.mark.parametrize("L", [1, 2, 3])
+@pytest.mark.parametrize("lam", [0.3, 0.1, 1.0])
+def test_pyr_weights(oracle, L, lam):
+    np.testing.assert_array_equal(oracle.pyr_weights(L, lam).view(np.uint32), pyref.pyr_weights(L, lam).view(np.uint32))
+    if L == 1:
+        assert oracle.pyr_weights(1, 0.3).view(np.uint32)[0] == 0x3F44EC4F   # the PY_LVL = 1 weight
+
+
+@pytest.mark.parametrize("L,H,W,md", [(2, 14, 21, 7), (3, 20, 26, 9)])
+def test_pyramid_pipeline(oracle, L, H, W, md):
+    p = tiny_pair(H, W, md + 1, 31 + L, smooth=True)
+    cfg = oracle.config(H, W, md)
+    np.testing.assert_array_equal(oracle.run_pyr(p, cfg, L), pyref.pipeline_pyr(p, md, L))
+    # PY_LEV = 1 through the pyramid driver is the plain pipeline
+    np.testing.assert_array_equal(oracle.run_pyr(p, cfg, 1), oracle.run(p, cfg)["disp"])

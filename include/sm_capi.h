@@ -14,6 +14,7 @@
  *   sm_solve_all       <- SolveAll(StereoMatching**&, PY_LVL, REG_LAMBDA)  stereoMatching.cpp:2142-2208
  *   sm_solve_all_pyr   <- the same with PY_LVL > 1 (one ctx per level)     stereoMatching.cpp:2142-2208
  *   sm_pyr_down        <- cv::pyrDown on the inputs                     main_.cpp:145-148
+ *   sm_cal_err         <- StereoMatching::calErr (one region)          stereoMatching.h:1748-1825
  *   sm_disp_optimize   <- StereoMatching::dispOptimize + DP[0]       stereoMatching.cpp:1046-1136, h:2724
  *   sm_refine          <- StereoMatching::refine (Do_refine)         stereoMatching.cpp:1138-1511, main_.cpp:165-166
  *   sm_get_disp / sm_set_disp <- public member DP[view]              stereoMatching.h:2724
@@ -161,6 +162,13 @@ SM_API sm_status sm_profile_enable(sm_ctx* ctx, int32_t on);
 SM_API sm_status sm_profile_read(sm_ctx* ctx, int32_t max, char* names /* max*48 */, int64_t* launches,
                                  double* total_ms, double* bytes_per_launch, int32_t* count);
 SM_API sm_status sm_profile_reset(sm_ctx* ctx);
+
+/* calErr (stereoMatching.h:1748-1825) for one region mask: over pixels with mask == 255, an error
+ * is DP < 0 or |DT - DP| > thres; *pbm = errors / count, *rms = sqrt(sum / count) where the float
+ * sum adds pow(dif, 2) per valid pixel and 2 per invalid one, in raster order (host code, exact
+ * reference arithmetic).  Host pointers; rows x cols, packed. */
+SM_API sm_status sm_cal_err(const int16_t* disp, const float* gt, const uint8_t* mask, int32_t rows, int32_t cols,
+                            float thres, float* pbm, float* rms);
 
 /* Diagnostics used by the parity tests. */
 SM_API float sm_expf_host(float x);   /* the device expf algorithm, evaluated on the host */

@@ -70,6 +70,7 @@ SIGNATURES = [
     ("sm_profile_enable", C.c_int, [_P, C.c_int32]),
     ("sm_profile_read", C.c_int, [_P, C.c_int32, _P, _P, _P, _P, C.POINTER(C.c_int32)]),
     ("sm_profile_reset", C.c_int, [_P]),
+    ("sm_cal_err", C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("sm_expf_host", C.c_float, [C.c_float]),
     ("sm_expf_device_range", C.c_int, [_P, C.c_uint32, C.c_uint32, _P]),
     ("sm_div_area_check", C.c_int, [_P, C.c_int32, C.c_int32, _P]),

@@ -1001,6 +1001,33 @@ sm_status sm_profile_reset(sm_ctx* c) {
     return SM_OK;
 }
 
+sm_status sm_cal_err(const int16_t* DP, const float* DT, const uint8_t* mask, int32_t rows, int32_t cols, float thres,
+                     float* pbm, float* rms) {
+    if (!DP || !DT || !mask || !pbm || !rms || rows < 1 || cols < 1) return SM_EINVAL;
+    int sumNum = 0, errorNumer = 0;
+    float errorValueSum = 0;
+    for (size_t i = 0; i < (size_t)rows * cols; i++) {
+        if (mask[i] != 255) continue;
+        sumNum++;
+        if (DP[i] >= 0) {
+            const float dif = fabsf(DT[i] - (float)DP[i]);
+            errorValueSum = (float)((double)errorValueSum + pow((double)dif, 2));   // float += pow(float, int)
+            if (dif > thres) errorNumer++;
+        } else {
+            errorNumer++;
+            errorValueSum += 2;
+        }
+    }
+    if (sumNum == 0) {   // the reference divides 0 / 0 here; report 0 instead of NaN
+        *pbm = 0;
+        *rms = 0;
+        return SM_OK;
+    }
+    *pbm = (float)errorNumer / sumNum;
+    *rms = sqrtf(errorValueSum / sumNum);
+    return SM_OK;
+}
+
 float sm_expf_host(float x) { return sm::expf_host(x); }
 
 sm_status sm_expf_device_range(sm_ctx* c, uint32_t first_bits, uint32_t n, float* out) {

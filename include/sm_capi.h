@@ -64,6 +64,7 @@ typedef enum sm_aggregation {
 typedef enum sm_optimization {
     SM_OPT_WTA = 0,          /* "" : WTA only (cpp:1104-1128) */
     SM_OPT_SGM = 1,          /* "sgm" (main:17; cpp:1051-1060) — default */
+    SM_OPT_SO = 2,           /* "so" scan-line DP + backtrack (cpp:1091-1105, 6272-6394) */
 } sm_optimization;
 
 /* The subset of StereoMatching::Parameters (h:85-351) that the hot path reads, plus the

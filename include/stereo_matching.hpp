@@ -71,9 +71,10 @@ class StereoMatching {
                                                         : -1;
         if (p.cost_method < 0) throw std::invalid_argument("unsupported costcalculation: " + costcalculation);
         if (aggregation != "CBCA" && !aggregation.empty()) throw std::invalid_argument("unsupported aggregation: " + aggregation);
-        if (optimization != "sgm" && !optimization.empty()) throw std::invalid_argument("unsupported optimization: " + optimization);
+        if (optimization != "sgm" && optimization != "so" && !optimization.empty())
+            throw std::invalid_argument("unsupported optimization: " + optimization);
         p.aggregation = aggregation == "CBCA" ? SM_AGG_CBCA : SM_AGG_NONE;
-        p.optimization = optimization == "sgm" ? SM_OPT_SGM : SM_OPT_WTA;
+        p.optimization = optimization == "sgm" ? SM_OPT_SGM : (optimization == "so" ? SM_OPT_SO : SM_OPT_WTA);
         p.census_ring = param.censusFunc == 3;
         p.lam_cen = (float)param.lamCen;
         p.lam_g = (float)param.lamG;

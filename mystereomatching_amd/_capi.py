@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libsm_hip.so")
 SM_OK, SM_EINVAL, SM_ENOMEM, SM_EHIP, SM_ESTATE = 0, 1, 2, 3, 4
 COST_METHODS = {"censusGrad": 0, "Census": 1, "ADCensus": 2, "AD": 3}
 AGGREGATIONS = {"": 0, "none": 0, "CBCA": 1}
-OPTIMIZATIONS = {"": 0, "wta": 0, "sgm": 1}
+OPTIMIZATIONS = {"": 0, "wta": 0, "sgm": 1, "so": 2}
 
 
 class sm_params(C.Structure):

@@ -56,6 +56,8 @@ struct sm_ctx {
     float* dummy = nullptr;     // 64 floats written by lanes past D
     uint8_t* flags = nullptr;   // [cap][npix] SGM colour-difference penalty bits, left image
     uint8_t* flags1 = nullptr;  // [cap][npix] same for the right image (do_refine)
+    uint8_t* so_trace = nullptr;   // [cap][npix][D] "so" choice codes
+    uint16_t* so_cidx = nullptr;   // [cap][npix] "so" row-minimum indices
     uint32_t* px = nullptr;     // [cap][2][npix] packed BGR
     int n_loaded = 0;
     int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized, 5 refined
@@ -157,7 +159,7 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (p.num_disparities < 1 || p.num_disparities > 1024) return bad("num_disparities must be in [1, 1024]");
     if (p.cost_method < 0 || p.cost_method > 3) return bad("unknown cost_method");
     if (p.aggregation < 0 || p.aggregation > 1) return bad("unknown aggregation");
-    if (p.optimization < 0 || p.optimization > 1) return bad("unknown optimization");
+    if (p.optimization < 0 || p.optimization > 2) return bad("unknown optimization");
     if (p.census_rv < 0 || p.census_ru < 0 || census_len(p) > 128) return bad("census code longer than 128 bits");
     if (p.arm_l_out < 0 || p.arm_l_out > 84 || p.arm_min_l < 0 || p.arm_min_l > 84 || p.arm_l < 0)
         return bad("arm lengths must be in [0, 84]");
@@ -205,7 +207,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 
 void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
-                    c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px};
+                    c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx};
     for (void* q : ptrs)
         if (q) hipFree(q);
     for (auto& r : c->recs) {
@@ -425,6 +427,23 @@ sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
             sm_status s = timed(c, name.c_str(), bytes, [&] { sm::launch_sgm_path(a, mode, n, c->st); });
             if (s) return s;
         }
+    } else if (p.optimization == SM_OPT_SO) {
+        // so(vm[i], DP[i], I_c) reads I[0] — the left colours — for both views (cpp:1098, 6284)
+        sm::SoArgs a{};
+        a.vm = vm;
+        a.trace = c->so_trace + (size_t)(B.disp - c->disp) * p.num_disparities;
+        a.cidx = c->so_cidx + (B.disp - c->disp);
+        a.px = B.px;
+        a.disp = disp;
+        a.H = p.rows;
+        a.W = p.cols;
+        a.D = p.num_disparities;
+        a.n = n;
+        a.keep_final = p.keep_final_volume;
+        const std::string name = std::string("so") + sfx;
+        sm_status s = timed(c, name.c_str(), (double)n * c->nvol * (4.0 + 1.0 + (p.keep_final_volume ? 4.0 : 0)),
+                            [&] { sm::launch_so(a, c->st); });
+        if (s) return s;
     } else {
         const std::string name = std::string("wta") + sfx;
         sm_status s = timed(c, name.c_str(), (double)n * c->nvol * 4.0 + (double)n * c->npix * 2,
@@ -598,6 +617,10 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
     if ((s = dalloc(c, &c->dummy, 64))) return s;
     if ((s = dalloc(c, &c->flags, cap * c->npix))) return s;
+    if (p->optimization == SM_OPT_SO) {
+        if ((s = dalloc(c, &c->so_trace, cap * c->nvol))) return s;
+        if ((s = dalloc(c, &c->so_cidx, cap * c->npix))) return s;
+    }
     if (p->do_refine) {
         if ((s = dalloc(c, &c->flags1, cap * c->npix))) return s;
         if ((s = dalloc(c, &c->disp1, cap * c->npix))) return s;

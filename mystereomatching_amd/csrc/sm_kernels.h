@@ -69,6 +69,15 @@ struct SgmArgs {
     int n;                      // pairs in the launch
 };
 
+struct SoArgs {                 // scan-line optimisation "so" (sm_so.hip)
+    float* vm;                  // [n][H][W][D] costs (accumulated in place when keep_final)
+    uint8_t* trace;             // [n][H][W][D] choice codes
+    uint16_t* cidx;             // [n][H][W] row-minimum index of the previous column
+    const uint32_t* px;         // [n][2][H][W] packed BGR (view 0 = I_c[0] is used)
+    int16_t* disp;              // [n][H][W]
+    int H, W, D, n, keep_final;
+};
+
 struct PyrArgs {                // SolveAll over PY_LVL pyramid levels (sm_pyramid.hip)
     float* vm[3];               // level s volume [n][H_s][W_s][D_s]; vm[0] is updated in place
     int H[3], W[3], D[3];
@@ -93,6 +102,7 @@ void launch_region_vote(const int16_t* src, int16_t* dst, const uint32_t* arms, 
                         float rv_ratio, hipStream_t st);
 void launch_proper_ipol(const int16_t* src, int16_t* dst, const uint32_t* px, int n, int H, int W, int disp_occ,
                         hipStream_t st);
+void launch_so(const SoArgs& a, hipStream_t st);
 void launch_pyr_down(const uint8_t* src, uint8_t* dst, int rows, int cols, int ch, hipStream_t st);
 void launch_solve_all_pyr(const PyrArgs& a, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int n, int H, int W, hipStream_t st);

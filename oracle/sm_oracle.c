@@ -534,6 +534,76 @@ void smo_wta(const smo_config* c, const float* vm, int16_t* disp) {
     }
 }
 
+/* so (cpp:6272-6394). */
+void smo_so(const smo_config* c, float* vm, int16_t* DP, const uint8_t* Ic) {
+    const int h = c->H, w = c->W, D = c->D;
+    int32_t* trace = (int32_t*)malloc((size_t)h * w * D * sizeof(int32_t));
+    for (int v = 0; v < h; v++)
+        for (int u = 1; u < w; u++) {
+            const uint8_t* IP = Ic + ((size_t)v * w + u) * 3;
+            const uint8_t* IPp = Ic + ((size_t)v * w + u - 1) * 3;
+            float sum = 0;
+            int L_isDisc = 0;
+            for (int ch = 0; ch < 3; ch++) sum += abs((int)IP[ch] - (int)IPp[ch]);
+            sum /= 3;
+            if (sum > 15) L_isDisc = 1;
+            float* vmP = vm + ((size_t)v * w + u) * D;
+            const float* vmPre = vm + ((size_t)v * w + u - 1) * D;
+            int32_t* traP = trace + ((size_t)v * w + u) * D;
+            for (int d = 0; d < D; d++) {
+                float Pn2 = 1.2f, Pn3 = 3.6f;   /* float Pn2 = 1.2; float Pn3 = 3.6; (cpp:6303-6304) */
+                if (L_isDisc) {
+                    Pn2 /= 2;
+                    Pn3 /= 2;
+                }
+                float c_min = vmPre[0];
+                float d_cMin = 0;
+                for (int dl = 1; dl < D; dl++)
+                    if (vmPre[dl] < c_min) {
+                        c_min = vmPre[dl];
+                        d_cMin = (float)dl;
+                    }
+                float c_minus = d > 0 ? vmPre[d - 1] + Pn2 : FLT_MAX;
+                float c_plus = d < D - 1 ? vmPre[d + 1] + Pn2 : FLT_MAX;
+                c_min += Pn3;
+                int d_min = d;
+                float cost_min = vmPre[d];
+                if (c_minus < cost_min) {
+                    d_min = d - 1;
+                    cost_min = c_minus;
+                }
+                if (c_plus < cost_min) {
+                    d_min = d + 1;
+                    cost_min = c_plus;
+                }
+                if (c_min < cost_min) {
+                    d_min = (int)d_cMin;
+                    cost_min = c_min;
+                }
+                vmP[d] += cost_min;
+                traP[d] = d_min;
+            }
+        }
+    for (int v = 0; v < h; v++) {
+        int16_t* disp = DP + (size_t)v * w;
+        const float* cP = vm + ((size_t)v * w + w - 1) * D;
+        float c_min = cP[0];
+        int d_min = 0;
+        for (int d = 1; d < D; d++)
+            if (cP[d] < c_min) {
+                c_min = cP[d];
+                d_min = d;
+            }
+        disp[w - 1] = (int16_t)d_min;
+        for (int u = w - 1; u > 0; u--) {
+            const int d_pre = trace[((size_t)v * w + u) * D + d_min];
+            disp[u - 1] = (int16_t)d_pre;
+            d_min = d_pre;
+        }
+    }
+    free(trace);
+}
+
 /* LRConsistencyCheck_normal (cpp:2262-2282), LOR = 0: a left disparity survives only if the
  * right map at u - d agrees within LRmaxDiff; otherwise -1. */
 void smo_lr_check(const smo_config* c, int16_t* disp0, const int16_t* disp1) {
@@ -739,14 +809,16 @@ int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR, co
     if (c->solve_all)
         for (int i = 0; i < views; i++) smo_solve_all(c, vm[i]);               /* img_n (cpp:2178) */
     t = now_ms(); ms[2] = t - t0; t0 = t;
+    if (refine && !(dp1 = (int16_t*)malloc(npix * 2))) goto done;
     if (c->optimization == 1)
         for (int i = 0; i < views; i++) smo_sgm(c, vm[i], i == 0 ? bgrL : bgrR);  /* cpp:1053-1060 */
+    if (c->optimization == 2)   /* "so": DP directly, I_c[0] for both views (cpp:1091-1105) */
+        for (int i = 0; i < views; i++) smo_so(c, vm[i], i == 0 ? disp : dp1, bgrL);
     if (d->vol_final) memcpy(d->vol_final, vm[0], nvol * 4);
     t = now_ms(); ms[3] = t - t0; t0 = t;
-    smo_wta(c, vm[0], disp);
+    if (c->optimization != 2) smo_wta(c, vm[0], disp);
     if (refine) {
-        if (!(dp1 = (int16_t*)malloc(npix * 2))) goto done;
-        smo_wta(c, vm[1], dp1);                                                /* cpp:1110-1127 */
+        if (c->optimization != 2) smo_wta(c, vm[1], dp1);                      /* cpp:1110-1127 */
         if (d->disp_left_raw) memcpy(d->disp_left_raw, disp, npix * 2);
         if (d->disp_right) memcpy(d->disp_right, dp1, npix * 2);
     }
@@ -926,11 +998,17 @@ int smo_run_pyr(const smo_config* c0, int L, const uint8_t* bgrL, const uint8_t*
         const smo_config* c = &cfg[0];
         if (c->optimization == 1)
             for (int v = 0; v < views; v++) smo_sgm(c, vm[0][v], v == 0 ? bgrL : bgrR);
-        smo_wta(c, vm[0][0], disp);
+        if (c->optimization == 2)
+            smo_so(c, vm[0][0], disp, bgrL);
+        else
+            smo_wta(c, vm[0][0], disp);
         if (c->do_refine) {
             int16_t* d1 = (int16_t*)malloc((size_t)c->H * c->W * 2);
             if (!d1) goto done;
-            smo_wta(c, vm[0][1], d1);
+            if (c->optimization == 2)
+                smo_so(c, vm[0][1], d1, bgrL);
+            else
+                smo_wta(c, vm[0][1], d1);
             smo_refine(c, disp, d1, arms[0][0], bgrL);
             free(d1);
         }

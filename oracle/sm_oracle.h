@@ -43,7 +43,7 @@ typedef struct smo_config {
     int cbca_iters;              /* cbca_iterationNum = 2 (h:260) */
     int solve_all;               /* apply SolveAll(PY_LEV=1) (main:158) */
     float reg_lambda;            /* REG_LAMBDA = 0.3 (main:157) */
-    int optimization;            /* 0 WTA only, 1 SGM (main:17) */
+    int optimization;            /* 0 WTA only, 1 SGM (main:17), 2 "so" scan-line DP (cpp:1091-1105) */
     int sgm_paths;               /* 4 (cpp:6214); 8 = full direction table (cpp:6207-6208) */
     float sgm_p1, sgm_p2;        /* 1.0, 3.0 hard-coded in updateCost (h:2234-2235) */
     int sgm_cor_thres;           /* sgm_corDifThres = 15 (h:239) */
@@ -81,6 +81,10 @@ float smo_solve_all_weight(float reg_lambda);
 void smo_solve_all(const smo_config* c, float* vm);
 void smo_sgm(const smo_config* c, float* vm, const uint8_t* bgrL);
 void smo_wta(const smo_config* c, const float* vm, int16_t* disp);
+/* so (cpp:6272-6394): per-row left-to-right DP with trace, then backtracking; vm is updated in
+ * place (accumulated), DP written directly.  Ic is I[0] = the LEFT colour image for both views
+ * (dispOptimize passes I_c and so() reads I[0] only, cpp:1098, 6284). */
+void smo_so(const smo_config* c, float* vm, int16_t* disp, const uint8_t* Ic);
 
 /* refine() stages (cpp:1364-1506); all act in place on an H*W int16 map. */
 void smo_lr_check(const smo_config* c, int16_t* disp0, const int16_t* disp1);          /* cpp:2262-2282 */

@@ -494,3 +494,47 @@ def pipeline_pyr(pair, max_disp, L, paths=4):
     vm = solve_all_pyr(vms)
     vm = sgm(vm, pair["lbgr"], paths=paths)
     return wta(vm)
+
+
+def so(vm, bgr):
+    """so (cpp:6272-6394): row DP left to right with trace + backtracking; returns (vm, DP)."""
+    H, W, D = vm.shape
+    vm = vm.copy()
+    I = bgr.astype(np.int64)
+    BIG = np.finfo(f32).max
+    trace = np.zeros((H, W, D), np.int64)
+    dd = np.arange(D)
+    for v in range(H):
+        for u in range(1, W):
+            s_ = f32(0)
+            for ch in range(3):
+                s_ = f32(s_ + f32(abs(int(I[v, u, ch]) - int(I[v, u - 1, ch]))))
+            s_ = f32(s_ / f32(3))
+            disc = s_ > 15
+            Pn2 = f32(f32(1.2) / f32(2)) if disc else f32(1.2)
+            Pn3 = f32(f32(3.6) / f32(2)) if disc else f32(3.6)
+            pre = vm[v, u - 1]
+            dc = int(np.argmin(pre))               # first minimum
+            cm = f32(pre[dc] + Pn3)
+            cminus = np.full(D, BIG, f32)
+            cminus[1:] = (pre[:-1] + Pn2).astype(f32)
+            cplus = np.full(D, BIG, f32)
+            cplus[:-1] = (pre[1:] + Pn2).astype(f32)
+            best = pre.copy()
+            dmin = dd.copy()
+            m = cminus < best
+            best, dmin = np.where(m, cminus, best), np.where(m, dd - 1, dmin)
+            m = cplus < best
+            best, dmin = np.where(m, cplus, best), np.where(m, dd + 1, dmin)
+            m = cm < best
+            best, dmin = np.where(m, cm, best), np.where(m, dc, dmin)
+            vm[v, u] = (vm[v, u] + best.astype(f32)).astype(f32)
+            trace[v, u] = dmin
+    DP = np.zeros((H, W), np.int16)
+    for v in range(H):
+        d = int(np.argmin(vm[v, W - 1]))
+        DP[v, W - 1] = d
+        for u in range(W - 1, 0, -1):
+            d = int(trace[v, u, d])
+            DP[v, u - 1] = d
+    return vm, DP

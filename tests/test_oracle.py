@@ -187,3 +187,20 @@ def test_pyramid_pipeline(oracle, L, H, W, md):
     np.testing.assert_array_equal(oracle.run_pyr(p, cfg, L), pyref.pipeline_pyr(p, md, L))
     # PY_LEV = 1 through the pyramid driver is the plain pipeline
     np.testing.assert_array_equal(oracle.run_pyr(p, cfg, 1), oracle.run(p, cfg)["disp"])
+
+
+# ---- scan-line optimisation "so" (cpp:6272-6394, optimization == "so") ---------------------
+
+@pytest.mark.parametrize("H,W,D,idx", [(7, 19, 6, 1), (9, 23, 11, 2)])
+def test_so_bitexact(oracle, H, W, D, idx):
+    p = tiny_pair(H, W, D, 60 + idx)
+    cfg = oracle.config(H, W, D - 1, optimization=2)
+    got = oracle.run(p, cfg, dumps=True)
+    ref_vm, ref_dp = pyref.so(pyref.solve_all(pyref.pipeline(p, D - 1)["agg"]), p["lbgr"])
+    np.testing.assert_array_equal(got["final"].view(np.uint32), ref_vm.view(np.uint32))
+    np.testing.assert_array_equal(got["disp"], ref_dp)
+    # refine with "so": DP[1] from vm[1] with the LEFT colours (so() reads I[0] only)
+    cfgr = oracle.config(H, W, D - 1, optimization=2, do_refine=1)
+    r = oracle.run_ex(p, cfgr, dumps=("agg_right", "disp_right"))
+    _, ref_d1 = pyref.so(pyref.solve_all(r["agg_right"]), p["lbgr"])
+    np.testing.assert_array_equal(r["disp_right"], ref_d1)

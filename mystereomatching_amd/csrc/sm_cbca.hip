@@ -54,6 +54,9 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 // 5-6 waves per CU the LDS rings allow, so PF tiles of loads are kept in flight; the loads of PF
 // tiles plus the stores of one stay below the 63 of vmcnt (V sweeps load one right-arm word per
 // position and set, hence their shorter tiles).
+// The normalising sweeps use T = 10 with two tiles in flight: their rings (2 lag + T + 1 slots of
+// S plus a u16 area ring) then fit five waves per CU instead of four (Teddy x16, same box:
+// h_norm 0.459 -> 0.425 ms, v_norm 0.505 -> 0.480 ms with the LDS-staged arm words).
 // (Overridable at build time for tuning sweeps, see tools/build_variants.sh.)
 #ifndef SM_CB_T_SCAN_H
 #define SM_CB_T_SCAN_H 24
@@ -62,10 +65,10 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #define SM_CB_T_SCAN_V 24
 #endif
 #ifndef SM_CB_T_NORM_H
-#define SM_CB_T_NORM_H 24
+#define SM_CB_T_NORM_H 10
 #endif
 #ifndef SM_CB_T_NORM_V
-#define SM_CB_T_NORM_V 16
+#define SM_CB_T_NORM_V 10
 #endif
 #ifndef SM_CB_PF_SCAN_H
 #define SM_CB_PF_SCAN_H 1
@@ -74,10 +77,18 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #define SM_CB_PF_SCAN_V 1
 #endif
 #ifndef SM_CB_PF_NORM_H
-#define SM_CB_PF_NORM_H 1
+#define SM_CB_PF_NORM_H 2
 #endif
 #ifndef SM_CB_PF_NORM_V
-#define SM_CB_PF_NORM_V 1
+#define SM_CB_PF_NORM_V 2
+#endif
+// Arm words of a tile are staged in LDS (SM_CB_LDS_WIN): the pixel's own arm pair of position k is
+// a broadcast read, and in horizontal sweeps the other image's arm pair of lane d at position k is
+// read from a staged span of 64 + T - 1 words at k + 63 - d (left view) / k + d (right view).  This
+// replaces per position and set a v_readlane (own) and a readlane + v_mov + DPP wave shift (other
+// image) by LDS reads with immediate offsets.  0 keeps the DPP-shifted register window.
+#ifndef SM_CB_LDS_WIN
+#define SM_CB_LDS_WIN 1
 #endif
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
     return mode == CB_SCAN ? (horiz ? SM_CB_T_SCAN_H : SM_CB_T_SCAN_V)
@@ -99,12 +110,22 @@ __host__ __device__ inline int cbca_ring(int lag, bool horiz, int mode) {
     return (2 * lag + T + 1 + T - 1) / T * T;
 }
 // dynamic LDS in 4-byte words: S ring(s) of ring x 64 floats, then the u16 area ring (6 bytes
-// per slot and lane; 8-byte {S, area} records were measured slower: one wave less per CU)
-__host__ __device__ inline int cbca_smem_words(int lag, bool horiz, int mode) {
+// per slot and lane; 8-byte {S, area} records were measured slower: one wave less per CU), then
+// the staged arm words of one tile (SM_CB_LDS_WIN): per set T own words [+ 64 + T - 1 span words]
+__host__ __device__ inline int cbca_ring_words(int lag, bool horiz, int mode) {
     const int ring = cbca_ring(lag, horiz, mode);
     const int floats = mode == CB_NORM_SCAN ? 2 : 1;
     const int u16s = mode == CB_SCAN ? 0 : 1;
     return ring * 64 * floats + ring * 32 * u16s;
+}
+__host__ __device__ inline int cbca_win_words(bool horiz, int mode) {
+    if (!SM_CB_LDS_WIN) return 0;
+    const int T = cbca_tile(horiz, mode);
+    const int nsets = mode == CB_SCAN ? 1 : (mode == CB_NORM ? 2 : 3);
+    return nsets * (T + (horiz ? 64 + T - 1 : 0));
+}
+__host__ __device__ inline int cbca_smem_words(int lag, bool horiz, int mode) {
+    return cbca_ring_words(lag, horiz, mode) + cbca_win_words(horiz, mode);
 }
 
 template <bool HORIZ, int T, int NSETS>
@@ -112,6 +133,7 @@ struct CbTile {
     float x[T];                          // vm at positions j0 .. j0+T-1
     uint32_t a0[NSETS];                  // lane k < T: left arm pair at position (j0 + k - off)
     uint32_t a1v[NSETS];                 // H: lane k < T: right arm pair at position (j0 + k - off)
+    uint32_t a1w[SM_CB_LDS_WIN && HORIZ ? NSETS : 1][2];  // H, LDS window: the other image's span
     uint32_t a1[HORIZ ? 1 : NSETS][T];   // V: right arm pair at (row j0 + k - off, u - d)
 };
 
@@ -143,6 +165,8 @@ struct CbLine {
     int c64;                  // first disparity of the chunk
     uint32_t vmask;           // V sweeps: all ones if u - d >= 0 else 0 (constant along the line)
     uint32_t sh[NSETS];       // H sweeps: shifted right-arm window per set
+    uint32_t* wown;           // LDS window: own arm words of the tile, T per set
+    uint32_t* wspan;          // LDS window (H): the other image's span, 64 + T - 1 per set
     float S1, S2;
     uint32_t Acc;
     int ws;                   // ring slot of the tile's first position
@@ -187,7 +211,15 @@ struct CbLine {
             // matters for the strided column loads of vertical sweeps)
             const int p0 = base + lane;
             t.a0[s] = buf_ld_u32(A0r[s], (lane < T && (unsigned)p0 < (unsigned)len) ? (uint32_t)(p0 * pstride) * 4u : 0x80000000u, 0);
-            if (HORIZ) {
+            if (HORIZ && SM_CB_LDS_WIN) {
+                // the other image's arm pairs that lanes c64 .. c64 + 63 pair with at positions
+                // base .. base + T - 1: left view q = p - d in [base - c64 - 63, base - c64 + T - 1],
+                // right view q = p + d in [base + c64, base + c64 + 63 + T - 1]; 0 outside the line
+                const int q0 = RV ? base + c64 : base - c64 - 63;
+                const int qa = q0 + lane, qb = q0 + 64 + lane;
+                t.a1w[s][0] = buf_ld_u32(A1r[s], (unsigned)qa < (unsigned)len ? (uint32_t)qa * 4u : 0x80000000u, 0);
+                t.a1w[s][1] = buf_ld_u32(A1r[s], (lane < T - 1 && (unsigned)qb < (unsigned)len) ? (uint32_t)qb * 4u : 0x80000000u, 0);
+            } else if (HORIZ) {
                 // H window input at position base + lane: left view — the right pixel of lane 0
                 // (shifted in at lane 0); right view — the left pixel of lane 63 (shifted in there)
                 const int q = RV ? base + lane + c64 + 63 : base + lane - c64;
@@ -202,7 +234,7 @@ struct CbLine {
 
     // Advance every set's window to position j (call once per position, in order).
     __device__ __forceinline__ void advance(const Tile& t, int k, int /*j*/) {
-        if (HORIZ) {
+        if (HORIZ && !SM_CB_LDS_WIN) {
 #pragma unroll
             for (int s = 0; s < NSETS; s++) {
                 const uint32_t in = (uint32_t)__builtin_amdgcn_readlane((int)t.a1v[s], k);
@@ -213,9 +245,27 @@ struct CbLine {
 
     // intersection arm pair of set s at tile position k
     __device__ __forceinline__ uint32_t isect(const Tile& t, int s, int k) const {
+        if (SM_CB_LDS_WIN) {
+            const uint32_t a0 = wown[s * T + k];   // broadcast read
+            const uint32_t a1 = HORIZ ? wspan[s * (64 + T - 1) + (RV ? k + lane : k + 63 - lane)] : (t.a1[s][k] & vmask);
+            return pkmin(a0, a1);
+        }
         const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
         const uint32_t a1 = HORIZ ? sh[s] : (t.a1[s][k] & vmask);
         return pkmin(a0, a1);
+    }
+    // stage the tile's arm words in LDS (one wave: its LDS accesses complete in order)
+    __device__ __forceinline__ void stage(const Tile& t) {
+        if (!SM_CB_LDS_WIN) return;
+#pragma unroll
+        for (int s = 0; s < NSETS; s++) {
+            if (lane < T) wown[s * T + lane] = t.a0[s];
+            if (HORIZ) {
+                uint32_t* sp = wspan + s * (64 + T - 1);
+                sp[lane] = t.a1w[s][0];
+                if (lane < T - 1) sp[64 + lane] = t.a1w[s][1];
+            }
+        }
     }
 
     __device__ __forceinline__ int uwrap(int s) const {  // uniform slot, any s in (-2 ring, 3 ring)
@@ -248,6 +298,7 @@ struct CbLine {
         const int s20 = uwrap(ws - 2 * lag);    // slot of i2 = j0 - 2 lag
         const int i0 = j0 - lag;
         const __amdgpu_buffer_rsrc_t ob = tile_rsrc(i0);
+        stage(t);
         // phase A: inputs j0 .. j0+T-1 (+ arm windows)
 #pragma unroll
         for (int k = 0; k < T; k++) {
@@ -394,7 +445,7 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
     L.ring = cbca_ring(a.lag, HORIZ, MODE);
-    if (HORIZ && RV) {
+    if (HORIZ && RV && !SM_CB_LDS_WIN) {
         // right view: the window before each set's first position p0 = -off holds, in lane l, the
         // left image's arm pair at p0 - 1 + c64 + l (0 outside the line)
 #pragma unroll
@@ -406,6 +457,8 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.r1 = smem;
     L.r2 = smem + (size_t)L.ring * 64;
     L.ra = (uint16_t*)(smem + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
+    L.wown = (uint32_t*)(smem + cbca_ring_words(a.lag, HORIZ, MODE));
+    L.wspan = L.wown + NSETS * T;
     L.scale = a.scale;
     {   // zero the rings: reads of positions before the line start then yield S = 0, area = 0
         const int words = cbca_smem_words(a.lag, HORIZ, MODE);

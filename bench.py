@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
+    ap.add_argument("--opt", default="sgm", choices=["sgm", "so"],
+                    help='optimization selector (h:53): "sgm" (default) or "so" scan-line DP (cpp:6272-6394)')
     ap.add_argument("--refine", action="store_true",
                     help="Do_refine = 1 (h:70): both views through CBCA/SolveAll/SGM/WTA, then refine() "
                          "(LR check, 2x region vote, 2x proper interpolation, 3x3 median)")
@@ -80,7 +82,9 @@ def main():
     D = md + 1
     # this rank's shard of the global batch: pair indices [rank*B, rank*B + B)
     batch = S.make_batch(B, H, W, D, first_index=rank * B)
-    sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine))
+    sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt)
+    if args.opt == "so":
+        desc = desc.replace("SGM 4-path+WTA", "so (scan-line DP)").replace("SGM 8-path+WTA", "so (scan-line DP)")
     if args.refine:
         desc = desc + " + Do_refine (right view CBCA/SGM, LR check, region vote, proper ipol, median)"
     sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
@@ -135,7 +139,8 @@ def main():
                               "GB_s": round(gbs, 1), "bytes_per_launch": k["bytes_per_launch"]}
         dom = max(kern_out, key=lambda n: kernels[n]["total_ms"])
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}{'_refine' if args.refine else ''}_b{B}.json")
+        tag = ("_refine" if args.refine else "") + ("_so" if args.opt == "so" else "")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}{tag}_b{B}.json")
         if os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
@@ -149,7 +154,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
-        cfg = O.config(H, W, md, sgm_paths=paths, do_refine=int(args.refine))
+        cfg = O.config(H, W, md, sgm_paths=paths, do_refine=int(args.refine), optimization=2 if args.opt == "so" else 1)
         n, t_cpu = 0, 0.0
         while n == 0 or (t_cpu < args.cpu_seconds and n < B):
             pair = {k: batch[k][n] for k in ("lbgr", "rbgr", "lgray", "rgray")}
@@ -170,7 +175,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded piecewise-planar pairs, mystereomatching_amd/synthetic.py)",
             "config": {"workload": desc, "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": B * world,
-                       "sgm_paths": paths, "refine": bool(args.refine),
+                       "sgm_paths": paths, "optimization": args.opt, "refine": bool(args.refine),
                        "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
             "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kern_out,

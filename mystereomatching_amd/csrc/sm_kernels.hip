@@ -51,6 +51,9 @@ __global__ void k_pack_bgr(const uint8_t* __restrict__ bgr, uint32_t* __restrict
     }
 }
 
+#ifndef SM_PREP_PROBE
+#define SM_PREP_PROBE 0   // timing probes: 1 = no arms, 2 = no census (results wrong)
+#endif
 __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
     extern __shared__ __align__(16) unsigned char prep_raw[];
     const int H = a.H, W = a.W, rv = a.rv, ru = a.ru, Lo = a.L_out;
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         if (u >= W || v >= H) continue;
         const size_t o = img * npix + (size_t)v * W + u;
         // census (genCensusCode_NC_Sur, h:867-934)
-        if (a.do_census) {
+        if (a.do_census && SM_PREP_PROBE != 2) {
             const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
             const int c = g[0];
             uint64_t w[2] = {0, 0};
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         const uint32_t* pc = P + (size_t)v * W + u;
         // cross arms (calHorVerDis 7-arg, cpp:2959-3050), direction order L, R, U, D; the walks
         // read the packed image (lanes = consecutive pixels, so every step is one coalesced load)
-        if (a.do_arms) {
+        if (a.do_arms && SM_PREP_PROBE != 1) {
             const uint32_t center = pc[0];
             uint32_t packed = 0;
 #pragma unroll
@@ -228,6 +231,9 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 // ---------------------------------------------------------------------------------------
 #ifndef SM_COST_PROBE
 #define SM_COST_PROBE 0
+#endif
+#ifndef SM_COST_STORE_AUX
+#define SM_COST_STORE_AUX 2   // buffer store cache policy: slc = non-temporal (see SM_ST_AUX, sm_device.h)
 #endif
 #ifndef SM_COST_UNROLL
 #define SM_COST_UNROLL 1
@@ -419,7 +425,8 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
 #if SM_COST_PROBE == 2
             res = (float)d;                              // timing probe: stores only
 #endif
-            buf_st(ro, (uint32_t)((pl * D + d) * 4), 0, res);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, (int)((pl * D + d) * 4), 0,
+                                                  SM_COST_STORE_AUX);
         };
         if (ONE) {
             elem(lane, u - sgn * lane);

@@ -186,10 +186,10 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
 #pragma unroll
             for (int c = 0; c < KV; c++)
                 if (FULL || cval[c])
-                    *(float4*)(base + (long)j * vstep + d0 + 4 * c) = make_float4(f[4 * c + 0], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]);
+                    st_stream4(base + (long)j * vstep + d0 + 4 * c, make_float4(f[4 * c + 0], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]));
         } else {
 #pragma unroll
-            for (int k = 0; k < K; k++) pk[k][(long)j * sst[k]] = f[k];
+            for (int k = 0; k < K; k++) st_stream(pk[k] + (long)j * sst[k], f[k]);
         }
     };
 
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
     auto store4 = [&](char* r, uint32_t so, const float* f) {
 #pragma unroll
         for (int c = 0; c < KV; c++)
-            if (FULLC || cval[c]) *(float4*)(r + so + voff[c]) = make_float4(f[4 * c + 0], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]);
+            if (FULLC || cval[c]) st_stream4((float*)(r + so + voff[c]), make_float4(f[4 * c + 0], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]));
     };
 
     auto process = [&](const RowTile<KV, T>& t, int j0) {

@@ -86,8 +86,11 @@ __device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int num_bytes = 0x7fffffff) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, num_bytes, 0x00020000);
 }
+#ifndef SM_LD_AUX
+#define SM_LD_AUX 0   // cache policy of streaming volume loads (tuning)
+#endif
 __device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, SM_LD_AUX));
 }
 __device__ __forceinline__ uint32_t buf_ld_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
@@ -112,6 +115,24 @@ __device__ __forceinline__ void st_stream(float* p, float v) {
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
+#endif
+}
+#ifndef SM_NT_LOADS
+#define SM_NT_LOADS 1   // SGM C / path-sum loads non-temporal: last path 0.302 -> 0.249 ms (Teddy x16)
+#endif
+__device__ __forceinline__ float ld_stream(const float* p) {
+#if SM_NT_LOADS
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float4 ld_stream4(const float* p) {
+#if SM_NT_LOADS
+    return make_float4(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2),
+                       __builtin_nontemporal_load(p + 3));
+#else
+    return *(const float4*)p;
 #endif
 }
 __device__ __forceinline__ void st_stream4(float* p, float4 v) {

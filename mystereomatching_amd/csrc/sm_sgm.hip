@@ -158,13 +158,13 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
             if (VEC) {
 #pragma unroll
                 for (int c = 0; c < KV; c++) {
-                    const float4 v = *(const float4*)(cbase + off + ldc[c]);
+                    const float4 v = ld_stream4(cbase + off + ldc[c]);
                     t.c[s][4 * c + 0] = v.x;
                     t.c[s][4 * c + 1] = v.y;
                     t.c[s][4 * c + 2] = v.z;
                     t.c[s][4 * c + 3] = v.w;
                     if (!(MODE & SGM_FIRST)) {
-                        const float4 q = *(const float4*)(abase + off + ldc[c]);
+                        const float4 q = ld_stream4(abase + off + ldc[c]);
                         t.acc[s][4 * c + 0] = q.x;
                         t.acc[s][4 * c + 1] = q.y;
                         t.acc[s][4 * c + 2] = q.z;
@@ -174,8 +174,8 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
             } else {
 #pragma unroll
                 for (int k = 0; k < K; k++) {
-                    t.c[s][k] = cbase[off + ld[k]];
-                    if (!(MODE & SGM_FIRST)) t.acc[s][k] = abase[off + ld[k]];
+                    t.c[s][k] = ld_stream(cbase + off + ld[k]);
+                    if (!(MODE & SGM_FIRST)) t.acc[s][k] = ld_stream(abase + off + ld[k]);
                 }
             }
         }
@@ -377,13 +377,13 @@ __global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
             const uint32_t so = soff(j0, s);
 #pragma unroll
             for (int c = 0; c < KV; c++) {
-                const float4 v = *(const float4*)(rc + so + voff[c]);
+                const float4 v = ld_stream4((const float*)(rc + so + voff[c]));
                 t.c[s][4 * c + 0] = v.x;
                 t.c[s][4 * c + 1] = v.y;
                 t.c[s][4 * c + 2] = v.z;
                 t.c[s][4 * c + 3] = v.w;
                 if (!(MODE & SGM_FIRST)) {
-                    const float4 q = *(const float4*)(ra + so + voff[c]);
+                    const float4 q = ld_stream4((const float*)(ra + so + voff[c]));
                     t.acc[s][4 * c + 0] = q.x;
                     t.acc[s][4 * c + 1] = q.y;
                     t.acc[s][4 * c + 2] = q.z;

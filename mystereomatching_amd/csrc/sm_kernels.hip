@@ -259,11 +259,24 @@ constexpr int LUT_A_N = 129, LUT_B_N = 766;
 template <int CW>
 __host__ __device__ constexpr int cost_rec_u4() { return CW <= 2 ? 1 : 2; }
 
+// Select-free gradient elements (NOSEL = censusGrad with >= 3 census words and OORZ): an
+// out-of-range candidate's staged record carries gx = gy = 1e30 and a census count bias of
+// icd, so the element's own arithmetic yields the reference's out-of-range value without a
+// select: min(|f - 1e30|, T) = T per axis (T = grad_trunc, 500) makes G >= 0.999 T (the host
+// enables the path only when -0.999 T / lamG < -17.5, so e1 rounds away exactly as it does for
+// the reference's 707.1068), and popc + icd >= icd
+// picks LUT entry icd (the LUT holds 2 - expf(-C / lamCen) and is clamped at icd, so no min
+// is needed either).  The exponential's input is clamped at -100 instead of selecting 0 below
+// -17.5: expf_glibc_core is exact down to -103.9, and every value below 2^-25 leaves
+// fl(t - e) == t (see above).  Saves the range test, three selects and a min per element.
+constexpr int LUT_T_N = 260;   // >= 128 census bits + icd (<= 128) + 1
+
 template <int METHOD, bool LAM1, int CW, bool ONE, bool OORZ>
 __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     extern __shared__ __align__(16) unsigned char cs_raw[];
     constexpr int RW = cost_rec_u4<CW>();
     constexpr int COST_P = cost_p(ONE);
+    constexpr bool NOSEL = METHOD == SM_M_CENSUS_GRAD && OORZ && CW >= 3;
     const int D = a.D, W = a.W, H = a.H;
     const int nbx = (W + COST_P - 1) / COST_P;
     const int blk = xcd_swizzle(blockIdx.x, gridDim.x);  // neighbouring segments share an XCD's L2
@@ -292,8 +305,12 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     float* luta = (float*)(fbgr + COST_P);                       // [LUT_A_N]
     float* lutb = luta + LUT_A_N;                                // [LUT_B_N]
     const int tid = threadIdx.y * 64 + threadIdx.x;
+    const float cd = a.census_default;
+    const int icd = (int)cd;                        // (int)fminf(pc, cd) == min(pc, (int)cd) for integer pc >= 0
     if (GRAD && tid < 32) etab[tid] = c_exp_tab[tid];
-    if (CEN)
+    if (NOSEL)   // luta's region (LUT_A_N + LUT_B_N floats) holds the clamped 2 - e0 table
+        for (int i = tid; i < LUT_T_N; i += 256) luta[i] = 2.0f - c_lut_a[min(i, icd)];
+    else if (CEN)
         for (int i = tid; i < LUT_A_N; i += 256) luta[i] = c_lut_a[i];
     if (METHOD == SM_M_AD_CENSUS)
         for (int i = tid; i < LUT_B_N; i += 256) lutb[i] = c_lut_b[i];
@@ -325,7 +342,7 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     for (int i = tid; i < nm; i += 256) {
         const int q = mbase + i;
         ulonglong2 c = make_ulonglong2(0, 0);
-        uint32_t w2 = 0, w3 = 0;
+        uint32_t w2 = 0, w3 = 0, bias = 0;
         if (q >= 0 && q < W) {
             if (CEN) c = a.code[mrow + q];
             if (GRAD) {
@@ -336,13 +353,16 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 const uint8_t* p = a.bgr + (mrow + q) * 3;
                 w2 = p[0] | (p[1] << 8) | (p[2] << 16);
             }
+        } else if (NOSEL) {   // out-of-range candidate: see NOSEL above
+            w2 = w3 = __float_as_uint(1e30f);
+            bias = (uint32_t)icd;
         }
         if (CW == 4) {
             mrec[2 * i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, (uint32_t)(c.y >> 32));
-            mrec[2 * i + 1] = make_uint4(w2, w3, 0, 0);
+            mrec[2 * i + 1] = make_uint4(w2, w3, bias, 0);
         } else if (CW == 3) {
             mrec[2 * i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, w2);
-            mrec[2 * i + 1] = make_uint4(w3, 0, 0, 0);
+            mrec[2 * i + 1] = make_uint4(w3, bias, 0, 0);
         } else {
             mrec[i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), w2, w3);
         }
@@ -350,12 +370,12 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     __syncthreads();
     const int lane = threadIdx.x;
     if (ONE && lane >= D) return;                   // D <= 64: one disparity per lane; no barrier follows
-    const float cd = a.census_default;
-    const int icd = (int)cd;                        // (int)fminf(pc, cd) == min(pc, (int)cd) for integer pc >= 0
     const float* out = a.vm + ((size_t)b * npix + (size_t)v * W + u0) * D;
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out, np * D * 4);
+    // the wave's pixel index is uniform: loop control and the store's pixel offset stay scalar
+    const int wy = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
 #pragma unroll SM_COST_UNROLL
-    for (int pl = threadIdx.y; pl < np; pl += 4) {
+    for (int pl = wy; pl < np; pl += 4) {
         const int u = u0 + pl;
         const ulonglong2 cf = CEN ? fcode[pl] : make_ulonglong2(0, 0);
         float fx = 0.f, fy = 0.f, wa = 0.f, wb = 0.f;
@@ -368,8 +388,40 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
         }
         if (ADM) fc = fbgr[pl];
         auto elem = [&](int d, int q) {                // q = u - sgn * d, the moving position
-            const bool oor = (unsigned)q >= (unsigned)W;
             const int mi = q - mbase;                  // staged record (zeros when out of range)
+            if constexpr (NOSEL) {
+                const uint4 r0 = mrec[RW * mi];
+                uint32_t pc, gxm, gym;
+                if constexpr (CW == 3) {
+                    const uint2 r1 = *(const uint2*)&mrec[RW * mi + 1];
+                    pc = r1.y;                         // icd for out-of-range candidates, else 0
+                    gxm = r0.w;
+                    gym = r1.x;
+                } else {
+                    const uint4 r1 = mrec[RW * mi + 1];
+                    pc = r1.z;
+                    gxm = r1.x;
+                    gym = r1.y;
+                }
+                pc += __popc((uint32_t)cf.x ^ r0.x);
+                pc += __popc((uint32_t)(cf.x >> 32) ^ r0.y);
+                pc += __popc((uint32_t)cf.y ^ r0.z);
+                if (CW == 4) pc += __popc((uint32_t)(cf.y >> 32) ^ r0.w);
+                asm volatile("" : "+v"(pc));   // a v_bcnt accumulate chain, not a sum of scaled counts
+                const float dx = fminf(fabsf(fx - __uint_as_float(gxm)), a.grad_trunc);
+                const float dy = fminf(fabsf(fy - __uint_as_float(gym)), a.grad_trunc);
+                const float t1 = wa * dx;
+                const float t2 = wb * dy;
+                const float g = t1 + t2;
+                const float xg = LAM1 ? -g : -g / a.lam2;
+                const float t = luta[pc];                       // fl(2 - expf(-min(pc, icd) / lamCen))
+                const float ex = expf_glibc_core(fmaxf(xg, -100.0f), etab);
+                const float res = t - ex;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, d * 4, pl * D * 4,
+                                                      SM_COST_STORE_AUX);
+                return;
+            }
+            const bool oor = (unsigned)q >= (unsigned)W;
             const uint4 r0 = mrec[RW * mi];
             uint32_t w2 = r0.z, w3 = r0.w;
             uint32_t pc = 0;
@@ -425,7 +477,7 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
 #if SM_COST_PROBE == 2
             res = (float)d;                              // timing probe: stores only
 #endif
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, (int)((pl * D + d) * 4), 0,
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, d * 4, pl * D * 4,
                                                   SM_COST_STORE_AUX);
         };
         if (ONE) {
@@ -520,11 +572,15 @@ static void launch_cost_z(const CostArgs& a, dim3 grid, dim3 block, size_t shm, 
 
 template <int METHOD, bool LAM1, int CW>
 static void launch_cost_nw(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
-    // the kernel's own expression for an out-of-range pair: xg = -G (lamG == 1) or -G / lamG
-    const float g = a.grad_oor;
-    const float xg = LAM1 ? -g : -g / a.lam2;
-    if constexpr (METHOD == SM_M_CENSUS_GRAD) {
-        if (xg < -17.5f) return launch_cost_z<METHOD, LAM1, CW, true>(a, grid, block, shm, st);
+    // select-free elements (NOSEL in k_cost): an out-of-range pair's G is fl(wa T) + fl(wb T)
+    // >= 0.999 T there (T = grad_trunc, wa + fl(1 - wa) = 1 up to 2^-24), and its exponential
+    // must still round away: xg = -G (lamG == 1) or -G / lamG below -17.5; the clamped
+    // 2 - e0 table covers counts up to 128 + icd
+    const float gmin = 0.999f * a.grad_trunc;
+    const float xg = LAM1 ? -gmin : -gmin / a.lam2;
+    if constexpr (METHOD == SM_M_CENSUS_GRAD && CW >= 3) {
+        if (xg < -17.5f && a.grad_trunc < 1e29f && (int)a.census_default <= 128 && (int)a.census_default >= 0)
+            return launch_cost_z<METHOD, LAM1, CW, true>(a, grid, block, shm, st);
     }
     launch_cost_z<METHOD, LAM1, CW, false>(a, grid, block, shm, st);
 }

@@ -103,6 +103,33 @@ def test_census_windows(oracle, rv, ru, ring, cost, md):
         lib.sm_destroy(ctx)
 
 
+@pytest.mark.parametrize("lam_g,trunc,adaptive,md", [(1.0, 500.0, 1, 23), (20.0, 500.0, 1, 23), (28.0, 500.0, 0, 70),
+                                                     (30.0, 500.0, 1, 23), (60.0, 500.0, 1, 70), (1.0, 10.0, 1, 23),
+                                                     (1.0, 20.0, 0, 99), (0.5, 3.0, 1, 23)])
+def test_grad_cost_constants(oracle, lam_g, trunc, adaptive, md):
+    """censusGrad cost volume of both views under lamG / gradient truncation / weighting choices
+    on either side of the select-free kernel's bound (-0.999 T / lamG < -17.5, k_cost NOSEL)."""
+    H, W = 19, 88
+    pair = S.make_pair(H, W, md + 1, 90 + md)
+    cfg = oracle.config(H, W, md, lam_g=lam_g, grad_trunc=trunc, grad_adaptive=adaptive)
+    lib = _capi.load()
+    p = _capi.default_params(md, H, W, aggregation=0, optimization=0, compute_right_view=1)
+    p.lam_g, p.grad_trunc, p.grad_adaptive = lam_g, trunc, adaptive
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        a = {k: np.ascontiguousarray(pair[k]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        _capi.check(lib, ctx, lib.sm_set_images(ctx, _capi.ptr(a["lbgr"]), _capi.ptr(a["rbgr"]), W * 3,
+                                                _capi.ptr(a["lgray"]), _capi.ptr(a["rgray"]), W))
+        _capi.check(lib, ctx, lib.sm_cost_calculate(ctx))
+        for view in (0, 1):
+            got = np.empty((H, W, md + 1), np.float32)
+            _capi.check(lib, ctx, lib.sm_get_volume(ctx, view, _capi.ptr(got)))
+            np.testing.assert_array_equal(bits(got), bits(oracle.cost_volume(pair, cfg, view=view)))
+    finally:
+        lib.sm_destroy(ctx)
+
+
 def test_right_view_volume(oracle):
     H, W, md = 33, 52, 19
     pair = S.make_pair(H, W, md + 1, 12)

@@ -58,7 +58,7 @@ struct sm_ctx {
     uint8_t* flags1 = nullptr;  // [cap][npix] same for the right image (do_refine)
     uint8_t* so_trace = nullptr;   // [cap][npix][D] "so" choice codes
     uint16_t* so_cidx = nullptr;   // [cap][npix] "so" row-minimum indices
-    uint32_t* px = nullptr;     // [cap][2][npix] packed BGR
+    uint32_t* px = nullptr;     // [cap][2][npix] packed BGR, then the pxh and pxv arm-walk planes (same shape)
     int n_loaded = 0;
     int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized, 5 refined
     float lut_a[1024], lut_b[1024];
@@ -246,6 +246,8 @@ struct Bufs {
     uint8_t* flags;
     uint8_t* flags1;
     uint32_t* px;
+    uint32_t* pxh;
+    uint32_t* pxv;
 };
 
 Bufs at(const sm_ctx* c, int off) {
@@ -266,6 +268,8 @@ Bufs at(const sm_ctx* c, int off) {
     b.flags = c->flags + o * np;
     b.flags1 = c->flags1 ? c->flags1 + o * np : nullptr;
     b.px = c->px + o * 2 * np;
+    b.pxh = c->px + (c->cap + o) * 2 * np;
+    b.pxv = c->px + (2 * c->cap + o) * 2 * np;
     return b;
 }
 
@@ -279,6 +283,8 @@ sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
         a.gray = B.gray;
         a.bgr = B.bgr;
         a.px = B.px;
+        a.pxh = B.pxh;
+        a.pxv = B.pxv;
         a.code = B.code;
         a.gx = B.gx;
         a.gy = B.gy;
@@ -626,7 +632,7 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->disp1, cap * c->npix))) return s;
         if ((s = dalloc(c, &c->disp_tmp, cap * c->npix))) return s;
     }
-    if ((s = dalloc(c, &c->px, cap * 2 * c->npix))) return s;
+    if ((s = dalloc(c, &c->px, 3 * cap * 2 * c->npix))) return s;
     build_luts(c);
     {
         const char* e = getenv("SM_FUSE_NORM_SCAN");

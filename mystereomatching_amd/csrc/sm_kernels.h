@@ -15,6 +15,8 @@ struct PrepArgs {
     const uint8_t* gray;        // [n][2][H][W]
     const uint8_t* bgr;         // [n][2][H][W][3]
     uint32_t* px;               // [n][2][H][W] packed BGR (written by the pack pass)
+    uint32_t* pxh;              // [n][2][H][W] arm-walk words, horizontal flags (k_pack_arms)
+    uint32_t* pxv;              // [n][2][H][W] arm-walk words, vertical flags
     ulonglong2* code;           // [n][2][H][W]
     float* gx;
     float* gy;

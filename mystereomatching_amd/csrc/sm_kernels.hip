@@ -26,11 +26,13 @@ __constant__ float c_lut_b[1024];
 __device__ inline float dev_expf(float x) { return expf_glibc(x, c_exp_tab); }
 
 // ---------------------------------------------------------------------------------------
-// K0: fused per-pixel prep for one view: census code, x/y gradients, cross arms and (left view)
-// the SGM colour-difference penalty flags, from LDS tiles.  Block = 64 x 16 pixels, 256 threads
-// (4 pixels each).  Gray tile with the census halo (REFLECT_101 applied while filling it, as
-// copyMakeBorder does, h:870-871); packed-BGR tile with an L_out halo for the arm walks
-// (out-of-image tile entries are never read: the walk stops at the border first).
+// K0: per-pixel prep of both views: k_pack_bgr (packed BGR), k_pack_arms (arm-walk words and
+// the SGM colour-difference penalty flags), then k_prep: census code, x/y gradients and cross
+// arms from LDS tiles.  Block = 64 x 16 pixels, 256 threads (4 pixels each).  Gray tile with
+// the census halo (REFLECT_101 applied while filling it, as copyMakeBorder does, h:870-871);
+// arm-walk strips with an L_out halo along each axis (Teddy x16: 0.261 -> 0.259 ms for the
+// three kernels; census unrolled for the default window and LDS walks each took ~20 % off
+// their share, the strip fills gave most of it back).
 // ---------------------------------------------------------------------------------------
 constexpr int PREP_TX = 64, PREP_TY = 16;
 
@@ -51,12 +53,89 @@ __global__ void k_pack_bgr(const uint8_t* __restrict__ bgr, uint32_t* __restrict
     }
 }
 
+// Arm-walk words (calHorVerDis, cpp:2959-3050).  A walk step compares the step pixel with the
+// centre under threshold t and with the previous step pixel under C_D.  k_pack_arms writes two
+// planes whose words hold the pixel in 10-bit fields (B | G << 10 | R << 20) and the C_D test
+// against the walk's previous pixel, precomputed once per pixel and axis:
+//   pxh bit 30: (p, p + 1) within C_D (an L walk reaches p from p + 1), bit 31: (p, p - 1) (R walk)
+//   pxv bit 30: (p, p + W) (U walk), bit 31: (p, p - W) (D walk); 0 where the partner is outside.
+// The centre test is one guard-bit subtraction for all three channels: with M = 1 | 1 << 10 |
+// 1 << 20, A = C + (512 + t) M - P and B = C + (511 - t) M - P keep every field in [1, 1022]
+// for -1 <= t <= 255 (no borrow crosses a field; the flag bits only borrow upwards), and
+// bit 9 of A's field c is set iff C_c - P_c >= -t, bit 9 of B's field clear iff C_c - P_c <= t.
+// So a step passes iff ((A & ~B) & B9) | (P & flag) == B9 | flag — words outside the image are
+// 0 and fail on the flag, which replaces the reference's border test.
+constexpr uint32_t ARM_M = 1u | (1u << 10) | (1u << 20);
+constexpr uint32_t ARM_B9 = ARM_M << 9;
+
+__device__ __forceinline__ uint32_t pack10(uint32_t p) {   // B | G << 8 | R << 16 -> 10-bit fields
+    return (p & 0xffu) | ((p & 0xff00u) << 2) | ((p & 0xff0000u) << 4);
+}
+
+// One thread per pixel (grid x: 256-pixel row segments, y: rows, z: images).  Also writes the
+// SGM colour-difference penalty flags (updateCost, h:2223-2229): bit i set when the neighbour
+// towards direction i (rv/ru tables of sgm, cpp:6207-6208) is inside and its max-channel
+// difference exceeds sgm_corDifThres — of the left image, and of the right image when vm[1] is
+// optimised too (leftFirst = false compares I_c[1], h:2224).
+__global__ __launch_bounds__(256) void k_pack_arms(const PrepArgs a, int arms) {
+    const int H = a.H, W = a.W;
+    const int u = blockIdx.x * 256 + threadIdx.x, v = blockIdx.y;
+    if (u >= W) return;
+    const size_t npix = (size_t)H * W;
+    const int img = blockIdx.z, b = img >> 1, view = img & 1;
+    const size_t i = (size_t)img * npix + (size_t)v * W + u;
+    const uint32_t* pc = a.px + i;
+    const uint32_t c = pc[0];
+    const bool inL = u > 0, inR = u + 1 < W, inU = v > 0, inD = v + 1 < H;
+    const uint32_t pl = inL ? pc[-1] : c, pr = inR ? pc[1] : c, pu = inU ? pc[-W] : c, pd = inD ? pc[W] : c;
+    if (arms) {
+        const uint32_t f = pack10(c);
+        uint32_t h = f, vv = f;
+        if (inR && color_ok_packed(c, pr, a.C_D)) h |= 1u << 30;
+        if (inL && color_ok_packed(c, pl, a.C_D)) h |= 1u << 31;
+        if (inD && color_ok_packed(c, pd, a.C_D)) vv |= 1u << 30;
+        if (inU && color_ok_packed(c, pu, a.C_D)) vv |= 1u << 31;
+        a.pxh[i] = h;
+        a.pxv[i] = vv;
+    }
+    if (a.do_flags && (view == 0 || a.flags1)) {
+        const int t = a.cor_thres;
+        uint32_t fl = 0;
+        // directions 0..7: (rv, ru) = (+1,0) (-1,0) (0,+1) (0,-1) (+1,-1) (+1,+1) (-1,+1) (-1,-1)
+        if (inD && color_d1(c, pd) > t) fl |= 1u;
+        if (inU && color_d1(c, pu) > t) fl |= 2u;
+        if (inR && color_d1(c, pr) > t) fl |= 4u;
+        if (inL && color_d1(c, pl) > t) fl |= 8u;
+        if (inD && inL && color_d1(c, pc[W - 1]) > t) fl |= 16u;
+        if (inD && inR && color_d1(c, pc[W + 1]) > t) fl |= 32u;
+        if (inU && inR && color_d1(c, pc[1 - W]) > t) fl |= 64u;
+        if (inU && inL && color_d1(c, pc[-1 - W]) > t) fl |= 128u;
+        (view == 0 ? a.flags : a.flags1)[(size_t)b * npix + (size_t)v * W + u] = (uint8_t)fl;
+    }
+}
+
+// prep LDS: gray tile (census/gradient halo), then the arm strips (STRIPS): hs = the tile's 16
+// rows over columns u0 - Lo .. u0 + 63 + Lo, vs = its 64 columns over rows v0 - Lo .. v0 + 15 + Lo
+__host__ __device__ inline int prep_gray_bytes(int rv, int ru) {
+    const int hv = rv > 1 ? rv : 1, hu = ru > 1 ? ru : 1;
+    return ((PREP_TX + 2 * hu) * (PREP_TY + 2 * hv) + 15) / 16 * 16;
+}
+__host__ __device__ inline int prep_strip_words(int Lo) {
+    return PREP_TY * (PREP_TX + 2 * Lo) + (PREP_TY + 2 * Lo) * PREP_TX;
+}
+
 #ifndef SM_PREP_PROBE
 #define SM_PREP_PROBE 0   // timing probes: 1 = no arms, 2 = no census (results wrong)
 #endif
+// TRV/TRU/TRING >= 0: census geometry fixed at compile time (the default 7 x 9 window with the
+// ring bits), so the bit loop unrolls into straight-line compares with immediate LDS offsets;
+// -1: the runtime geometry.  STRIPS: arm walks over the LDS strips (else over global memory).
+template <int TRV, int TRU, int TRING, bool STRIPS>
 __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
     extern __shared__ __align__(16) unsigned char prep_raw[];
-    const int H = a.H, W = a.W, rv = a.rv, ru = a.ru, Lo = a.L_out;
+    const int H = a.H, W = a.W, Lo = a.L_out;
+    const int rv = TRV >= 0 ? TRV : a.rv, ru = TRU >= 0 ? TRU : a.ru;
+    const int ring = TRING >= 0 ? TRING : a.ring;
     const int u0 = blockIdx.x * PREP_TX, v0 = blockIdx.y * PREP_TY;
     const int b = blockIdx.z >> 1, view = blockIdx.z & 1;
     const size_t npix = (size_t)H * W;
@@ -75,6 +154,24 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
             gt[i] = G[(size_t)vv * W + uu];
         }
     }
+    const int hsw = PREP_TX + 2 * Lo;
+    uint32_t* hs = (uint32_t*)(prep_raw + prep_gray_bytes(rv, ru));
+    uint32_t* vs = hs + PREP_TY * hsw;
+    if (STRIPS && a.do_arms) {
+        const uint32_t* PH = a.pxh + img * npix;
+        const uint32_t* PV = a.pxv + img * npix;
+        for (int r = 0; r < PREP_TY; r++) {
+            const int vv = v0 + r;
+            for (int xx = tid; xx < hsw; xx += 256) {
+                const int uu = u0 - Lo + xx;
+                hs[r * hsw + xx] = (vv < H && (unsigned)uu < (unsigned)W) ? PH[(size_t)vv * W + uu] : 0u;
+            }
+        }
+        for (int i = tid; i < (PREP_TY + 2 * Lo) * PREP_TX; i += 256) {
+            const int vv = v0 - Lo + (i >> 6), uu = u0 + (i & 63);
+            vs[i] = ((unsigned)vv < (unsigned)H && uu < W) ? PV[(size_t)vv * W + uu] : 0u;
+        }
+    }
     __syncthreads();
     const int x = tid & 63;
     for (int yy = tid >> 6; yy < PREP_TY; yy += 4) {
@@ -88,7 +185,9 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
             uint64_t w[2] = {0, 0};
             uint64_t cs = 0;
             int step = 0, dep = 0;
+#pragma unroll
             for (int dv = -rv; dv <= rv; dv++)
+#pragma unroll
                 for (int du = -ru; du <= ru; du++) {
                     if (step > 63) {
                         w[dep & 1] = cs;
@@ -100,7 +199,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
                     if (c - (int)g[dv * gw + du] < 0) cs++;
                     step++;
                 }
-            if (a.ring) {
+            if (ring) {
                 const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
                 const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
 #pragma unroll
@@ -146,21 +245,44 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         if (a.do_arms && SM_PREP_PROBE != 1) {
             const uint32_t center = pc[0];
             uint32_t packed = 0;
+            // strip walks: centre words and the two thresholds' guard-bit operands
+            const uint32_t* hc = hs + yy * hsw + (x + Lo);
+            const uint32_t* vc = vs + (yy + Lo) * PREP_TX + x;
+            const uint32_t cf = pack10(center);
+            const int t1 = min(max(a.C_D, -1), 255), t2 = min(max(a.C_D_out, -1), 255);
+            const uint32_t ca1 = cf + (uint32_t)(512 + t1) * ARM_M, cb1 = cf + (uint32_t)(511 - t1) * ARM_M;
+            const uint32_t ca2 = cf + (uint32_t)(512 + t2) * ARM_M, cb2 = cf + (uint32_t)(511 - t2) * ARM_M;
+            const int Lin = min(a.L, Lo);
 #pragma unroll
             for (int direc = 0; direc < 4; direc++) {
                 const int du = direc == 0 ? -1 : (direc == 1 ? 1 : 0);
                 const int dv = direc == 2 ? -1 : (direc == 3 ? 1 : 0);
-                const int off = dv * W + du;
                 int arm = 1;
-                uint32_t prev = center;
-                for (; arm <= Lo; arm++) {
-                    const int va = v + arm * dv, ua = u + arm * du;
-                    if (va < 0 || va >= H || ua < 0 || ua >= W) break;
-                    const uint32_t cur = pc[arm * off];
-                    const bool nb = color_ok_packed(cur, prev, a.C_D);
-                    const bool ip = color_ok_packed(center, cur, arm <= a.L ? a.C_D : a.C_D_out);
-                    if (!nb || !ip) break;
-                    prev = cur;
+                if (STRIPS) {
+                    const uint32_t* sp = direc < 2 ? hc : vc;
+                    const int sst = direc == 0 ? -1 : (direc == 1 ? 1 : (direc == 2 ? -PREP_TX : PREP_TX));
+                    const uint32_t fb = (direc == 0 || direc == 2) ? (1u << 30) : (1u << 31);
+                    const uint32_t want = ARM_B9 | fb;
+                    auto pass = [&](uint32_t p, uint32_t ca, uint32_t cb) {
+                        return ((((ca - p) & ~(cb - p)) & ARM_B9) | (p & fb)) == want;
+                    };
+                    for (; arm <= Lin; arm++)
+                        if (!pass(sp[arm * sst], ca1, cb1)) break;
+                    if (arm > Lin)
+                        for (; arm <= Lo; arm++)
+                            if (!pass(sp[arm * sst], ca2, cb2)) break;
+                } else {
+                    const int off = dv * W + du;
+                    uint32_t prev = center;
+                    for (; arm <= Lo; arm++) {
+                        const int va = v + arm * dv, ua = u + arm * du;
+                        if (va < 0 || va >= H || ua < 0 || ua >= W) break;
+                        const uint32_t cur = pc[arm * off];
+                        const bool nb = color_ok_packed(cur, prev, a.C_D);
+                        const bool ip = color_ok_packed(center, cur, arm <= a.L ? a.C_D : a.C_D_out);
+                        if (!nb || !ip) break;
+                        prev = cur;
+                    }
                 }
                 int outv = 0;
                 if (--arm >= a.minL)
@@ -179,28 +301,23 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
             planes[0] = (packed & 0xffu) | ((packed >> 8 & 0xffu) << 16);
             planes[npix] = (packed >> 16 & 0xffu) | ((packed >> 24) << 16);
         }
-        // SGM penalty flags of the left image (updateCost, h:2223-2229), and of the right image
-        // when vm[1] is optimised too (leftFirst = false compares I_c[1], h:2224)
-        if (a.do_flags && (view == 0 || a.flags1)) {
-            const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};
-            const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};
-            const uint32_t c0 = pc[0];
-            uint32_t f = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const int vv = v + RV[i], uu = u + RU[i];
-                if (vv < 0 || vv >= H || uu < 0 || uu >= W) continue;
-                if (color_d1(c0, pc[RV[i] * W + RU[i]]) > a.cor_thres) f |= 1u << i;
-            }
-            (view == 0 ? a.flags : a.flags1)[(size_t)b * npix + (size_t)v * W + u] = (uint8_t)f;
-        }
     }
 }
 
+// strip walks when the strips fit comfortably: L_out <= 64 is <= 49 KB of LDS per block (the
+// default 34 takes 30 KB: five blocks per CU); longer arms walk global memory
+static bool prep_strips(int L_out) { return L_out >= 0 && L_out <= 64; }
+
 size_t prep_smem_bytes(int rv, int ru, int L_out) {
-    const int hv = rv > 1 ? rv : 1, hu = ru > 1 ? ru : 1;
-    (void)L_out;
-    return (size_t)(PREP_TX + 2 * hu) * (PREP_TY + 2 * hv);
+    return (size_t)prep_gray_bytes(rv, ru) + (prep_strips(L_out) ? 4 * (size_t)prep_strip_words(L_out) : 0);
+}
+
+template <int TRV, int TRU, int TRING>
+static void launch_prep_g(const PrepArgs& a, dim3 grid, size_t shm, bool strips, hipStream_t st) {
+    if (strips)
+        hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, true>), grid, dim3(256), shm, st, a);
+    else
+        hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, false>), grid, dim3(256), shm, st, a);
 }
 
 void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
@@ -208,8 +325,15 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
     size_t blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(k_pack_bgr, dim3((unsigned)blocks), dim3(256), 0, st, a.bgr, a.px, total);
+    const bool strips = a.do_arms && prep_strips(a.L_out);
+    if (strips || a.do_flags)   // arm-walk planes and the SGM penalty flags
+        hipLaunchKernelGGL(k_pack_arms, dim3((a.W + 255) / 256, a.H, 2 * n), dim3(256), 0, st, a, (int)strips);
     dim3 grid((a.W + PREP_TX - 1) / PREP_TX, (a.H + PREP_TY - 1) / PREP_TY, 2 * n);
-    hipLaunchKernelGGL(k_prep, grid, dim3(256), prep_smem_bytes(a.rv, a.ru, a.L_out), st, a);
+    const size_t shm = (size_t)prep_gray_bytes(a.rv, a.ru) + (strips ? 4 * (size_t)prep_strip_words(a.L_out) : 0);
+    if (a.rv == 3 && a.ru == 4 && a.ring == 1)   // the reference's default census window (cpp:815)
+        launch_prep_g<3, 4, 1>(a, grid, shm, strips, st);
+    else
+        launch_prep_g<-1, -1, -1>(a, grid, shm, strips, st);
 }
 
 // ---------------------------------------------------------------------------------------

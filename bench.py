@@ -66,12 +66,20 @@ def main():
     args = parse()
     world, rank, local = dist_setup(args.gpus)
     import torch
+    # SM_BENCH_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs than ranks
+    # (ranks share devices round-robin; the driver's runs use RCCL, one rank per GPU)
+    backend = os.environ.get("SM_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from mystereomatching_amd import StereoBatch
     from mystereomatching_amd import synthetic as S
@@ -96,10 +104,6 @@ def main():
     for _ in range(args.warmup):
         sb.run(0.3, download=False)
     sb.synchronize()
-    profile = not args.no_profile
-    if profile:
-        sb.profile(True)
-        sb.profile_reset()
 
     barrier()
     torch.cuda.synchronize()
@@ -113,12 +117,26 @@ def main():
     barrier()
     elapsed = t1 - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kernels = sb.profile_read() if profile else {}
-    sb.profile(False)
+    # Per-kernel durations: the same K steps again with a HIP event pair around every kernel on
+    # the context stream.  Kept out of the throughput timing above: each event record is a
+    # barrier packet on the queue (~0.14 ms per Teddy x16 step), which perturbs the step time
+    # but not the kernels' own durations.
+    profile = not args.no_profile
+    kernels, ms_prof = {}, None
+    if profile:
+        sb.profile(True)
+        sb.profile_reset()
+        tp = time.perf_counter()
+        for _ in range(args.steps):
+            sb.run(0.3, download=False)
+        sb.synchronize()
+        ms_prof = (time.perf_counter() - tp) / args.steps * 1e3
+        kernels = sb.profile_read()
+        sb.profile(False)
     disp = sb.download()
     bad2 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 2.0)[0] for i in range(B)]))
     bad1 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 1.0)[0] for i in range(B)]))
@@ -179,6 +197,7 @@ def main():
                        "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
             "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kern_out,
+            "ms_per_step_instrumented": None if ms_prof is None else round(ms_prof, 4),
         }
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sm_device.h"
 #include "sm_kernels.h"
 
@@ -30,9 +32,9 @@ __device__ inline float dev_expf(float x) { return expf_glibc(x, c_exp_tab); }
 // the SGM colour-difference penalty flags), then k_prep: census code, x/y gradients and cross
 // arms from LDS tiles.  Block = 64 x 16 pixels, 256 threads (4 pixels each).  Gray tile with
 // the census halo (REFLECT_101 applied while filling it, as copyMakeBorder does, h:870-871);
-// arm-walk strips with an L_out halo along each axis (Teddy x16: 0.261 -> 0.259 ms for the
-// three kernels; census unrolled for the default window and LDS walks each took ~20 % off
-// their share, the strip fills gave most of it back).
+// arm-walk strips with an L_out halo along each axis.  Teddy x16, rocprof, same box: 0.261 ->
+// 0.229 ms for the three kernels (census unrolled for the default window, LDS walks, tile
+// fills with 8 loads in flight per thread).
 // ---------------------------------------------------------------------------------------
 constexpr int PREP_TX = 64, PREP_TY = 16;
 
@@ -147,30 +149,44 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
     const int gw = PREP_TX + 2 * hu, gh = PREP_TY + 2 * hv;
     uint8_t* gt = prep_raw;
     const int tid = threadIdx.x;
-    if (a.do_census || a.do_grad) {
-        for (int i = tid; i < gw * gh; i += 256) {
+    // Tile fills: the loads of FB entries per thread are issued before any of them is stored, so a
+    // block waits on global-memory latency a few times instead of once per entry.
+    constexpr int FB = 8;
+    auto fill = [&](auto* dst, int count, auto&& load) {
+        for (int i0 = 0; i0 < count; i0 += FB * 256) {
+            uint32_t r[FB];
+#pragma unroll
+            for (int k = 0; k < FB; k++) {
+                const int i = i0 + k * 256 + tid;
+                r[k] = i < count ? load(i) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < FB; k++) {
+                const int i = i0 + k * 256 + tid;
+                if (i < count) dst[i] = (std::remove_reference_t<decltype(dst[0])>)r[k];
+            }
+        }
+    };
+    if (a.do_census || a.do_grad)
+        fill(gt, gw * gh, [&](int i) -> uint32_t {
             const int ty = i / gw, tx = i - ty * gw;
             const int vv = reflect101(v0 - hv + ty, H), uu = reflect101(u0 - hu + tx, W);
-            gt[i] = G[(size_t)vv * W + uu];
-        }
-    }
+            return G[(size_t)vv * W + uu];
+        });
     const int hsw = PREP_TX + 2 * Lo;
     uint32_t* hs = (uint32_t*)(prep_raw + prep_gray_bytes(rv, ru));
     uint32_t* vs = hs + PREP_TY * hsw;
     if (STRIPS && a.do_arms) {
         const uint32_t* PH = a.pxh + img * npix;
         const uint32_t* PV = a.pxv + img * npix;
-        for (int r = 0; r < PREP_TY; r++) {
-            const int vv = v0 + r;
-            for (int xx = tid; xx < hsw; xx += 256) {
-                const int uu = u0 - Lo + xx;
-                hs[r * hsw + xx] = (vv < H && (unsigned)uu < (unsigned)W) ? PH[(size_t)vv * W + uu] : 0u;
-            }
-        }
-        for (int i = tid; i < (PREP_TY + 2 * Lo) * PREP_TX; i += 256) {
+        fill(hs, PREP_TY * hsw, [&](int i) -> uint32_t {
+            const int r = i / hsw, vv = v0 + r, uu = u0 - Lo + (i - r * hsw);
+            return (vv < H && (unsigned)uu < (unsigned)W) ? PH[(size_t)vv * W + uu] : 0u;
+        });
+        fill(vs, (PREP_TY + 2 * Lo) * PREP_TX, [&](int i) -> uint32_t {
             const int vv = v0 - Lo + (i >> 6), uu = u0 + (i & 63);
-            vs[i] = ((unsigned)vv < (unsigned)H && uu < W) ? PV[(size_t)vv * W + uu] : 0u;
-        }
+            return ((unsigned)vv < (unsigned)H && uu < W) ? PV[(size_t)vv * W + uu] : 0u;
+        });
     }
     __syncthreads();
     const int x = tid & 63;

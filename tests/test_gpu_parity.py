@@ -164,6 +164,26 @@ def test_census_and_arms(oracle):
         np.testing.assert_array_equal(sm.HVL[view], oracle.arms(pair[c], cfg))
 
 
+@pytest.mark.parametrize("L,L_out,cT,cT_out,minL", [(17, 34, 20, 6, 1), (5, 10, 12, 30, 2), (40, 80, 20, 6, 1),
+                                                     (17, 64, 0, 255, 0), (0, 3, -1, 300, 1)])
+def test_arm_parameters(oracle, L, L_out, cT, cT_out, minL):
+    """Cross arms under other calHorVerDis arguments (cpp:5371): LDS-strip walks (L_out <= 64) and
+    global-memory walks (L_out > 64), thresholds at the guard-bit test's ends, minL fallbacks."""
+    H, W, md = 70, 90, 15
+    pair = S.make_pair(H, W, md + 1, 33)
+    for k in ("lbgr", "rbgr"):   # mix flat and textured regions so both long and short arms occur
+        pair[k][: H // 2] = (pair[k][: H // 2] // 96 * 96).astype(np.uint8)
+    pair["lgray"], pair["rgray"] = S.bgr_to_gray(pair["lbgr"]), S.bgr_to_gray(pair["rbgr"])
+    cfg = oracle.config(H, W, md, arm_L=L, arm_L_out=L_out, arm_cT=cT, arm_cT_out=cT_out, arm_minL=minL)
+    sm = make_sm(pair, md, cbca_crossL=[L, 0, 0], cbca_crossL_out=[L_out, 0, 0], cbca_cTresh=[cT, 0, 0],
+                 cbca_cTresh_out=[cT_out, 0, 0], cbca_minArmL=minL)
+    sm.costCalculate()
+    for view, c in ((0, "lbgr"), (1, "rbgr")):
+        np.testing.assert_array_equal(sm.HVL[view], oracle.arms(pair[c], cfg))
+    ref = oracle.run(pair, cfg, dumps=True)
+    np.testing.assert_array_equal(bits(sm.vm[0]), bits(ref["agg"]))
+
+
 @pytest.mark.parametrize("H,W,md,paths", [(2, 2, 0, 4), (3, 70, 63, 4), (70, 3, 5, 8), (17, 23, 64, 8),
                                           (25, 31, 127, 4), (13, 90, 191, 8), (9, 40, 255, 4),
                                           (11, 37, 199, 8), (7, 30, 130, 4)])

@@ -171,7 +171,8 @@ def main():
             avg = k["total_ms"] / k["launches"]
             gbs = k["bytes_per_launch"] / (avg * 1e-3) / 1e9
             kern_out[name] = {"avg_ms": round(avg, 4), "share": round(k["total_ms"] / tot, 4),
-                              "GB_s": round(gbs, 1), "bytes_per_launch": k["bytes_per_launch"]}
+                              "GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                              "bytes_per_launch": k["bytes_per_launch"]}
         # dominant kernel by total time, the right view's launches (suffix _r) counted with the
         # left view's kernel of the same name
         tot_by = {}

@@ -167,7 +167,13 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (p.sgm_paths < 1 || p.sgm_paths > 8) return bad("sgm_paths must be in [1, 8]");
     if (p.sgm_redu_coeff == 0) return bad("sgm_redu_coeff must be non-zero");
     if (p.batch_capacity < 1) return bad("batch_capacity must be >= 1");
-    if (p.lam_cen == 0 || p.lam_g == 0 || p.lam_ad == 0 || p.lam_cen_adc == 0) return bad("fusion lambdas must be non-zero");
+    // The kernels rely on every cost and path cost being >= +0 (SGM and WTA minima compare float
+    // bit patterns as unsigned integers, sm_device.h), which these constants guarantee: fusion
+    // terms 2 - exp(-C / lam) - exp(-G / lam) with C, G >= 0, truncations >= 0, P1, P2 >= 0.
+    if (!(p.lam_cen > 0) || !(p.lam_g > 0) || !(p.lam_ad > 0) || !(p.lam_cen_adc > 0))
+        return bad("fusion lambdas must be > 0");
+    if (!(p.grad_trunc >= 0) || !(p.ad_trunc_adc >= 0) || !(p.ad_trunc_ad >= 0)) return bad("truncations must be >= 0");
+    if (!(p.sgm_p1 >= 0) || !(p.sgm_p2 >= 0) || p.sgm_redu_coeff < 0) return bad("SGM penalties must be >= 0");
     if (p.do_refine) {
         if (!(p.rv_ratio > 0)) return bad("rv_ratio must be > 0");
         if (p.region_vote_nums < 0 || p.region_vote_nums > 64) return bad("region_vote_nums must be in [0, 64]");

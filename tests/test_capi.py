@@ -55,6 +55,8 @@ def test_params_struct_layout_and_defaults():
     ("rows", 1, b"rows"), ("num_disparities", 0, b"num_disparities"), ("num_disparities", 2000, b"num_disparities"),
     ("census_rv", 7, b"census"), ("arm_l_out", 200, b"arm"), ("sgm_paths", 9, b"sgm_paths"),
     ("batch_capacity", 0, b"batch"), ("cost_method", 7, b"cost_method"), ("lam_cen", 0.0, b"lambda"),
+    ("lam_g", -1.0, b"lambda"), ("grad_trunc", -5.0, b"truncation"), ("sgm_p2", -1.0, b"penalties"),
+    ("sgm_redu_coeff", -4, b"penalties"),
 ])
 def test_validation_rejects_before_device(field, value, msg):
     lib = _capi.load()

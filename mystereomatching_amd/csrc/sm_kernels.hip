@@ -127,7 +127,7 @@ __host__ __device__ inline int prep_strip_words(int Lo) {
 }
 
 #ifndef SM_PREP_PROBE
-#define SM_PREP_PROBE 0   // timing probes: 1 = no arms, 2 = no census (results wrong)
+#define SM_PREP_PROBE 0   // timing probes: 1 = no arms, 2 = no census, 3 = neither (results wrong)
 #endif
 // TRV/TRU/TRING >= 0: census geometry fixed at compile time (the default 7 x 9 window with the
 // ring bits), so the bit loop unrolls into straight-line compares with immediate LDS offsets;
@@ -195,7 +195,33 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         if (u >= W || v >= H) continue;
         const size_t o = img * npix + (size_t)v * W + u;
         // census (genCensusCode_NC_Sur, h:867-934)
-        if (a.do_census && SM_PREP_PROBE != 2) {
+        if (TRV >= 0 && a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
+            // compile-time geometry: every bit's position is a constant, so the bits go into four
+            // 32-bit accumulators (acc = 2 acc + bit: a compare and an add-with-carry per bit)
+            // instead of a 64-bit shift register; the words are then assembled exactly as the
+            // reference's 64-bit chunks (MSB first, a partial last chunk in the low bits)
+            const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
+            const int c = g[0];
+            uint32_t acc[4] = {0, 0, 0, 0};
+            int k = 0;
+#pragma unroll
+            for (int dv = -rv; dv <= rv; dv++)
+#pragma unroll
+                for (int du = -ru; du <= ru; du++, k++)
+                    acc[k >> 5] = acc[k >> 5] + acc[k >> 5] + (uint32_t)(c < (int)g[dv * gw + du]);
+            if (ring) {
+                const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
+                const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
+#pragma unroll
+                for (int i = 0; i < 8; i++, k++)
+                    acc[k >> 5] = acc[k >> 5] + acc[k >> 5] +
+                                  (uint32_t)((int)g[dvs[i] * gw + dus[i]] < (int)g[dvs[i + 1] * gw + dus[i + 1]]);
+            }
+            const int nb0 = k < 64 ? k : 64, nb1 = k - nb0;   // bits of chunk 0 and chunk 1
+            const uint64_t w0 = nb0 > 32 ? ((uint64_t)acc[0] << (nb0 - 32)) | acc[1] : acc[0];
+            const uint64_t w1 = nb1 > 32 ? ((uint64_t)acc[2] << (nb1 - 32)) | acc[3] : acc[2];
+            a.code[o] = make_ulonglong2(w0, w1);
+        } else if (a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
             const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
             const int c = g[0];
             uint64_t w[2] = {0, 0};
@@ -258,7 +284,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         const uint32_t* pc = P + (size_t)v * W + u;
         // cross arms (calHorVerDis 7-arg, cpp:2959-3050), direction order L, R, U, D; the walks
         // read the packed image (lanes = consecutive pixels, so every step is one coalesced load)
-        if (a.do_arms && SM_PREP_PROBE != 1) {
+        if (a.do_arms && SM_PREP_PROBE != 1 && SM_PREP_PROBE != 3) {
             const uint32_t center = pc[0];
             uint32_t packed = 0;
             // strip walks: centre words and the two thresholds' guard-bit operands

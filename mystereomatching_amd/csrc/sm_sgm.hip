@@ -39,6 +39,9 @@
 #ifndef SM_SGM_ROWS_T4
 #define SM_SGM_ROWS_T4 2
 #endif
+#ifndef SM_SGM_T_K1
+#define SM_SGM_T_K1 16
+#endif
 #ifndef SM_SGM_T_K3
 #define SM_SGM_T_K3 5
 #endif
@@ -519,7 +522,7 @@ static void launch_kf(const SgmArgs& a, int mode, int n, hipStream_t st) {
     const int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
     dim3 grid((nlines + 3) / 4, n);
     constexpr int T = VEC ? (K == 4 ? SM_SGM_T_V4 : SM_SGM_T_BIG)
-                          : (K >= 8 ? SM_SGM_T_BIG : (K == 3 ? SM_SGM_T_K3 : (K == 4 ? SM_SGM_T_K4 : 16 / K)));
+                          : (K >= 8 ? SM_SGM_T_BIG : (K == 3 ? SM_SGM_T_K3 : (K == 4 ? SM_SGM_T_K4 : (K == 1 ? SM_SGM_T_K1 : 16 / K))));
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
     switch (mode) {
         case SGM_FIRST: hipLaunchKernelGGL((k_sgm<K, SGM_FIRST, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;

@@ -22,11 +22,19 @@
 #include "sm_device.h"
 #include "sm_kernels.h"
 
+#ifndef SM_SO_LDS_TRACE
+#define SM_SO_LDS_TRACE 1
+#endif
+
 namespace sm {
 
 namespace {
 
 constexpr int SO_T = 8;   // columns per prefetch tile
+
+__host__ __device__ inline size_t so_lds_words(int W, int K) {   // per wave, in u64 words
+    return (size_t)W * 2 * K + ((size_t)W * 2 + 7) / 8;
+}
 
 __device__ __forceinline__ float shr1_f(float v) {   // lane l <- lane l - 1 (lane 0 <- FLT_MAX)
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp((int)0x7f7fffff, __builtin_bit_cast(int, v),
@@ -37,8 +45,14 @@ __device__ __forceinline__ float shl1_f(float v) {   // lane l <- lane l + 1 (la
                                                                  DPP_WAVE_SHL1, 0xF, 0xF, false));
 }
 
-template <int K>
+// LT (LDS trace): the choice codes of a row live in LDS as two ballot masks per column and
+// per lane slot j (bit l of mask 2j / 2j + 1 = bit 0 / 1 of the code of disparity l K + j), and
+// the row-minimum indices as u16; the backtrack's W dependent reads then hit LDS instead of
+// global memory (Teddy x16: the chain of ~450 dependent global loads per row dominated the
+// kernel), and the byte-wise trace stores disappear.  Used when 4 rows' traces fit in 64 KB.
+template <int K, bool LT>
 __global__ __launch_bounds__(256) void k_so(const SoArgs a) {
+    extern __shared__ __align__(16) uint64_t so_lds[];
     const int lane = threadIdx.x & 63;
     const int row_id = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int H = a.H, W = a.W, D = a.D;
@@ -49,6 +63,9 @@ __global__ __launch_bounds__(256) void k_so(const SoArgs a) {
     float* vrow = a.vm + pix0 * D;                     // (u, d) at u * D + d
     uint8_t* trow = a.trace + pix0 * D;
     uint16_t* crow = a.cidx + pix0;
+    // LT: this wave's trace masks [W][2K] u64, then its row-minimum indices [W] u16
+    uint64_t* tl = so_lds + (size_t)(threadIdx.x >> 6) * so_lds_words(W, K);
+    uint16_t* cl = (uint16_t*)(tl + (size_t)W * 2 * K);
     const uint32_t* prow = a.px + ((size_t)b * 2) * npix + (size_t)v * W;   // left view's packed BGR
     const int d0 = lane * K;
     bool valid[K];
@@ -133,6 +150,14 @@ __global__ __launch_bounds__(256) void k_so(const SoArgs a) {
                     code = 3;
                 }
                 nv[j] = t[k][j] + cost_min;
+                if (LT) {
+                    const uint64_t b0 = __ballot(code & 1u), b1 = __ballot(code & 2u);
+                    if (lane == 0) {
+                        tl[(size_t)u * 2 * K + 2 * j] = b0;
+                        tl[(size_t)u * 2 * K + 2 * j + 1] = b1;
+                    }
+                    continue;
+                }
                 codes |= code << (8 * (j & 3));
                 if ((j & 3) == 3 || j == K - 1) {   // flush the codes of disparities base .. j
                     const int base = j & ~3;
@@ -147,7 +172,12 @@ __global__ __launch_bounds__(256) void k_so(const SoArgs a) {
                     codes = 0;
                 }
             }
-            if (lane == 0) crow[u] = (uint16_t)cidx;
+            if (lane == 0) {
+                if (LT)
+                    cl[u] = (uint16_t)cidx;
+                else
+                    crow[u] = (uint16_t)cidx;
+            }
 #pragma unroll
             for (int j = 0; j < K; j++) {
                 prev[j] = valid[j] ? nv[j] : FLT_MAX;
@@ -185,8 +215,16 @@ __global__ __launch_bounds__(256) void k_so(const SoArgs a) {
     int u = W - 1;
     outv = lane == (u & 63) ? dmin : outv;
     for (; u > 0; u--) {
-        const int code = trow[(size_t)u * D + dmin];
-        const int ci = crow[u];
+        int code, ci;
+        if (LT) {   // uniform LDS reads: the two masks of dmin's slot and the column's row minimum
+            const int l = dmin / K, j = dmin - l * K;
+            const uint64_t m0 = tl[(size_t)u * 2 * K + 2 * j], m1 = tl[(size_t)u * 2 * K + 2 * j + 1];
+            code = (int)((m0 >> l) & 1u) | (int)(((m1 >> l) & 1u) << 1);
+            ci = cl[u];
+        } else {
+            code = trow[(size_t)u * D + dmin];
+            ci = crow[u];
+        }
         dmin = code == 0 ? dmin : (code == 1 ? dmin - 1 : (code == 2 ? dmin + 1 : ci));
         const int t = u - 1;
         if ((t & 63) == 63) {   // the group of columns t + 1 .. has been filled: flush it
@@ -204,11 +242,21 @@ void launch_so(const SoArgs& a, hipStream_t st) {
     const int rows = a.n * a.H;
     dim3 grid((unsigned)((rows + 3) / 4));
     const int k = (a.D + 63) / 64;
-    if (k <= 1) hipLaunchKernelGGL(k_so<1>, grid, dim3(256), 0, st, a);
-    else if (k <= 2) hipLaunchKernelGGL(k_so<2>, grid, dim3(256), 0, st, a);
-    else if (k <= 4) hipLaunchKernelGGL(k_so<4>, grid, dim3(256), 0, st, a);
-    else if (k <= 8) hipLaunchKernelGGL(k_so<8>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_so<16>, grid, dim3(256), 0, st, a);
+    const int kk = k <= 1 ? 1 : (k <= 2 ? 2 : (k <= 4 ? 4 : (k <= 8 ? 8 : 16)));
+    const size_t shm = 4 * so_lds_words(a.W, kk) * 8;
+    const bool lt = shm <= 64 * 1024 && SM_SO_LDS_TRACE;
+    const size_t sh = lt ? shm : 0;
+#define SM_SO_LAUNCH(KV)                                                              \
+    do {                                                                              \
+        if (lt) hipLaunchKernelGGL((k_so<KV, true>), grid, dim3(256), sh, st, a);     \
+        else hipLaunchKernelGGL((k_so<KV, false>), grid, dim3(256), 0, st, a);       \
+    } while (0)
+    if (kk == 1) SM_SO_LAUNCH(1);
+    else if (kk == 2) SM_SO_LAUNCH(2);
+    else if (kk == 4) SM_SO_LAUNCH(4);
+    else if (kk == 8) SM_SO_LAUNCH(8);
+    else SM_SO_LAUNCH(16);
+#undef SM_SO_LAUNCH
 }
 
 }  // namespace sm

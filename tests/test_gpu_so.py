@@ -17,8 +17,11 @@ def bits(a):
 
 
 @pytest.mark.parametrize("H,W,md,idx", [(31, 57, 15, 1), (24, 130, 63, 2), (20, 90, 64, 3), (17, 150, 127, 4),
-                                        (13, 300, 255, 5), (9, 70, 99, 6), (5, 3, 9, 7)])
+                                        (13, 300, 255, 5), (9, 70, 99, 6), (5, 3, 9, 7),
+                                        (6, 1100, 255, 8), (7, 2100, 63, 9)])
 def test_so_reference_order(oracle, H, W, md, idx):
+    """Rows whose trace fits in LDS (most) and rows that keep it in global memory (W = 1100 at
+    D = 256, W = 2100 at D = 64: four rows' masks exceed 64 KB)."""
     pair = S.make_pair(H, W, md + 1, 500 + idx)
     StereoMatching.costcalculation, StereoMatching.aggregation, StereoMatching.optimization = "censusGrad", "CBCA", "so"
     prm = StereoMatching.Parameters(md, H, W)

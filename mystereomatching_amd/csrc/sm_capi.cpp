@@ -176,6 +176,7 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (!(p.sgm_p1 >= 0) || !(p.sgm_p2 >= 0) || p.sgm_redu_coeff < 0) return bad("SGM penalties must be >= 0");
     if (p.do_refine) {
         if (!(p.rv_ratio > 0)) return bad("rv_ratio must be > 0");
+        if (p.disp_occ == -32768) return bad("disp_occ = -32768 is reserved (properIpol's outside-the-image mark)");
         if (p.region_vote_nums < 0 || p.region_vote_nums > 64) return bad("region_vote_nums must be in [0, 64]");
     }
     return SM_OK;

@@ -155,7 +155,8 @@ __global__ __launch_bounds__(256) void k_proper_ipol(const int16_t* __restrict__
                 qu[j] = u + n0 * sw0 + n1 * sw1;
                 qv[j] = v + n0 * sh0 + n1 * sh1;
                 const bool in = qu[j] >= 0 && qu[j] < W && qv[j] >= 0 && qv[j] < H;
-                q[j] = in ? (int)dp[(size_t)qv[j] * W + qu[j]] : -2;   // -2: outside (ends the walk)
+                q[j] = in ? (int)dp[(size_t)qv[j] * W + qu[j]] : -32768;   // outside (ends the walk; sm_create
+                                                                              // rejects DISP_OCC = -32768)
             }
 #pragma unroll
             for (int j = PI_CHUNK - 1; j >= 0; j--)   // first valid step of the chunk before any exit
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256) void k_proper_ipol(const int16_t* __restrict__
                 }
             // positions are monotone: after the first outside step every later one is outside, so
             // a valid step of the chunk always precedes the exit
-            if (q[PI_CHUNK - 1] == -2) break;
+            if (q[PI_CHUNK - 1] == -32768) break;
         }
         const bool occ = cur == disp_occ;
         // keys: occ -> the disparity; else (colour diff < 255) -> diff * 16 + direction

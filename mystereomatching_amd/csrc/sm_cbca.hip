@@ -57,6 +57,8 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 // The normalising sweeps use T = 10 with two tiles in flight: their rings (2 lag + T + 1 slots of
 // S plus a u16 area ring) then fit five waves per CU instead of four (Teddy x16, same box:
 // h_norm 0.459 -> 0.425 ms, v_norm 0.505 -> 0.480 ms with the LDS-staged arm words).
+// Three tiles in flight (PF = 3, 141 / 217 VGPRs for H / V norm) measured no better: h_norm
+// 0.415 -> 0.416, v_norm 0.463 -> 0.469 ms (Teddy x16, same box).
 // (Overridable at build time for tuning sweeps, see tools/build_variants.sh.)
 #ifndef SM_CB_T_SCAN_H
 #define SM_CB_T_SCAN_H 24
@@ -470,8 +472,25 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.Acc = 0;
     L.ws = 0;
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    typename CbLine<HORIZ, MODE, FULL, SCALE, RV>::Tile ta, tb, tc;
-    if constexpr (CbCfg<HORIZ, MODE>::PF == 2) {
+    typename CbLine<HORIZ, MODE, FULL, SCALE, RV>::Tile ta, tb, tc, td;
+    if constexpr (CbCfg<HORIZ, MODE>::PF == 3) {
+        L.load(ta, 0);
+        L.load(tb, T);
+        L.load(tc, 2 * T);
+        for (int j0 = 0; j0 < nst; j0 += 4 * T) {
+            L.load(td, j0 + 3 * T);
+            L.process(ta, j0);
+            if (j0 + T >= nst) break;
+            L.load(ta, j0 + 4 * T);
+            L.process(tb, j0 + T);
+            if (j0 + 2 * T >= nst) break;
+            L.load(tb, j0 + 5 * T);
+            L.process(tc, j0 + 2 * T);
+            if (j0 + 3 * T >= nst) break;
+            L.load(tc, j0 + 6 * T);
+            L.process(td, j0 + 3 * T);
+        }
+    } else if constexpr (CbCfg<HORIZ, MODE>::PF == 2) {
         L.load(ta, 0);
         L.load(tb, T);
         for (int j0 = 0; j0 < nst; j0 += 3 * T) {

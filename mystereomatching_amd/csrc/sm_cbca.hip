@@ -92,6 +92,16 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #ifndef SM_CB_LDS_WIN
 #define SM_CB_LDS_WIN 1
 #endif
+// H sweeps keep the other image's span as a ring (SM_CB_WIN_RING): consecutive tiles' spans
+// overlap in 63 words, so a tile loads only its T new words (one lane-vector load per set
+// instead of 64 + T - 1 words); the ring of R = 63 + T words is mirrored (every word written at
+// i and i + R), so reads at start + offset never wrap.  Probe with no window loads at all:
+// h_scan 0.265 -> 0.242 ms, h_norm 0.435 -> 0.418 ms (Teddy x16); the ring itself measured
+// h_norm 0.416 -> 0.409 ms, h_scan unchanged (same box).
+#ifndef SM_CB_WIN_RING
+#define SM_CB_WIN_RING 1
+#endif
+__host__ __device__ constexpr int cbca_win_ring(int T) { return 63 + T; }
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
     return mode == CB_SCAN ? (horiz ? SM_CB_T_SCAN_H : SM_CB_T_SCAN_V)
                            : (mode == CB_NORM ? (horiz ? SM_CB_T_NORM_H : SM_CB_T_NORM_V) : 8);
@@ -124,7 +134,7 @@ __host__ __device__ inline int cbca_win_words(bool horiz, int mode) {
     if (!SM_CB_LDS_WIN) return 0;
     const int T = cbca_tile(horiz, mode);
     const int nsets = mode == CB_SCAN ? 1 : (mode == CB_NORM ? 2 : 3);
-    return nsets * (T + (horiz ? 64 + T - 1 : 0));
+    return nsets * (T + (horiz ? (SM_CB_WIN_RING ? 2 * cbca_win_ring(T) : 64 + T - 1) : 0));
 }
 __host__ __device__ inline int cbca_smem_words(int lag, bool horiz, int mode) {
     return cbca_ring_words(lag, horiz, mode) + cbca_win_words(horiz, mode);
@@ -172,6 +182,7 @@ struct CbLine {
     float S1, S2;
     uint32_t Acc;
     int ws;                   // ring slot of the tile's first position
+    int wrs;                  // SM_CB_WIN_RING: span-ring slot of the current tile's first word (j0 mod R)
     float* r1;
     float* r2;
     uint16_t* ra;
@@ -219,9 +230,14 @@ struct CbLine {
                 // base .. base + T - 1: left view q = p - d in [base - c64 - 63, base - c64 + T - 1],
                 // right view q = p + d in [base + c64, base + c64 + 63 + T - 1]; 0 outside the line
                 const int q0 = RV ? base + c64 : base - c64 - 63;
-                const int qa = q0 + lane, qb = q0 + 64 + lane;
-                t.a1w[s][0] = buf_ld_u32(A1r[s], (unsigned)qa < (unsigned)len ? (uint32_t)qa * 4u : 0x80000000u, 0);
-                t.a1w[s][1] = buf_ld_u32(A1r[s], (lane < T - 1 && (unsigned)qb < (unsigned)len) ? (uint32_t)qb * 4u : 0x80000000u, 0);
+                if (SM_CB_WIN_RING) {   // the tile's T new words q0 + 63 .. q0 + 62 + T
+                    const int qn = q0 + 63 + lane;
+                    t.a1w[s][0] = buf_ld_u32(A1r[s], (lane < T && (unsigned)qn < (unsigned)len) ? (uint32_t)qn * 4u : 0x80000000u, 0);
+                } else {
+                    const int qa = q0 + lane, qb = q0 + 64 + lane;
+                    t.a1w[s][0] = buf_ld_u32(A1r[s], (unsigned)qa < (unsigned)len ? (uint32_t)qa * 4u : 0x80000000u, 0);
+                    t.a1w[s][1] = buf_ld_u32(A1r[s], (lane < T - 1 && (unsigned)qb < (unsigned)len) ? (uint32_t)qb * 4u : 0x80000000u, 0);
+                }
             } else if (HORIZ) {
                 // H window input at position base + lane: left view — the right pixel of lane 0
                 // (shifted in at lane 0); right view — the left pixel of lane 63 (shifted in there)
@@ -250,7 +266,9 @@ struct CbLine {
     __device__ __forceinline__ uint32_t isect(const Tile& t, int s, int k) const {
         if (SM_CB_LDS_WIN) {
             const uint32_t a0 = wown[s * T + k];   // broadcast read
-            const uint32_t a1 = HORIZ ? wspan[s * (64 + T - 1) + (RV ? k + lane : k + 63 - lane)] : (t.a1[s][k] & vmask);
+            const uint32_t a1 = HORIZ ? (SM_CB_WIN_RING ? wspan[s * 2 * cbca_win_ring(T) + wrs + (RV ? k + lane : k + 63 - lane)]
+                                                        : wspan[s * (64 + T - 1) + (RV ? k + lane : k + 63 - lane)])
+                                      : (t.a1[s][k] & vmask);
             return pkmin(a0, a1);
         }
         const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
@@ -263,7 +281,16 @@ struct CbLine {
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             if (lane < T) wown[s * T + lane] = t.a0[s];
-            if (HORIZ) {
+            if (HORIZ && SM_CB_WIN_RING) {
+                constexpr int R = cbca_win_ring(T);
+                uint32_t* sp = wspan + s * 2 * R;
+                const int w = wrs + 63 + lane;           // < 2 R
+                const int i = w >= R ? w - R : w;
+                if (lane < T) {
+                    sp[i] = t.a1w[s][0];
+                    sp[i + R] = t.a1w[s][0];
+                }
+            } else if (HORIZ) {
                 uint32_t* sp = wspan + s * (64 + T - 1);
                 sp[lane] = t.a1w[s][0];
                 if (lane < T - 1) sp[64 + lane] = t.a1w[s][1];
@@ -382,6 +409,7 @@ struct CbLine {
                 if (!GUARD || (unsigned)(i20 + k) < (unsigned)len) store_tile(ob2, k, s2h[k] - s2t[k]);
         }
         ws = (ws + T == ring) ? 0 : ws + T;
+        if (SM_CB_WIN_RING) wrs = (wrs + T >= cbca_win_ring(T)) ? wrs + T - cbca_win_ring(T) : wrs + T;
     }
 
     __device__ __forceinline__ void process(const Tile& t, int j0) {
@@ -471,6 +499,21 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.S1 = L.S2 = 0.f;
     L.Acc = 0;
     L.ws = 0;
+    L.wrs = 0;
+    if constexpr (HORIZ && SM_CB_LDS_WIN && SM_CB_WIN_RING) {
+        // span-ring prologue: the first tile's words q0 .. q0 + 62 of every set (the tiles add the rest)
+        constexpr int R = cbca_win_ring(T);
+#pragma unroll
+        for (int s = 0; s < NSETS; s++) {
+            const int base = -L.set_off(s);
+            const int q = (RV ? base + L.c64 : base - L.c64 - 63) + L.lane;
+            const uint32_t w = buf_ld_u32(L.A1r[s], (L.lane < 63 && (unsigned)q < (unsigned)L.len) ? (uint32_t)q * 4u : 0x80000000u, 0);
+            if (L.lane < 63) {
+                L.wspan[s * 2 * R + L.lane] = w;
+                L.wspan[s * 2 * R + L.lane + R] = w;
+            }
+        }
+    }
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
     typename CbLine<HORIZ, MODE, FULL, SCALE, RV>::Tile ta, tb, tc, td;
     if constexpr (CbCfg<HORIZ, MODE>::PF == 3) {

@@ -55,6 +55,14 @@ __global__ void k_pack_bgr(const uint8_t* __restrict__ bgr, uint32_t* __restrict
     }
 }
 
+// Same, four pixels per thread: three aligned dword loads (12 bytes) and one dwordx4 store.
+__global__ void k_pack_bgr4(const uint32_t* __restrict__ bgr, uint4* __restrict__ px, size_t quads) {
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t w0 = bgr[3 * q], w1 = bgr[3 * q + 1], w2 = bgr[3 * q + 2];
+        px[q] = make_uint4(w0 & 0xffffffu, (w0 >> 24) | ((w1 & 0xffffu) << 8), (w1 >> 16) | ((w2 & 0xffu) << 16), w2 >> 8);
+    }
+}
+
 // Arm-walk words (calHorVerDis, cpp:2959-3050).  A walk step compares the step pixel with the
 // centre under threshold t and with the previous step pixel under C_D.  k_pack_arms writes two
 // planes whose words hold the pixel in 10-bit fields (B | G << 10 | R << 20) and the C_D test
@@ -79,12 +87,25 @@ __device__ __forceinline__ uint32_t pack10(uint32_t p) {   // B | G << 8 | R << 
 // towards direction i (rv/ru tables of sgm, cpp:6207-6208) is inside and its max-channel
 // difference exceeds sgm_corDifThres — of the left image, and of the right image when vm[1] is
 // optimised too (leftFirst = false compares I_c[1], h:2224).
+#ifndef SM_PACK_ROWS
+#define SM_PACK_ROWS 4   // rows per thread (short one-row blocks were latency-bound: 33 us on Teddy x16)
+#endif
+__device__ __forceinline__ void pack_arms_pixel(const PrepArgs& a, int arms, int img, int v, int u);
+
 __global__ __launch_bounds__(256) void k_pack_arms(const PrepArgs a, int arms) {
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= a.W) return;
+#pragma unroll
+    for (int r = 0; r < SM_PACK_ROWS; r++) {
+        const int v = blockIdx.y * SM_PACK_ROWS + r;
+        if (v < a.H) pack_arms_pixel(a, arms, blockIdx.z, v, u);
+    }
+}
+
+__device__ __forceinline__ void pack_arms_pixel(const PrepArgs& a, int arms, int img, int v, int u) {
     const int H = a.H, W = a.W;
-    const int u = blockIdx.x * 256 + threadIdx.x, v = blockIdx.y;
-    if (u >= W) return;
     const size_t npix = (size_t)H * W;
-    const int img = blockIdx.z, b = img >> 1, view = img & 1;
+    const int b = img >> 1, view = img & 1;
     const size_t i = (size_t)img * npix + (size_t)v * W + u;
     const uint32_t* pc = a.px + i;
     const uint32_t c = pc[0];
@@ -366,10 +387,20 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
     const size_t total = (size_t)n * 2 * a.H * a.W;
     size_t blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_pack_bgr, dim3((unsigned)blocks), dim3(256), 0, st, a.bgr, a.px, total);
+    if (((uintptr_t)a.bgr & 3) == 0 && ((uintptr_t)a.px & 15) == 0) {
+        const size_t quads = total / 4;
+        size_t qb = (quads + 255) / 256;
+        if (qb > 4096) qb = 4096;
+        if (quads) hipLaunchKernelGGL(k_pack_bgr4, dim3((unsigned)qb), dim3(256), 0, st, (const uint32_t*)a.bgr, (uint4*)a.px, quads);
+        if (total % 4)   // the last one to three pixels
+            hipLaunchKernelGGL(k_pack_bgr, dim3(1), dim3(64), 0, st, a.bgr + quads * 12, a.px + quads * 4, total % 4);
+    } else {
+        hipLaunchKernelGGL(k_pack_bgr, dim3((unsigned)blocks), dim3(256), 0, st, a.bgr, a.px, total);
+    }
     const bool strips = a.do_arms && prep_strips(a.L_out);
     if (strips || a.do_flags)   // arm-walk planes and the SGM penalty flags
-        hipLaunchKernelGGL(k_pack_arms, dim3((a.W + 255) / 256, a.H, 2 * n), dim3(256), 0, st, a, (int)strips);
+        hipLaunchKernelGGL(k_pack_arms, dim3((a.W + 255) / 256, (a.H + SM_PACK_ROWS - 1) / SM_PACK_ROWS, 2 * n), dim3(256), 0,
+                           st, a, (int)strips);
     dim3 grid((a.W + PREP_TX - 1) / PREP_TX, (a.H + PREP_TY - 1) / PREP_TY, 2 * n);
     const size_t shm = (size_t)prep_gray_bytes(a.rv, a.ru) + (strips ? 4 * (size_t)prep_strip_words(a.L_out) : 0);
     if (a.rv == 3 && a.ru == 4 && a.ring == 1)   // the reference's default census window (cpp:815)

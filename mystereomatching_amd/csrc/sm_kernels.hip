@@ -432,6 +432,9 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 #ifndef SM_COST_STORE_AUX
 #define SM_COST_STORE_AUX 2   // buffer store cache policy: slc = non-temporal (see SM_ST_AUX, sm_device.h)
 #endif
+#ifndef SM_COST_SPLIT
+#define SM_COST_SPLIT 1
+#endif
 #ifndef SM_COST_UNROLL
 #define SM_COST_UNROLL 1
 #endif
@@ -493,6 +496,13 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     constexpr bool ADM = METHOD == SM_M_AD || METHOD == SM_M_AD_CENSUS;
     uint4* mrec = (uint4*)cs_raw;                                // [(P + D - 1) * RW]
     ulonglong2* fcode = (ulonglong2*)(mrec + RW * (COST_P + D - 1));  // [P]
+    // SM_COST_SPLIT: records of 2 uint4 (CW = 3, 4) live as two planes, so a lane's record
+    // reads are 16-byte (plane A) and 8 / 16-byte (plane B) strided instead of 32-byte strided
+    // (half the LDS banks per pass: 2-way conflicts on every element)
+    constexpr bool SPLIT = SM_COST_SPLIT && RW == 2;
+    uint4* mrecB4 = mrec + (COST_P + D - 1);                     // plane B (SPLIT), CW = 4
+    uint2* mrecB2 = (uint2*)mrecB4;                              // plane B (SPLIT), CW = 3
+    auto recA = [&](int i) -> uint4& { return SPLIT ? mrec[i] : mrec[RW * i]; };
     uint64_t* etab = (uint64_t*)(fcode + COST_P);               // [32] 2^(i/32)
     float* fgx = (float*)(etab + 32);                            // [P]
     float* fgy = fgx + COST_P;
@@ -555,11 +565,13 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
             bias = (uint32_t)icd;
         }
         if (CW == 4) {
-            mrec[2 * i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, (uint32_t)(c.y >> 32));
-            mrec[2 * i + 1] = make_uint4(w2, w3, bias, 0);
+            recA(i) = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, (uint32_t)(c.y >> 32));
+            if (SPLIT) mrecB4[i] = make_uint4(w2, w3, bias, 0);
+            else mrec[2 * i + 1] = make_uint4(w2, w3, bias, 0);
         } else if (CW == 3) {
-            mrec[2 * i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, w2);
-            mrec[2 * i + 1] = make_uint4(w3, bias, 0, 0);
+            recA(i) = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, w2);
+            if (SPLIT) mrecB2[i] = make_uint2(w3, bias);
+            else mrec[2 * i + 1] = make_uint4(w3, bias, 0, 0);
         } else {
             mrec[i] = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), w2, w3);
         }
@@ -587,15 +599,15 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
         auto elem = [&](int d, int q) {                // q = u - sgn * d, the moving position
             const int mi = q - mbase;                  // staged record (zeros when out of range)
             if constexpr (NOSEL) {
-                const uint4 r0 = mrec[RW * mi];
+                const uint4 r0 = recA(mi);
                 uint32_t pc, gxm, gym;
                 if constexpr (CW == 3) {
-                    const uint2 r1 = *(const uint2*)&mrec[RW * mi + 1];
+                    const uint2 r1 = SPLIT ? mrecB2[mi] : *(const uint2*)&mrec[RW * mi + 1];
                     pc = r1.y;                         // icd for out-of-range candidates, else 0
                     gxm = r0.w;
                     gym = r1.x;
                 } else {
-                    const uint4 r1 = mrec[RW * mi + 1];
+                    const uint4 r1 = SPLIT ? mrecB4[mi] : mrec[RW * mi + 1];
                     pc = r1.z;
                     gxm = r1.x;
                     gym = r1.y;
@@ -619,7 +631,7 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 return;
             }
             const bool oor = (unsigned)q >= (unsigned)W;
-            const uint4 r0 = mrec[RW * mi];
+            const uint4 r0 = recA(mi);
             uint32_t w2 = r0.z, w3 = r0.w;
             uint32_t pc = 0;
             if (CEN) {
@@ -629,9 +641,9 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
             }
             if (CW == 3) {
                 w2 = r0.w;
-                w3 = ((const uint32_t*)mrec)[4 * (RW * mi + 1)];
+                w3 = SPLIT ? mrecB2[mi].x : ((const uint32_t*)mrec)[4 * (RW * mi + 1)];
             } else if (CW == 4) {
-                const uint4 r1 = mrec[RW * mi + 1];
+                const uint4 r1 = SPLIT ? mrecB4[mi] : mrec[RW * mi + 1];
                 w2 = r1.x;
                 w3 = r1.y;
             }

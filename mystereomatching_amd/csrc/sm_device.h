@@ -24,6 +24,10 @@
      0x3feee89f995ad3adULL, 0x3feeff76f2fb5e47ULL, 0x3fef199bdd85529cULL, 0x3fef3720dcef9069ULL, \
      0x3fef5818dcfba487ULL, 0x3fef7c97337b9b5fULL, 0x3fefa4afa2a490daULL, 0x3fefd0765b6e4540ULL}
 
+#ifndef SM_EXPF_FMA_SHIFT
+#define SM_EXPF_FMA_SHIFT 1
+#endif
+
 namespace sm {
 
 // expf core; `tab` is the 32-entry 2^(i/32) table (device: __constant__, host: static).
@@ -37,13 +41,22 @@ __host__ __device__ inline float expf_glibc_core(float x, const Tab& tab) {
     const double C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32;
     const double C2 = 0x1.62e42ff0c52d6p-1 / 32;
     double xd = (double)x;
+#if SM_EXPF_FMA_SHIFT
+    // kd = round(InvLn2N * xd) through one fma instead of a rounded product plus SHIFT: equal
+    // to glibc's result on every float the device path sees (tests/test_gpu_parity.py,
+    // test_device_expf_exhaustive: all of [-104, -0])
+    double kd = __builtin_fma(InvLn2N, xd, SHIFT);
+#else
     double z = InvLn2N * xd;
     double kd = z + SHIFT;
+#endif
     uint64_t ki = __builtin_bit_cast(uint64_t, kd);
     kd -= SHIFT;
     double r = __builtin_fma(InvLn2N, xd, -kd);
     uint64_t t = tab[ki % 32];
-    t += ki << (52 - 5);
+    // t += ki << 47: the shifted term's low word is 0, so only the high word changes (one
+    // 32-bit add instead of a 64-bit shift and add)
+    t = (t & 0xffffffffull) | ((uint64_t)((uint32_t)(t >> 32) + ((uint32_t)ki << 15)) << 32);
     double s = __builtin_bit_cast(double, t);
     double zz = __builtin_fma(C0, r, C1);
     double r2 = r * r;

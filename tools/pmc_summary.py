@@ -34,7 +34,7 @@ def profile_name(sym: str, seen: dict) -> str:
         return f"sgm_path{seen['mid']}"
     if "k_cost" in sym:
         return "cost_volume"
-    if "k_prep" in sym or "k_pack_bgr" in sym:
+    if "k_prep" in sym or "k_pack_bgr" in sym or "k_pack_arms" in sym:
         return "prep"
     if "k_wta" in sym:
         return "wta"
@@ -49,28 +49,29 @@ def load(path: str, counter: str):
     for r in rows:
         if r["Counter_Name"] != counter:
             continue
-        out.append((profile_name(r["Kernel_Name"], seen), float(r["Counter_Value"]) * 1024.0))
+        # a step of "prep" is three dispatches (k_pack_bgr4, k_pack_arms, k_prep): count steps by k_prep
+        step = "k_prep" in r["Kernel_Name"] or "k_pack" not in r["Kernel_Name"]
+        out.append((profile_name(r["Kernel_Name"], seen), float(r["Counter_Value"]) * 1024.0, step))
     return out
 
 
 def main():
     fetch, write, dst = sys.argv[1:4]
     acc = defaultdict(lambda: {"read": 0.0, "write": 0.0, "n_read": 0, "n_write": 0})
-    for name, v in load(fetch, "FETCH_SIZE"):
+    for name, v, step in load(fetch, "FETCH_SIZE"):
         acc[name]["read"] += 2.0 * v
-        acc[name]["n_read"] += 1
-    for name, v in load(write, "WRITE_SIZE"):
+        acc[name]["n_read"] += step
+    for name, v, step in load(write, "WRITE_SIZE"):
         acc[name]["write"] += v
-        acc[name]["n_write"] += 1
+        acc[name]["n_write"] += step
     kernels = {}
     for name, a in acc.items():
         if not a["n_read"] or not a["n_write"] or name.startswith("__"):
             continue
         r, w = a["read"] / a["n_read"], a["write"] / a["n_write"]
-        # "prep" is two dispatches per step (pack + prep): report per step, like the bench
-        per = 2 if name == "prep" else 1
-        kernels[name] = {"hbm_read_bytes_per_launch": r * per, "hbm_write_bytes_per_launch": w * per,
-                         "hbm_bytes_per_launch": (r + w) * per, "dispatches": a["n_read"]}
+        # "prep" sums its three dispatches per step, like the bench's "prep" timer
+        kernels[name] = {"hbm_read_bytes_per_launch": r, "hbm_write_bytes_per_launch": w,
+                         "hbm_bytes_per_launch": r + w, "steps": a["n_read"]}
     json.dump({"source": [fetch, write],
                "correction": "read = 2 x FETCH_SIZE(KB) x 1024 (gfx950 half-count), write = WRITE_SIZE(KB) x 1024",
                "kernels": kernels}, open(dst, "w"), indent=1)

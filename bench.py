@@ -6,8 +6,12 @@ torch.distributed.run, one rank per GPU.  A step = one pass of the whole hot pat
 already resident in HBM.  Pairs shard across ranks with no data-path collective (weak scaling:
 each rank owns its own batch); RCCL is used only for the barrier and the max-over-ranks time.
 
-Default workload = BASELINE.json configs[1]: Middlebury Teddy size 450x375, D = 64 (maxdisp 63),
-the bit-exact default path.  Prints ONE JSON line on rank 0.
+Default workload = BASELINE.json configs[3], the largest single-GPU config and the one north_star's
+targets are quoted on: Middlebury-2014 full resolution 3000x2000, D = 256, censusGrad + CBCA(2) +
+SolveAll + SGM 4-path + WTA, 2 pairs per GPU.  Rank 0's pair 0 map is checked bit-exact against
+the committed oracle fixture of that pair (tests/golden/large_fullres_d256.npz).  Other configs:
+--workload teddy (configs[1], 16 pairs, CPU baseline on whole pairs with map comparison),
+kitti (configs[2]), hd (configs[4] per-GPU shard).  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -30,12 +34,30 @@ WORKLOADS = {
     "teddy": (375, 450, 63, 4, 16, "Middlebury Teddy 450x375 D=64, censusGrad+CBCA(2 it)+SolveAll+SGM 4-path+WTA "
                                    "(BASELINE configs[1], bit-exact path)"),
     "kitti": (375, 1242, 191, 8, 4, "KITTI-2015 1242x375 D=192, censusGrad+CBCA+SGM 8-path+WTA (configs[2])"),
-    "fullres": (2000, 3000, 255, 4, 1, "Middlebury-2014 full-res 3000x2000 D=256, censusGrad+CBCA+SGM 4-path+WTA (configs[3])"),
+    "fullres": (2000, 3000, 255, 4, 2, "Middlebury-2014 full-res 3000x2000 D=256, censusGrad+CBCA+SGM 4-path+WTA (configs[3])"),
     "hd": (1080, 1920, 255, 4, 8, "1920x1080 D=256 synthetic pairs, censusGrad+CBCA+SGM 4-path+WTA (configs[4] per-GPU shard)"),
 }
 
 
 CPU_FULL_PAIR_MAX = 200_000_000   # disparities per pair the CPU baseline runs whole (KITTI: 89 M)
+
+# oracle fixture of synthetic pair 0 per workload (tests/golden/make_large.py / make_golden.py)
+FIXTURE = {"fullres": "large_fullres_d256", "hd": "large_hd1080_d256", "kitti": "large_kitti_8path_d192",
+           "teddy": "teddy_censusgrad_d64"}
+
+
+def fixture_check(workload, refine, opt, disp0):
+    """Compare rank 0's pair-0 map with the committed oracle map of that pair (no oracle run)."""
+    name = FIXTURE.get(workload)
+    path = os.path.join(ROOT, "tests", "golden", f"{name}.npz") if name else None
+    if refine or opt != "sgm" or not path or not os.path.exists(path):
+        return None
+    z = np.load(path)
+    want = z["disp"]
+    ok = want.shape == disp0.shape and bool(np.array_equal(want, disp0))
+    if not ok:
+        raise SystemExit(f"bench: pair 0 map differs from the oracle fixture {name}.npz")
+    return {"fixture": f"tests/golden/{name}.npz", "pair": 0, "bit_exact": ok}
 
 
 def _host_cpu():
@@ -57,7 +79,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="teddy", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="fullres", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="pairs per GPU (0 = workload default)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,6 +177,7 @@ def main():
         kernels = sb.profile_read()
         sb.profile(False)
     disp = sb.download()
+    parity = fixture_check(args.workload, args.refine, args.opt, disp[0]) if rank == 0 else None
     bad2 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 2.0)[0] for i in range(B)]))
     bad1 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 1.0)[0] for i in range(B)]))
 
@@ -237,7 +260,7 @@ def main():
                        "sgm_paths": paths, "optimization": args.opt, "refine": bool(args.refine),
                        "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
             "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
-            "roofline": roofline, "cpu_baseline": cpu, "kernels": kern_out,
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "kernels": kern_out,
             "ms_per_step_instrumented": None if ms_prof is None else round(ms_prof, 4),
         }
         if cpu:

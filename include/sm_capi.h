@@ -106,6 +106,11 @@ typedef struct sm_params {
     int32_t do_proper_ipol;      /* Do_properIpol = 1 (h:76) */
     int32_t disp_occ;            /* DISP_OCC = -2 * 16 (h:216) */
     int32_t do_last_median_blur; /* Do_lastMedianBlur = 1 (h:80) */
+    /* scheduling of sm_run (results are identical for every setting): */
+    int32_t sub_batch;           /* run the n pairs in groups of k (0 = one group), stages back to back */
+    int32_t num_streams;         /* 0/1: one stream; 2-4: groups alternate over that many streams,
+                                  * group k + 1 starting once group k's CBCA is done */
+    int32_t fuse_norm_scan;      /* 1: CBCA normalising sweep fused with the next scan (measured slower) */
 } sm_params;
 
 typedef struct sm_ctx sm_ctx;
@@ -132,6 +137,8 @@ SM_API sm_status sm_solve_all_pyr(sm_ctx* const* levels, int32_t py_lvl, float r
  * ((rows + 1) / 2) x ((cols + 1) / 2); host or device pointers, synchronous.  (main_.cpp:145-148) */
 SM_API sm_status sm_pyr_down(int32_t hip_device, const uint8_t* src, int32_t rows, int32_t cols, int32_t channels,
                              uint8_t* dst);
+/* cv::pyrDown of a 1-channel f32 image (the ground truth DT, main_.cpp:149), same contract. */
+SM_API sm_status sm_pyr_down_f32(int32_t hip_device, const float* src, int32_t rows, int32_t cols, float* dst);
 /* refine() on DP[0] (needs do_refine = 1 at sm_create and a preceding sm_disp_optimize). */
 SM_API sm_status sm_refine(sm_ctx* ctx, int16_t* disp_out);
 SM_API sm_status sm_get_disp(sm_ctx* ctx, int32_t view, int16_t* dst);  /* DP[view], H*W int16 */

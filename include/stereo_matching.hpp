@@ -1,21 +1,45 @@
 // stereo_matching.hpp — header-only C++ facade with the reference's class API over sm_capi.h.
 //
-// A user of the reference replaces `#include "stereoMatching.h"` by this header and keeps the
-// main_.cpp call sequence (main_.cpp:138-172):
+// Source-compatible with the reference driver's use of class StereoMatching (main_.cpp:130-178):
+// a user replaces `#include "stereoMatching.h"` and OpenCV's Mat/imread/pyrDown by this header
+// (`using namespace smamd;` in place of `using namespace cv;`) and keeps the call sequence:
 //
-//   smamd::StereoMatching::Parameters param(maxDisp, rows, cols, lamCen, lamG, M, lamc, ts, csv, disSc);
-//   auto* sm = new smamd::StereoMatching(I1_c, I2_c, I1, I2, param);
-//   sm->costCalculate();                       // stereoMatching.cpp:945-1021
-//   smamd::SolveAll(&sm, 1, 0.3f);             // stereoMatching.cpp:2142-2208
-//   sm->dispOptimize();                        // stereoMatching.cpp:1046-1136
-//   const int16_t* disparity = sm->DP[0].data();
+//   string StereoMatching::costcalculation = "censusGrad";     // main_.cpp:15-19: the program
+//   string StereoMatching::aggregation = "CBCA";               // defines the static selectors,
+//   string StereoMatching::optimization = "sgm";               // exactly as the reference's
+//   string StereoMatching::object = "";                        // header declares them (h:50-54)
+//   const string StereoMatching::root = "...";
+//   ...
+//   StereoMatching::Parameters param(maxDisp, rows, cols, lamCen, lamG, M, lamc, ts, csv, disSc);  // main:138
+//   smPsy[p] = new StereoMatching(I1_c, I2_c, I1, I2, DT, all, nonocc, disc, param);              // main:139
+//   smPsy[p]->costCalculate();                                  // cpp:945-1021
+//   pyrDown(I1_c, I1_c); ...                                    // main:145-154
+//   SolveAll(smPsy, PY_LEV, REG_LAMBDA);                        // cpp:2142-2208
+//   smPsy[0]->openCSV(); smPsy[0]->dispOptimize();              // main:159-163, cpp:1046-1136
+//   if (StereoMatching::Do_refine) smPsy[0]->refine();          // main:165-166
+//   smPsy[0]->closeCSV(); smPsy[0]->saveTime(time, "all");      // main:168-171
+//   const int16_t* d = smPsy[0]->DP[0].ptr<int16_t>(0);         // public member DP (h:2724)
 //
-// Images are plain views (smamd::Mat: rows, cols, channels, step, data) instead of cv::Mat so
-// the facade needs no OpenCV; with OpenCV available, wrap a cv::Mat as {m.rows, m.cols,
-// m.channels(), m.step, m.data}.  Non-OK statuses become std::runtime_error (the reference threw
-// cv::Exception from CV_Assert).
+// smamd::Mat mirrors the part of cv::Mat the driver touches: reference-counted shallow copies
+// (the reference's ctor keeps headers of the caller's images, cpp:2066-2075), rows/cols/step/data,
+// empty(), channels(), ptr<T>(row), convertTo(CV_32F, alpha).  imread reads binary PNM (P5 gray,
+// P6 colour; flags 1 -> BGR, 0 -> gray with libpng's rgb_to_gray weights, the formula OpenCV's
+// PNG decoder uses) since the container has no image codecs.  All compute runs in libsm_hip.so on
+// the GPU; the library does no file I/O, so openCSV/closeCSV/saveTime keep their records in memory
+// (the reference wrote savePath files and exit()ed on failure, h:1727-1744).  Non-OK statuses
+// become std::runtime_error (the reference threw cv::Exception from CV_Assert).
 #pragma once
 #include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -24,46 +48,274 @@
 
 namespace smamd {
 
-struct Mat {
-    int rows = 0, cols = 0, channels = 1;
-    size_t step = 0;          // bytes per row
-    const uint8_t* data = nullptr;
+// OpenCV depth codes used by the driver (CV_8U images, CV_16S DP, CV_32F DT)
+enum { CV_8U = 0, CV_16S = 3, CV_32F = 5 };
+
+#ifndef CV_Assert
+#define CV_Assert(expr) \
+    do { if (!(expr)) throw std::runtime_error("Assertion failed: " #expr); } while (0)
+#endif
+
+inline int& default_device() {   // HIP device for the free functions (pyrDown); ctor takes its own
+    static int dev = 0;
+    return dev;
+}
+
+class Mat {
+   public:
+    int rows = 0, cols = 0;
+    size_t step = 0;             // bytes per row
+    uint8_t* data = nullptr;
+
+    Mat() = default;
+    Mat(int nrows, int ncols, int depth, int channels = 1) { create(nrows, ncols, depth, channels); }
+    // non-owning view of caller memory (e.g. a cv::Mat: view(m.rows, m.cols, m.channels(), m.step, m.data))
+    static Mat view(int nrows, int ncols, int channels, size_t row_step, const void* ptr0, int depth = CV_8U) {
+        Mat m;
+        m.rows = nrows, m.cols = ncols, m.cn_ = channels, m.depth_ = depth, m.step = row_step;
+        m.data = (uint8_t*)ptr0;
+        return m;
+    }
+    void create(int nrows, int ncols, int depth, int channels = 1) {
+        rows = nrows, cols = ncols, depth_ = depth, cn_ = channels;
+        step = (size_t)cols * elemSize();
+        buf_ = std::make_shared<std::vector<uint8_t>>(step * rows);
+        data = buf_->data();
+    }
+    bool empty() const { return data == nullptr || rows == 0 || cols == 0; }
+    int channels() const { return cn_; }
+    int depth() const { return depth_; }
+    int type() const { return depth_ + ((cn_ - 1) << 3); }   // CV_MAKETYPE
+    size_t elemSize1() const { return depth_ == CV_8U ? 1 : depth_ == CV_16S ? 2 : 4; }
+    size_t elemSize() const { return elemSize1() * cn_; }
+    bool isContinuous() const { return step == (size_t)cols * elemSize(); }
+    template <typename T> T* ptr(int r = 0) { return (T*)(data + (size_t)r * step); }
+    template <typename T> const T* ptr(int r = 0) const { return (const T*)(data + (size_t)r * step); }
+    Mat clone() const {
+        Mat m(rows, cols, depth_, cn_);
+        for (int r = 0; r < rows; r++) std::memcpy(m.ptr<uint8_t>(r), ptr<uint8_t>(r), (size_t)cols * elemSize());
+        return m;
+    }
+    // Mat::convertTo(dst, rtype, alpha, beta) for u8 / s16 / f32 -> f32 (main_.cpp:127-129:
+    // DT.convertTo(DT, CV_32F, 1.0 / disp_reduceCoeff)): (float)v * (float)alpha + (float)beta
+    void convertTo(Mat& dst, int rtype, double alpha = 1, double beta = 0) const {
+        if (rtype != CV_32F) throw std::invalid_argument("convertTo: only CV_32F targets are supported");
+        Mat out(rows, cols, CV_32F, cn_);
+        const float a = (float)alpha, b = (float)beta;
+        for (int r = 0; r < rows; r++) {
+            float* o = out.ptr<float>(r);
+            for (int i = 0; i < cols * cn_; i++) {
+                const float v = depth_ == CV_8U ? (float)ptr<uint8_t>(r)[i]
+                                : depth_ == CV_16S ? (float)ptr<int16_t>(r)[i] : ptr<float>(r)[i];
+                o[i] = b == 0.f ? v * a : v * a + b;
+            }
+        }
+        dst = out;   // a new buffer; other headers of the old one keep it (cv::Mat semantics)
+    }
+    // rows x cols x channels packed copy of the pixels (host), element type T
+    template <typename T> std::vector<T> packed() const {
+        std::vector<T> v((size_t)rows * cols * cn_);
+        for (int r = 0; r < rows; r++) std::memcpy(v.data() + (size_t)r * cols * cn_, ptr<uint8_t>(r), (size_t)cols * elemSize());
+        return v;
+    }
+
+   private:
+    int depth_ = CV_8U, cn_ = 1;
+    std::shared_ptr<std::vector<uint8_t>> buf_;
 };
+
+// cv::imread for binary PNM: P6 (RGB) or P5 (gray), maxval 255.  flags 1: 3-channel BGR; flags 0:
+// gray ((R*9798 + G*19235 + B*3735 + 16384) >> 15, libpng's rgb_to_gray).  Empty Mat on failure
+// (main_.cpp:108 tests empty()).
+inline Mat imread(const std::string& path, int flags = 1) {
+    std::ifstream f(path, std::ios::binary);
+    std::string magic;
+    int w = 0, h = 0, maxv = 0;
+    if (!(f >> magic >> w >> h >> maxv) || (magic != "P6" && magic != "P5") || maxv != 255 || w < 1 || h < 1)
+        return Mat();
+    f.get();
+    const int cin = magic == "P6" ? 3 : 1;
+    std::vector<uint8_t> px((size_t)w * h * cin);
+    if (!f.read((char*)px.data(), (std::streamsize)px.size())) return Mat();
+    Mat m(h, w, CV_8U, flags == 0 ? 1 : 3);
+    for (size_t i = 0; i < (size_t)w * h; i++) {
+        const uint8_t R = px[i * cin], G = px[i * cin + (cin - 1) / 2], B = px[i * cin + cin - 1];
+        if (flags == 0) {
+            m.data[i] = cin == 1 ? R : (uint8_t)((R * 9798 + G * 19235 + B * 3735 + 16384) >> 15);
+        } else {
+            m.data[i * 3] = B, m.data[i * 3 + 1] = G, m.data[i * 3 + 2] = R;
+        }
+    }
+    return m;
+}
+
+// cv::pyrDown (main_.cpp:145-154) on the GPU: u8 with 1 or 3 channels (the inputs, masks) or
+// 1-channel f32 (the ground truth DT).  dst gets a new buffer of (rows+1)/2 x (cols+1)/2.
+inline void pyrDown(const Mat& src, Mat& dst) {
+    if (src.empty()) throw std::invalid_argument("pyrDown: empty source");
+    Mat out((src.rows + 1) / 2, (src.cols + 1) / 2, src.depth(), src.channels());
+    sm_status s;
+    if (src.depth() == CV_8U) {
+        const std::vector<uint8_t> in = src.packed<uint8_t>();
+        s = sm_pyr_down(default_device(), in.data(), src.rows, src.cols, src.channels(), out.data);
+    } else if (src.depth() == CV_32F && src.channels() == 1) {
+        const std::vector<float> in = src.packed<float>();
+        s = sm_pyr_down_f32(default_device(), in.data(), src.rows, src.cols, (float*)out.data);
+    } else {
+        throw std::invalid_argument("pyrDown: u8 (1/3 channels) or 1-channel f32 only");
+    }
+    if (s != SM_OK) throw std::runtime_error(std::string("pyrDown: ") + sm_status_string(s));
+    dst = out;
+}
 
 class StereoMatching {
    public:
-    // static selectors (stereoMatching.h:51-53)
-    inline static std::string costcalculation = "censusGrad";
-    inline static std::string aggregation = "CBCA";
-    inline static std::string optimization = "sgm";
-    // h:70-80 are static const in the reference (compile-time); here they are read at construction
-    inline static bool Do_refine = false;      // h:70
-    static constexpr bool Do_LRConsis = true;  // h:72
-    inline static bool Do_regionVote = true;   // h:75
-    inline static bool Do_properIpol = true;   // h:76
-    inline static bool Do_lastMedianBlur = true;  // h:80
+    // static selectors (h:50-54): declared here, defined once by the program (main_.cpp:15-19)
+    static const std::string root;
+    static std::string costcalculation;
+    static std::string aggregation;
+    static std::string optimization;
+    static std::string object;
+    // compile-time switches (h:57-83); static const in the reference, settable here before a ctor
+    static constexpr bool preMedBlur = false;      // h:66
+    inline static bool Do_refine = false;          // h:70
+    static constexpr bool Do_LRConsis = true;      // h:72
+    inline static bool Do_regionVote = true;       // h:75
+    inline static bool Do_properIpol = true;       // h:76
+    inline static bool Do_lastMedianBlur = true;   // h:80
 
     struct Parameters {  // StereoMatching::Parameters (h:85-351), the fields the hot path reads
         int numDisparities, rows, cols;
         int lamCen, lamG, disSc;
-        int censusFunc = 3;
+        int vmTop_Num, ts;
+        float vmTop_thres;
+        std::string errCsvName;
+        int censusFunc = 3;                   // h:244
         int cbca_iterationNum = 2, cbca_minArmL = 1;
         int cbca_crossL0 = 17, cbca_crossL_out0 = 34, cbca_cTresh0 = 20, cbca_cTresh_out0 = 6;
         int sgm_scanNum = 4, sgm_corDifThres = 15, sgm_reduCoeffi1 = 4;
-        int errorThreshold = 1;
+        int errorThreshold = 1;               // h:225
         float LRmaxDiff = 0;                  // h:212
         int DISP_OCC = -2 * 16;               // h:216
         int region_vote_nums = 2;             // h:306
-        Parameters(int maxDisp, int h, int w, int lamCen_ = 13, int lamG_ = 1, int /*M*/ = 2, int /*lamc*/ = 109,
-                   int /*ts*/ = 10, const std::string& /*errCsvName*/ = "", int disSc_ = 1)
-            : numDisparities(maxDisp + 1), rows(h), cols(w), lamCen(lamCen_), lamG(lamG_), disSc(disSc_) {}
+        // Parameters(maxDisp, h, w, lamCen, lamG, M, lamc, ts, errCsvName, disSc) — main_.cpp:138
+        Parameters(int maxDisp, int h, int w, int lamCen_ = 13, int lamG_ = 1, int M = 2, int lamc = 109,
+                   int ts_ = 10, const std::string& errCsvName_ = "", int disSc_ = 1)
+            : numDisparities(maxDisp + 1), rows(h), cols(w), lamCen(lamCen_), lamG(lamG_), disSc(disSc_),
+              vmTop_Num(M), ts(ts_), vmTop_thres(lamc * 0.01f), errCsvName(errCsvName_) {}
     };
 
+    struct RegionErr {            // one line of calErr's report (h:1798-1799)
+        std::string region;
+        float PBM, RMS;
+    };
+
+    // StereoMatching(I1_c, I2_c, I1_g, I2_g, DT, all_mask, nonocc_mask, disc_mask, param) — cpp:2058;
+    // main_.cpp:139.  DT and the masks are kept (shallow, like the reference's headers) for calErr.
+    StereoMatching(Mat& I1_c, Mat& I2_c, Mat& I1_g, Mat& I2_g, Mat& DT_, Mat& all_mask, Mat& nonocc_mask,
+                   Mat& disc_mask, const Parameters& param, int hip_device = 0)
+        : param_(param), h_(I1_c.rows), w_(I1_c.cols), d_(param.numDisparities) {
+        DT = DT_;
+        I_mask[0] = nonocc_mask;   // cpp:2073-2075
+        I_mask[1] = all_mask;
+        I_mask[2] = disc_mask;
+        init(I1_c, I2_c, I1_g, I2_g, hip_device);
+    }
+    // without ground truth (no calErr)
     StereoMatching(const Mat& I1_c, const Mat& I2_c, const Mat& I1_g, const Mat& I2_g, const Parameters& param,
                    int hip_device = 0)
-        : h_(I1_c.rows), w_(I1_c.cols), d_(param.numDisparities) {
+        : param_(param), h_(I1_c.rows), w_(I1_c.cols), d_(param.numDisparities) {
+        init(I1_c, I2_c, I1_g, I2_g, hip_device);
+    }
+    ~StereoMatching() { sm_destroy(ctx_); }
+    StereoMatching(const StereoMatching&) = delete;
+    StereoMatching& operator=(const StereoMatching&) = delete;
+
+    void costCalculate() { check(sm_cost_calculate(ctx_), "costCalculate"); }
+    void dispOptimize() {  // DP[0] (and DP[1] when Do_refine), cpp:1046-1136
+        DP[0].create(h_, w_, CV_16S);
+        check(sm_disp_optimize(ctx_, DP[0].ptr<int16_t>()), "dispOptimize");
+        if (refine_on_) {
+            DP[1].create(h_, w_, CV_16S);
+            check(sm_get_disp(ctx_, 1, DP[1].ptr<int16_t>()), "DP[1]");
+        }
+    }
+    void refine() {  // cpp:1138-1511; needs Do_refine at construction
+        DP[0].create(h_, w_, CV_16S);
+        check(sm_refine(ctx_, DP[0].ptr<int16_t>()), "refine");
+    }
+    void pipeline() {  // cpp:1950-1981 (no SolveAll)
+        costCalculate();
+        dispOptimize();
+        if (Do_refine) refine();
+    }
+    std::vector<float> volume(int view = 0) {   // public member vm[view] (h:2720)
+        std::vector<float> v((size_t)h_ * w_ * d_);
+        check(sm_get_volume(ctx_, view, v.data()), "vm");
+        return v;
+    }
+
+    // CSV of per-object error ratios (cpp:1940-1948): the rows calErr(.., calCSV = true) appends
+    // are kept in csv() instead of a file under savePath.
+    void openCSV() { csv_open_ = true; }
+    void closeCSV() {
+        if (csv_open_) csv_ << "\n";
+        csv_open_ = false;
+    }
+    const std::string csv() const { return csv_.str(); }
+    // saveTime(ms, procedure) (h:1727-1744): "procedure: ms" records, kept in times()
+    void saveTime(long ms, const std::string& procedure) { times_.push_back(procedure + ": " + std::to_string(ms)); }
+    const std::vector<std::string>& times() const { return times_; }
+
+    // calErr<T>(DP, DT, procedure, calCSV) (h:1748-1825): per region mask (nonocc, all, disc; empty
+    // masks skipped) the bad ratio PBM (DP < 0 or |DT - DP| > errorThreshold) and the RMS, printed
+    // like the reference and returned; the float arithmetic is sm_cal_err's (the reference's order).
+    template <typename T = int16_t>
+    std::vector<RegionErr> calErr(Mat& DP_, Mat& DT_, const std::string& procedure, bool calCSV = false) {
+        static_assert(sizeof(T) == 2, "DP is CV_16S");
+        if (DP_.empty() || DT_.empty() || DT_.depth() != CV_32F || DP_.rows != DT_.rows || DP_.cols != DT_.cols)
+            throw std::invalid_argument("calErr: DP (CV_16S) and DT (CV_32F) of one size required");
+        static const char* names[3] = {"nonocc", "all", "disc"};
+        std::vector<RegionErr> out;
+        const std::vector<int16_t> dp = DP_.packed<int16_t>();
+        const std::vector<float> dt = DT_.packed<float>();
+        for (int region = 0; region < 3; region++) {
+            if (I_mask[region].empty()) continue;
+            const std::vector<uint8_t> m = I_mask[region].packed<uint8_t>();
+            RegionErr e{names[region], 0.f, 0.f};
+            check(sm_cal_err(dp.data(), dt.data(), m.data(), DP_.rows, DP_.cols, (float)param_.errorThreshold, &e.PBM,
+                             &e.RMS),
+                  "calErr");
+            std::cout << "\n" << e.region << "\terrorRatio: " << e.PBM << " epe: " << e.RMS << " " + procedure << "\n";
+            if (calCSV && csv_open_) csv_ << e.PBM << ",";
+            out.push_back(e);
+        }
+        return out;
+    }
+    std::vector<RegionErr> calErr() { return calErr<int16_t>(DP[0], DT, "DP0"); }
+
+    Mat DP[2];        // int16 H x W disparity, -1 = invalid (h:2724)
+    Mat DT;           // ground truth (cpp:2072)
+    Mat I_mask[3];    // nonocc, all, disc (cpp:2073-2075)
+    Parameters param_;
+    int h_, w_, d_;
+    sm_ctx* ctx_ = nullptr;
+
+   private:
+    bool refine_on_ = false, csv_open_ = false;
+    std::ostringstream csv_;
+    std::vector<std::string> times_;
+
+    void init(const Mat& I1_c, const Mat& I2_c, const Mat& I1_g, const Mat& I2_g, int hip_device) {
+        const Parameters& param = param_;
+        if (I1_c.channels() != 3 || I2_c.channels() != 3 || I1_g.channels() != 1 || I2_g.channels() != 1 ||
+            I1_c.depth() != CV_8U || I1_g.depth() != CV_8U)
+            throw std::invalid_argument("expected BGR colour and single-channel gray u8 images");
+        if (I2_c.rows != h_ || I2_c.cols != w_ || I1_g.rows != h_ || I1_g.cols != w_ || I2_g.rows != h_ ||
+            I2_g.cols != w_ || I2_c.step != I1_c.step || I2_g.step != I1_g.step)
+            throw std::invalid_argument("images of one size (and row stride per kind) required");
         sm_params p;
-        sm_params_default(&p, param.numDisparities - 1, I1_c.rows, I1_c.cols);
+        sm_params_default(&p, param.numDisparities - 1, h_, w_);
         p.cost_method = costcalculation == "censusGrad" ? SM_COST_CENSUS_GRAD
                         : costcalculation == "Census"   ? SM_COST_CENSUS
                         : costcalculation == "ADCensus" ? SM_COST_AD_CENSUS
@@ -88,6 +340,7 @@ class StereoMatching {
         p.sgm_paths = param.sgm_scanNum;
         p.sgm_cor_dif_thres = param.sgm_corDifThres;
         p.sgm_redu_coeff = param.sgm_reduCoeffi1;
+        refine_on_ = Do_refine;
         p.do_refine = Do_refine ? 1 : 0;
         p.lr_max_diff = param.LRmaxDiff;
         p.disp_occ = param.DISP_OCC;
@@ -96,40 +349,11 @@ class StereoMatching {
         p.do_proper_ipol = Do_properIpol ? 1 : 0;
         p.do_last_median_blur = Do_lastMedianBlur ? 1 : 0;
         check(sm_create(&ctx_, &p, hip_device), "sm_create");
-        if (I1_c.channels != 3 || I2_c.channels != 3 || I1_g.channels != 1 || I2_g.channels != 1)
-            throw std::invalid_argument("expected BGR colour and single-channel gray images");
         check(sm_set_images(ctx_, I1_c.data, I2_c.data, I1_c.step, I1_g.data, I2_g.data, I1_g.step), "sm_set_images");
     }
-    ~StereoMatching() { sm_destroy(ctx_); }
-    StereoMatching(const StereoMatching&) = delete;
-    StereoMatching& operator=(const StereoMatching&) = delete;
-
-    void costCalculate() { check(sm_cost_calculate(ctx_), "costCalculate"); }
-    void dispOptimize() {  // DP[0] (and DP[1] when Do_refine), cpp:1046-1136
-        DP[0].resize((size_t)h_ * w_);
-        check(sm_disp_optimize(ctx_, DP[0].data()), "dispOptimize");
-        if (Do_refine) {
-            DP[1].resize((size_t)h_ * w_);
-            check(sm_get_disp(ctx_, 1, DP[1].data()), "DP[1]");
-        }
-    }
-    void refine() {  // cpp:1138-1511; needs Do_refine at construction
-        DP[0].resize((size_t)h_ * w_);
-        check(sm_refine(ctx_, DP[0].data()), "refine");
-    }
-    std::vector<float> volume(int view = 0) {
-        std::vector<float> v((size_t)h_ * w_ * d_);
-        check(sm_get_volume(ctx_, view, v.data()), "vm");
-        return v;
-    }
-
-    std::vector<int16_t> DP[2];  // DP[0]: int16 H x W disparity, -1 = invalid (h:2724)
-    int h_, w_, d_;
-    sm_ctx* ctx_ = nullptr;
-
-   private:
     void check(sm_status s, const char* what) {
-        if (s != SM_OK) throw std::runtime_error(std::string(what) + ": " + sm_last_error(ctx_));
+        if (s != SM_OK)
+            throw std::runtime_error(std::string(what) + ": " + (ctx_ ? sm_last_error(ctx_) : sm_status_string(s)));
     }
     friend void SolveAll(StereoMatching** smPyr, int PY_LVL, float REG_LAMBDA);
 };
@@ -144,18 +368,6 @@ inline void SolveAll(StereoMatching** smPyr, int PY_LVL, float REG_LAMBDA) {
     std::vector<sm_ctx*> lv;
     for (int i = 0; i < PY_LVL; i++) lv.push_back(smPyr[i]->ctx_);
     smPyr[0]->check(sm_solve_all_pyr(lv.data(), PY_LVL, REG_LAMBDA), "SolveAll");
-}
-
-// cv::pyrDown for u8 images (main_.cpp:145-148) on the GPU; returns the (rows+1)/2 x (cols+1)/2 image.
-inline std::vector<uint8_t> pyrDown(const Mat& src, int hip_device = 0) {
-    std::vector<uint8_t> in((size_t)src.rows * src.cols * src.channels);
-    for (int r = 0; r < src.rows; r++)
-        std::copy(src.data + (size_t)r * src.step, src.data + (size_t)r * src.step + (size_t)src.cols * src.channels,
-                  in.begin() + (size_t)r * src.cols * src.channels);
-    std::vector<uint8_t> out((size_t)((src.rows + 1) / 2) * ((src.cols + 1) / 2) * src.channels);
-    if (sm_pyr_down(hip_device, in.data(), src.rows, src.cols, src.channels, out.data()) != SM_OK)
-        throw std::runtime_error("pyrDown failed");
-    return out;
 }
 
 }  // namespace smamd

@@ -38,6 +38,7 @@ class sm_params(C.Structure):
         ("do_refine", C.c_int32), ("lr_max_diff", C.c_float), ("do_region_vote", C.c_int32),
         ("region_vote_nums", C.c_int32), ("rv_ratio", C.c_float), ("rv_s", C.c_int32),
         ("do_proper_ipol", C.c_int32), ("disp_occ", C.c_int32), ("do_last_median_blur", C.c_int32),
+        ("sub_batch", C.c_int32), ("num_streams", C.c_int32), ("fuse_norm_scan", C.c_int32),
     ]
 
 
@@ -56,6 +57,7 @@ SIGNATURES = [
     ("sm_disp_optimize", C.c_int, [_P, _P]),
     ("sm_solve_all_pyr", C.c_int, [C.POINTER(_P), C.c_int32, C.c_float]),
     ("sm_pyr_down", C.c_int, [C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32, _P]),
+    ("sm_pyr_down_f32", C.c_int, [C.c_int32, _P, C.c_int32, C.c_int32, _P]),
     ("sm_refine", C.c_int, [_P, _P]),
     ("sm_get_disp", C.c_int, [_P, C.c_int32, _P]),
     ("sm_set_disp", C.c_int, [_P, C.c_int32, _P]),

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <new>
 #include <string>
@@ -64,8 +65,8 @@ struct sm_ctx {
     float lut_a[1024], lut_b[1024];
     float ad_oor_exp = 0;
     bool fuse_norm_scan = false;
-    int sub_batch = 0;          // SM_SUB_BATCH=k: run sm_run in groups of k pairs (0 = all)
-    int nstreams = 1;           // SM_STREAMS=s: groups alternate over s streams (staggered, see sm_run)
+    int sub_batch = 0;          // sm_params.sub_batch: run sm_run in groups of k pairs (0 = all)
+    int nstreams = 1;           // sm_params.num_streams: groups alternate over s streams (see sm_run)
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
     std::vector<hipEvent_t> xev;                        // stagger / join events
     // profiling
@@ -151,6 +152,8 @@ int n_views(const sm_params& p) { return p.do_refine ? 2 : 1; }   // imgNum = Do
 
 int cbca_lag(const sm_params& p) { return p.arm_l_out > p.arm_min_l ? p.arm_l_out : p.arm_min_l; }
 
+bool nonneg(float x) { return x >= 0 && !std::signbit(x); }   // >= +0 (rejects NaN and -0.0)
+
 sm_status validate(const sm_params& p, std::string& why) {
     auto bad = [&](const char* m) { why = m; return SM_EINVAL; };
     if (p.rows < 2 || p.cols < 2) return bad("rows and cols must be >= 2 (calGrad reads I[1] and I[w-2])");
@@ -167,13 +170,16 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (p.sgm_paths < 1 || p.sgm_paths > 8) return bad("sgm_paths must be in [1, 8]");
     if (p.sgm_redu_coeff == 0) return bad("sgm_redu_coeff must be non-zero");
     if (p.batch_capacity < 1) return bad("batch_capacity must be >= 1");
+    if (p.sub_batch < 0 || p.num_streams < 0 || p.num_streams > 4) return bad("sub_batch >= 0 and num_streams in [0, 4] required");
     // The kernels rely on every cost and path cost being >= +0 (SGM and WTA minima compare float
     // bit patterns as unsigned integers, sm_device.h), which these constants guarantee: fusion
     // terms 2 - exp(-C / lam) - exp(-G / lam) with C, G >= 0, truncations >= 0, P1, P2 >= 0.
     if (!(p.lam_cen > 0) || !(p.lam_g > 0) || !(p.lam_ad > 0) || !(p.lam_cen_adc > 0))
         return bad("fusion lambdas must be > 0");
-    if (!(p.grad_trunc >= 0) || !(p.ad_trunc_adc >= 0) || !(p.ad_trunc_ad >= 0)) return bad("truncations must be >= 0");
-    if (!(p.sgm_p1 >= 0) || !(p.sgm_p2 >= 0) || p.sgm_redu_coeff < 0) return bad("SGM penalties must be >= 0");
+    // -0.0 passes `>= 0` but its bit pattern 0x80000000 ranks above every positive cost in those
+    // unsigned minima (the reference's std::min would treat it as 0), so it is rejected as well
+    if (!nonneg(p.grad_trunc) || !nonneg(p.ad_trunc_adc) || !nonneg(p.ad_trunc_ad)) return bad("truncations must be >= +0");
+    if (!nonneg(p.sgm_p1) || !nonneg(p.sgm_p2) || p.sgm_redu_coeff < 0) return bad("SGM penalties must be >= +0");
     if (p.do_refine) {
         if (!(p.rv_ratio > 0)) return bad("rv_ratio must be > 0");
         if (p.disp_occ == -32768) return bad("disp_occ = -32768 is reserved (properIpol's outside-the-image mark)");
@@ -576,6 +582,9 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->do_proper_ipol = 1;      // h:76
     p->disp_occ = -2 * 16;      // h:216
     p->do_last_median_blur = 1; // h:80
+    p->sub_batch = 0;
+    p->num_streams = 1;
+    p->fuse_norm_scan = 0;
 }
 
 const char* sm_status_string(sm_status s) {
@@ -642,14 +651,9 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->px, 3 * cap * 2 * c->npix))) return s;
     build_luts(c);
     {
-        const char* e = getenv("SM_FUSE_NORM_SCAN");
-        c->fuse_norm_scan = e && e[0] == '1';
-        const char* sb = getenv("SM_SUB_BATCH");
-        c->sub_batch = sb ? atoi(sb) : 0;
-        const char* ns = getenv("SM_STREAMS");
-        c->nstreams = ns ? atoi(ns) : 1;
-        if (c->nstreams < 1) c->nstreams = 1;
-        if (c->nstreams > 4) c->nstreams = 4;
+        c->fuse_norm_scan = p->fuse_norm_scan != 0;
+        c->sub_batch = p->sub_batch;
+        c->nstreams = p->num_streams < 1 ? 1 : p->num_streams;
         for (int i = 0; i + 1 < c->nstreams; i++) HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking));
         for (int i = 0; i < 16; i++) {
             hipEvent_t e;
@@ -811,6 +815,24 @@ sm_status sm_pyr_down(int32_t dev, const uint8_t* src, int32_t rows, int32_t col
     return e == hipSuccess ? SM_OK : SM_EHIP;
 }
 
+sm_status sm_pyr_down_f32(int32_t dev, const float* src, int32_t rows, int32_t cols, float* dst) {
+    if (!src || !dst || rows < 1 || cols < 1) return SM_EINVAL;
+    if (hipSetDevice(dev) != hipSuccess) return SM_EHIP;
+    const size_t in = (size_t)rows * cols * 4, out = (size_t)((rows + 1) / 2) * ((cols + 1) / 2) * 4;
+    float *dsrc = nullptr, *ddst = nullptr;
+    hipError_t e = hipMalloc((void**)&dsrc, in);
+    if (e == hipSuccess) e = hipMalloc((void**)&ddst, out);
+    if (e == hipSuccess) e = hipMemcpy(dsrc, src, in, hipMemcpyDefault);
+    if (e == hipSuccess) {
+        sm::launch_pyr_down_f32(dsrc, ddst, rows, cols, nullptr);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(dst, ddst, out, hipMemcpyDefault);
+    if (dsrc) hipFree(dsrc);
+    if (ddst) hipFree(ddst);
+    return e == hipSuccess ? SM_OK : SM_EHIP;
+}
+
 sm_status sm_disp_optimize(sm_ctx* c, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
@@ -933,7 +955,11 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
         const int m2 = n - off < g ? n - off : g;
         const Bufs B = at(c, off);
         c->st = (ns > 1 && k % ns) ? c->xst[k % ns - 1] : main_st;
-        if (ns > 1 && k > 0) hipStreamWaitEvent(c->st, c->xev[1 + (k - 1) % 8], 0);
+        hipError_t e = hipSuccess;
+        if (ns > 1 && k > 0 && (e = hipStreamWaitEvent(c->st, c->xev[1 + (k - 1) % 8], 0)) != hipSuccess) {
+            s_out = hip_fail(c, e, "hipStreamWaitEvent (group stagger)");
+            break;
+        }
         if ((s_out = run_prep(c, m2, B))) break;
         if ((s_out = run_cost(c, m2, 0, B))) break;
         if (right_view(c->p) && (s_out = run_cost(c, m2, 1, B))) break;
@@ -944,16 +970,24 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
                 s_out = run_scale(c, m2, v, w, B);
         }
         if (s_out) break;
-        if (ns > 1) hipEventRecord(c->xev[1 + k % 8], c->st);
+        if (ns > 1 && (e = hipEventRecord(c->xev[1 + k % 8], c->st)) != hipSuccess) {
+            s_out = hip_fail(c, e, "hipEventRecord (group CBCA done)");
+            break;
+        }
         for (int v = 0; v < n_views(c->p) && !s_out; v++) s_out = run_optimize(c, m2, v, B);
         if (s_out) break;
         if (c->p.do_refine && (s_out = run_refine(c, m2, B))) break;
     }
     c->st = main_st;
-    if (ns > 1) {
+    if (ns > 1) {   // the join runs on the error path too: nothing stays queued behind the main stream
         for (int i = 0; i + 1 < ns; i++) {
-            hipEventRecord(c->xev[9 + i], c->xst[i]);
-            hipStreamWaitEvent(main_st, c->xev[9 + i], 0);
+            hipError_t e = hipEventRecord(c->xev[9 + i], c->xst[i]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(main_st, c->xev[9 + i], 0);
+            if (e != hipSuccess) {
+                // a failed join: drain the side stream on the host so its groups cannot race later work
+                hipStreamSynchronize(c->xst[i]);
+                if (!s_out) s_out = hip_fail(c, e, "stream join");
+            }
         }
     }
     if (s_out) return s_out;

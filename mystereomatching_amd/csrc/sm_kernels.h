@@ -106,6 +106,7 @@ void launch_proper_ipol(const int16_t* src, int16_t* dst, const uint32_t* px, in
                         hipStream_t st);
 void launch_so(const SoArgs& a, hipStream_t st);
 void launch_pyr_down(const uint8_t* src, uint8_t* dst, int rows, int cols, int ch, hipStream_t st);
+void launch_pyr_down_f32(const float* src, float* dst, int rows, int cols, hipStream_t st);
 void launch_solve_all_pyr(const PyrArgs& a, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int n, int H, int W, hipStream_t st);
 int sgm_k_for(int D);

@@ -45,6 +45,30 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
     }
 }
 
+// cv::pyrDown on a 1-channel f32 image (main_.cpp:149: the ground truth DT goes down the pyramid
+// with the inputs).  OpenCV's scalar pyrDown_ (FltCast<float, 8>) order, restated: the row pass
+// r = s0*6 + (s-1 + s+1)*4 + s-2 + s+2 (left to right), the column pass the same over the five row
+// sums, then * (1/256) (exact: a power of two).  OpenCV's SIMD rows may fuse multiply-adds, so the
+// last bit is unpinned; only the evaluator reads DT, never the disparity path.
+__global__ __launch_bounds__(256) void k_pyr_down_f32(const float* __restrict__ src, float* __restrict__ dst, int rows,
+                                                      int cols) {
+    const int dr = (rows + 1) / 2, dc = (cols + 1) / 2;
+    const size_t total = (size_t)dr * dc;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % dc), y = (int)(i / dc);
+        int cx[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) cx[j] = reflect101(2 * x + j - 2, cols);
+        float r[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float* row = src + (size_t)reflect101(2 * y + k - 2, rows) * cols;
+            r[k] = row[cx[2]] * 6.f + (row[cx[1]] + row[cx[3]]) * 4.f + row[cx[0]] + row[cx[4]];
+        }
+        dst[i] = (r[2] * 6.f + (r[1] + r[3]) * 4.f + r[0] + r[4]) * (1.f / 256.f);
+    }
+}
+
 // one wave per level-0 pixel (grid-stride), lanes over disparities; levels read in order
 __global__ __launch_bounds__(256) void k_solve_all_pyr(const PyrArgs a) {
     const int lane = threadIdx.x & 63;
@@ -80,6 +104,14 @@ void launch_pyr_down(const uint8_t* src, uint8_t* dst, int rows, int cols, int c
     if (blocks > 8192) blocks = 8192;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(k_pyr_down, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, rows, cols, ch);
+}
+
+void launch_pyr_down_f32(const float* src, float* dst, int rows, int cols, hipStream_t st) {
+    const size_t total = (size_t)((rows + 1) / 2) * ((cols + 1) / 2);
+    size_t blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_pyr_down_f32, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, rows, cols);
 }
 
 void launch_solve_all_pyr(const PyrArgs& a, hipStream_t st) {

@@ -228,12 +228,22 @@ def SolveAll(smPyr: Sequence[StereoMatching], PY_LVL: int, REG_LAMBDA: float):
 
 
 def pyrDown(img, device: int = 0) -> np.ndarray:
-    """cv::pyrDown for u8 H x W or H x W x 3 images (main_.cpp:145-148), on the GPU."""
+    """cv::pyrDown (main_.cpp:145-154), on the GPU: u8 H x W or H x W x 3 images (the inputs and
+    masks) or a float32 H x W image (the ground truth DT, main_.cpp:149)."""
+    lib = _capi.load()
+    if np.asarray(img).dtype == np.float32:
+        a = np.ascontiguousarray(img, np.float32)
+        if a.ndim != 2:
+            raise ValueError("float pyrDown takes a 1-channel image")
+        rows, cols = a.shape
+        out = np.empty(((rows + 1) // 2, (cols + 1) // 2), np.float32)
+        st = lib.sm_pyr_down_f32(device, _capi.ptr(a), rows, cols, _capi.ptr(out))
+        _capi.check(lib, None, st, "pyrDown")
+        return out
     a = np.ascontiguousarray(img, np.uint8)
     rows, cols = a.shape[:2]
     ch = 1 if a.ndim == 2 else a.shape[2]
     out = np.empty(((rows + 1) // 2, (cols + 1) // 2) + a.shape[2:], np.uint8)
-    lib = _capi.load()
     st = lib.sm_pyr_down(device, _capi.ptr(a), rows, cols, ch, _capi.ptr(out))
     _capi.check(lib, None, st, "pyrDown")
     return out

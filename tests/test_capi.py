@@ -49,6 +49,7 @@ def test_params_struct_layout_and_defaults():
     assert (p.do_refine, p.lr_max_diff, p.do_region_vote, p.region_vote_nums, p.rv_s) == (0, 0.0, 1, 2, 20)
     assert (p.do_proper_ipol, p.disp_occ, p.do_last_median_blur) == (1, -32, 1)
     assert np.float32(p.rv_ratio) == np.float32(0.4)
+    assert (p.sub_batch, p.num_streams, p.fuse_norm_scan) == (0, 1, 0)
 
 
 @pytest.mark.parametrize("field,value,msg", [
@@ -56,7 +57,9 @@ def test_params_struct_layout_and_defaults():
     ("census_rv", 7, b"census"), ("arm_l_out", 200, b"arm"), ("sgm_paths", 9, b"sgm_paths"),
     ("batch_capacity", 0, b"batch"), ("cost_method", 7, b"cost_method"), ("lam_cen", 0.0, b"lambda"),
     ("lam_g", -1.0, b"lambda"), ("grad_trunc", -5.0, b"truncation"), ("sgm_p2", -1.0, b"penalties"),
-    ("sgm_redu_coeff", -4, b"penalties"),
+    ("sgm_redu_coeff", -4, b"penalties"), ("sgm_p2", -0.0, b"penalties"), ("sgm_p1", -0.0, b"penalties"),
+    ("grad_trunc", -0.0, b"truncation"), ("ad_trunc_ad", -0.0, b"truncation"), ("num_streams", 5, b"num_streams"),
+    ("sub_batch", -1, b"sub_batch"),
 ])
 def test_validation_rejects_before_device(field, value, msg):
     lib = _capi.load()

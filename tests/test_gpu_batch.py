@@ -47,3 +47,19 @@ def test_runner_single_rank_hip(oracle):
         np.testing.assert_array_equal(got, _oracle_maps(oracle, batch, H, W, md))
     finally:
         fn.close()
+
+
+@pytest.mark.parametrize("sub_batch,num_streams", [(2, 2), (1, 3), (2, 1)])
+def test_multi_stream_sub_batches(oracle, sub_batch, num_streams):
+    """sm_params.sub_batch / num_streams only reschedule sm_run: groups of pairs alternate over
+    side streams with the stagger / join events; the maps must equal the oracle's."""
+    H, W, md, n = 37, 53, 19, 5
+    batch = S.make_batch(n, H, W, md + 1, first_index=340)
+    sb = StereoBatch(md, H, W, n, device=0, sub_batch=sub_batch, num_streams=num_streams)
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        first = sb.run(0.3)
+        np.testing.assert_array_equal(first, _oracle_maps(oracle, batch, H, W, md))
+        np.testing.assert_array_equal(sb.run(0.3), first)
+    finally:
+        sb.close()

@@ -19,6 +19,38 @@ def test_pyr_down(oracle, shape):
     np.testing.assert_array_equal(pyrDown(img), oracle.pyr_down(img))
 
 
+def _pyr_down_f32_ref(a):
+    """OpenCV's scalar pyrDown_ order for float (FltCast<float, 8>): row pass then column pass,
+    s0*6 + (s-1 + s+1)*4 + s-2 + s+2, then * 1/256; BORDER_REFLECT_101 (last bit unpinned)."""
+    a = a.astype(np.float32)
+    H, W = a.shape
+    ry = np.array([abs(i) if i < 0 else (2 * H - 2 - i if i >= H else i) for i in range(-2, 2 * ((H + 1) // 2) + 1)])
+    rx = np.array([abs(i) if i < 0 else (2 * W - 2 - i if i >= W else i) for i in range(-2, 2 * ((W + 1) // 2) + 1)])
+    if H == 1:
+        ry[:] = 0
+    if W == 1:
+        rx[:] = 0
+    dc, dr = (W + 1) // 2, (H + 1) // 2
+    cx = [rx[2 * np.arange(dc) + j] for j in range(5)]
+    f6, f4 = np.float32(6), np.float32(4)
+    rows = []
+    for y in range(dr):
+        r = []
+        for k in range(5):
+            row = a[ry[2 * y + k]]
+            r.append(row[cx[2]] * f6 + (row[cx[1]] + row[cx[3]]) * f4 + row[cx[0]] + row[cx[4]])
+        rows.append((r[2] * f6 + (r[1] + r[3]) * f4 + r[0] + r[4]) * np.float32(1 / 256))
+    return np.stack(rows).astype(np.float32)
+
+
+@pytest.mark.parametrize("shape", [(375, 450), (21, 34), (3, 5), (188, 225)])
+def test_pyr_down_f32(shape):
+    """pyrDown(DT, DT) of the float ground truth (main_.cpp:149)."""
+    rng = np.random.default_rng(sum(shape))
+    img = (rng.integers(0, 256, size=shape).astype(np.float32) * np.float32(1 / 3))
+    np.testing.assert_array_equal(pyrDown(img), _pyr_down_f32_ref(img))
+
+
 def run_pyramid(pair, max_disp, L, refine=False):
     """main_.cpp:131-166 through the mirror API."""
     StereoMatching.costcalculation, StereoMatching.aggregation, StereoMatching.optimization = "censusGrad", "CBCA", "sgm"

@@ -65,6 +65,7 @@ struct sm_ctx {
     float lut_a[1024], lut_b[1024];
     float ad_oor_exp = 0;
     bool fuse_norm_scan = false;
+    int num_cu = 256;           // compute units of the device
     int sub_batch = 0;          // sm_params.sub_batch: run sm_run in groups of k pairs (0 = all)
     int nstreams = 1;           // sm_params.num_streams: groups alternate over s streams (see sm_run)
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
@@ -375,6 +376,7 @@ sm_status run_cbca(sm_ctx* c, int n, int view, bool fuse_scale, float w, const B
     a.arms_end = (const uint32_t*)(c->arms + c->arms_bytes);
     a.scale = w;
     a.apply_scale = 0;
+    a.num_cu = c->num_cu;
     const double bytes = (double)n * c->nvol * 8.0;
     // profile names: "cbca_h_scan" etc. for vm[0], "cbca_h_scan_r" etc. for vm[1]
     std::string sfx = view == 0 ? "" : "_r";
@@ -606,6 +608,8 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     *out = c;  // returned even on failure so sm_last_error works; caller must sm_destroy
     c->p = *p;
     c->device = hip_device;
+    if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess || c->num_cu < 1)
+        c->num_cu = 256;
     std::string why;
     if (validate(c->p, why) != SM_OK) return fail(c, SM_EINVAL, why);
     int ndev = 0;

@@ -30,6 +30,7 @@
 // current tile is processed; inside a steady-state tile all ring writes precede all ring reads,
 // so a tile costs one or two LDS round trips.  Rings hold 2*lag + T + 1 slots.
 #include <float.h>
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -101,31 +102,69 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #ifndef SM_CB_WIN_RING
 #define SM_CB_WIN_RING 1
 #endif
+#ifndef SM_CB_PROBE_NOVG
+#define SM_CB_PROBE_NOVG 0   // timing probe only (wrong results): V sweeps skip the other image's arm gather
+#endif
 __host__ __device__ constexpr int cbca_win_ring(int T) { return 63 + T; }
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
     return mode == CB_SCAN ? (horiz ? SM_CB_T_SCAN_H : SM_CB_T_SCAN_V)
                            : (mode == CB_NORM ? (horiz ? SM_CB_T_NORM_H : SM_CB_T_NORM_V) : 8);
 }
-template <bool HORIZ, int MODE>
+// V sweeps as workgroups of KW waves on KW adjacent columns of one 64-disparity chunk
+// (SM_CB_VGROUP): per tile the workgroup stages, for each arm set and row, the KW own-image words
+// and the KW + 63 other-image words its lanes pair with (lane d of column u0 + w reads the
+// other image at u0 + w - d, i.e. span index w + 63 - d) in LDS with one coalesced load per
+// thread, instead of every wave gathering 64 words per row and set (the same words, shifted by
+// one column, as its neighbours: full resolution, probe without the gather: v_norm 7.29 ->
+// 5.5 ms, v_scan 5.56 -> 4.6-5.1 ms).  Staging is double-buffered, one barrier per tile.
+// KW waves share one CU's LDS with their rings, so the normalising sweep runs T = 7 (ring 77
+// slots) to fit five waves; the host falls back to KW = 1 when the rings of a larger lag do not fit.
+// Measured (full resolution, same box): v_scan 5.57 -> 5.69 ms, v_norm 7.30 -> 11.07 ms — the
+// extra LDS round trip for the staged words on the tile's critical path and the per-tile barrier
+// of five lock-stepped waves cost more than the gathers; kept as a switch, off.
+#ifndef SM_CB_VGROUP
+#define SM_CB_VGROUP 0   // measured slower (see above): off
+#endif
+#ifndef SM_CB_KW_SCAN
+#define SM_CB_KW_SCAN 6
+#endif
+#ifndef SM_CB_KW_NORM
+#define SM_CB_KW_NORM 5
+#endif
+#ifndef SM_CB_T_NORM_VG
+#define SM_CB_T_NORM_VG 7
+#endif
+__host__ __device__ constexpr int cbca_kw(bool horiz, int mode) {
+    return (horiz || !SM_CB_VGROUP || mode == CB_NORM_SCAN) ? 1 : (mode == CB_SCAN ? SM_CB_KW_SCAN : SM_CB_KW_NORM);
+}
+// staged words per set and row: KW own + KW + 63 other
+__host__ __device__ constexpr int cbca_spw(int kw) { return 2 * kw + 63; }
+
+template <bool HORIZ, int MODE, int KW = 1>
 struct CbCfg {
-    static constexpr int T = cbca_tile(HORIZ, MODE);
+    static constexpr int T = (KW > 1 && MODE == CB_NORM) ? SM_CB_T_NORM_VG : cbca_tile(HORIZ, MODE);
     static constexpr int PF = MODE == CB_SCAN ? (HORIZ ? SM_CB_PF_SCAN_H : SM_CB_PF_SCAN_V)
                                               : (MODE == CB_NORM ? (HORIZ ? SM_CB_PF_NORM_H : SM_CB_PF_NORM_V) : (HORIZ ? 2 : 1));
     // arm sets: 0 = pass pair at i (= j - lag), 1 = perpendicular pair at j, 2 = pass pair at j - 2 lag
     static constexpr int NSETS = MODE == CB_SCAN ? 1 : (MODE == CB_NORM ? 2 : 3);
+    static constexpr int NW = KW > 1 ? NSETS * T * cbca_spw(KW) : 0;          // staged words per tile
+    static constexpr int NV = KW > 1 ? (NW + 64 * KW - 1) / (64 * KW) : 1;   // per thread
 };
 
 // ring slots: >= 2*lag + T + 1 (a whole tile is written before any of it is read) and a multiple
 // of T (a tile's write slots never wrap)
-__host__ __device__ inline int cbca_ring(int lag, bool horiz, int mode) {
-    const int T = cbca_tile(horiz, mode);
+__host__ __device__ inline int cbca_tile_kw(bool horiz, int mode, int kw) {
+    return (kw > 1 && mode == CB_NORM) ? SM_CB_T_NORM_VG : cbca_tile(horiz, mode);
+}
+__host__ __device__ inline int cbca_ring(int lag, bool horiz, int mode, int kw = 1) {
+    const int T = cbca_tile_kw(horiz, mode, kw);
     return (2 * lag + T + 1 + T - 1) / T * T;
 }
 // dynamic LDS in 4-byte words: S ring(s) of ring x 64 floats, then the u16 area ring (6 bytes
 // per slot and lane; 8-byte {S, area} records were measured slower: one wave less per CU), then
 // the staged arm words of one tile (SM_CB_LDS_WIN): per set T own words [+ 64 + T - 1 span words]
-__host__ __device__ inline int cbca_ring_words(int lag, bool horiz, int mode) {
-    const int ring = cbca_ring(lag, horiz, mode);
+__host__ __device__ inline int cbca_ring_words(int lag, bool horiz, int mode, int kw = 1) {
+    const int ring = cbca_ring(lag, horiz, mode, kw);
     const int floats = mode == CB_NORM_SCAN ? 2 : 1;
     const int u16s = mode == CB_SCAN ? 0 : 1;
     return ring * 64 * floats + ring * 32 * u16s;
@@ -139,24 +178,34 @@ __host__ __device__ inline int cbca_win_words(bool horiz, int mode) {
 __host__ __device__ inline int cbca_smem_words(int lag, bool horiz, int mode) {
     return cbca_ring_words(lag, horiz, mode) + cbca_win_words(horiz, mode);
 }
+// V-group launch: KW rings, then two staging buffers
+__host__ __device__ inline int cbca_smem_words_vg(int lag, int mode, int kw) {
+    const int T = cbca_tile_kw(false, mode, kw);
+    const int nsets = mode == CB_SCAN ? 1 : 2;
+    return kw * cbca_ring_words(lag, false, mode, kw) + 2 * nsets * T * cbca_spw(kw);
+}
 
-template <bool HORIZ, int T, int NSETS>
+template <bool HORIZ, int T, int NSETS, int KW, int NV>
 struct CbTile {
     float x[T];                          // vm at positions j0 .. j0+T-1
-    uint32_t a0[NSETS];                  // lane k < T: left arm pair at position (j0 + k - off)
+    uint32_t a0[KW > 1 ? 1 : NSETS];     // lane k < T: left arm pair at position (j0 + k - off)
     uint32_t a1v[NSETS];                 // H: lane k < T: right arm pair at position (j0 + k - off)
     uint32_t a1w[SM_CB_LDS_WIN && HORIZ ? NSETS : 1][2];  // H, LDS window: the other image's span
-    uint32_t a1[HORIZ ? 1 : NSETS][T];   // V: right arm pair at (row j0 + k - off, u - d)
+    uint32_t a1[HORIZ || KW > 1 ? 1 : NSETS][T];   // V: right arm pair at (row j0 + k - off, u - d)
+    uint32_t sv[NV];                     // V group: this thread's staged words of the tile
 };
 
 // RV: the right view's volume vm[1] (cbca_core's LOR = 1, run when Do_refine): the pixel's own
 // arms are the right image's, and lane d pairs them with the LEFT image's arms at u + d
 // (HVL_INTERSECTION[1], cpp:2794-2845) — zero once u + d >= W.
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW = 1>
 struct CbLine {
-    static constexpr int T = CbCfg<HORIZ, MODE>::T;
-    static constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
-    using Tile = CbTile<HORIZ, T, NSETS>;
+    static constexpr int T = CbCfg<HORIZ, MODE, KW>::T;
+    static constexpr int NSETS = CbCfg<HORIZ, MODE, KW>::NSETS;
+    static constexpr int NW = CbCfg<HORIZ, MODE, KW>::NW;
+    static constexpr int NV = CbCfg<HORIZ, MODE, KW>::NV;
+    static constexpr int SPW = cbca_spw(KW);
+    using Tile = CbTile<HORIZ, T, NSETS, KW, NV>;
 
     // Volume and V-sweep arm accesses are buffer instructions: the tile's first position in the
     // resource base, lane + k * stride in a loop-invariant VGPR.  Loads are not clamped: the
@@ -187,6 +236,17 @@ struct CbLine {
     float* r2;
     uint16_t* ra;
     float scale;
+    // V group (KW > 1)
+    int wv;                   // wave index in the workgroup = column u0 + wv
+    bool active;              // column < W (the last group's spare waves only keep the barriers)
+    int H;                    // rows (staged rows outside [0, H) read 0)
+    uint32_t rowb;            // bytes per arm-plane row
+    __amdgpu_buffer_rsrc_t Ar;   // the pair's four arm planes
+    uint32_t sboff[NV];       // staged word m: plane + column byte offset
+    int skoff[NV];            // staged word m: row offset from the tile's first position
+    uint32_t sok;             // bit m: word m exists and its column lies inside the image
+    uint32_t* stg;            // two staging buffers of NW words
+    int sbuf;                 // buffer of the current tile
 
     __device__ __forceinline__ int set_off(int s) const { return s == 0 ? lag : (s == 1 ? 0 : 2 * lag); }
     __device__ __forceinline__ static int clampi(int k, int n) { return k < 0 ? 0 : (k >= n ? n - 1 : k); }
@@ -201,6 +261,7 @@ struct CbLine {
         return buf_rsrc(base, room <= 0 ? 0 : (room > 0x7fffffffL ? 0x7fffffff : (int)room));
     }
     __device__ __forceinline__ void store_tile(const __amdgpu_buffer_rsrc_t& r, int k, float v) const {
+        if (KW > 1 && !active) return;
         if (FULL)
             buf_st(r, xo[k], 0, v);
         else
@@ -218,6 +279,16 @@ struct CbLine {
         // for the right image's arms that is the reference's zeroed intersection when u - d < 0.
         // The offset is a select, never a wrapped negative sum: the range check does not wrap,
         // and the compiler would otherwise move constant parts of a sum into the immediate field.
+        if constexpr (KW > 1) {
+            // the workgroup's staged words of this tile: one coalesced dword per thread and word
+#pragma unroll
+            for (int m = 0; m < NV; m++) {
+                const int row = j0 + skoff[m];
+                const bool ok = ((sok >> m) & 1u) && (unsigned)row < (unsigned)H;
+                t.sv[m] = buf_ld_u32(Ar, ok ? sboff[m] + (uint32_t)row * rowb : 0x80000000u, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             const int base = j0 - set_off(s);
@@ -246,7 +317,7 @@ struct CbLine {
             } else {
                 const __amdgpu_buffer_rsrc_t ra1 = bounded_rsrc(A1v[s] + (long)base * (long)(pstride * 4), aend);
 #pragma unroll
-                for (int k = 0; k < T; k++) t.a1[s][k] = buf_ld_u32(ra1, ao[k], 0);
+                for (int k = 0; k < T; k++) t.a1[s][k] = SM_CB_PROBE_NOVG ? 0x00110011u : buf_ld_u32(ra1, ao[k], 0);
             }
         }
     }
@@ -264,6 +335,11 @@ struct CbLine {
 
     // intersection arm pair of set s at tile position k
     __device__ __forceinline__ uint32_t isect(const Tile& t, int s, int k) const {
+        if constexpr (KW > 1) {
+            // own word: broadcast; other word: span index wv + 63 - d (left) / wv + d (right view)
+            const uint32_t* row = stg + sbuf * NW + (s * T + k) * SPW;
+            return pkmin(row[wv], row[KW + (RV ? wv + lane : wv + 63 - lane)]);
+        }
         if (SM_CB_LDS_WIN) {
             const uint32_t a0 = wown[s * T + k];   // broadcast read
             const uint32_t a1 = HORIZ ? (SM_CB_WIN_RING ? wspan[s * 2 * cbca_win_ring(T) + wrs + (RV ? k + lane : k + 63 - lane)]
@@ -277,6 +353,17 @@ struct CbLine {
     }
     // stage the tile's arm words in LDS (one wave: its LDS accesses complete in order)
     __device__ __forceinline__ void stage(const Tile& t) {
+        if constexpr (KW > 1) {
+            // the other buffer was last read in the previous tile, before every wave passed that
+            // tile's barrier, so one barrier per tile orders both reuse hazards
+            sbuf ^= 1;
+            const int tid = wv * 64 + lane;
+#pragma unroll
+            for (int m = 0; m < NV; m++)
+                if (m * 64 * KW + tid < NW) stg[sbuf * NW + m * 64 * KW + tid] = t.sv[m];
+            __syncthreads();
+            return;
+        }
         if (!SM_CB_LDS_WIN) return;
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
@@ -422,20 +509,51 @@ struct CbLine {
     }
 };
 
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV>
-__global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
-    extern __shared__ float smem[];
-    CbLine<HORIZ, MODE, FULL, SCALE, RV> L;
-    constexpr int T = CbCfg<HORIZ, MODE>::T;
-    constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
-    L.lane = threadIdx.x;
+// Persistent V sweeps (SM_CB_PERSIST_V): the grid is the number of blocks that fit the chip at
+// once and block i runs lines i, i + grid, i + 2 grid, ...  All resident waves then start their
+// k-th line together, so the waves of neighbouring columns (one XCD, see xcd_swizzle) walk down
+// the rows in near lockstep and share the other image's arm rows through the XCD's L2.  With one
+// block per line, blocks of later dispatch waves start whenever a slot frees, neighbours drift
+// apart and the 64-word arm gathers of every row miss L2.  Measured at full resolution (same
+// box, FETCH_SIZE x 2 per launch): the fetched bytes did not fall (v_norm 20.8 -> 22.2 GB) and the
+// sweeps got slower (v_norm 7.35 -> 7.85 ms, v_scan 5.6 -> 6.0 ms): off.
+#ifndef SM_CB_PERSIST_V
+#define SM_CB_PERSIST_V 0
+#endif
+// What did cut the gathers' misses is the block order: chunk-major V sweeps (below) put one
+// chunk's consecutive columns on an XCD at a time, and neighbouring columns' other-image spans
+// overlap in all but one word: v_norm fetches 20.8 -> 13.4 GB (12.3 GB of volume), v_scan 17.2 ->
+// 14.2 GB; time 7.34 -> 7.20 ms and 5.60 -> 5.53 ms (full resolution, same box) — the gathers'
+// remaining cost is their issue and latency on the tile's critical path (no gathers at all:
+// v_norm 5.5 ms), not bytes.
+#ifndef SM_CB_CHUNK_MAJOR_V
+#define SM_CB_CHUNK_MAJOR_V 1
+#endif
+
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW>
+__device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
+    CbLine<HORIZ, MODE, FULL, SCALE, RV, KW> L;
+    constexpr int T = CbCfg<HORIZ, MODE, KW>::T;
+    constexpr int NSETS = CbCfg<HORIZ, MODE, KW>::NSETS;
+    L.lane = KW > 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+    L.wv = KW > 1 ? (int)(threadIdx.x >> 6) : 0;
     const int nchunks = (a.D + 63) >> 6;
-    const int per_pair = (HORIZ ? a.H : a.W) * nchunks;
-    const int blk = xcd_swizzle(blockIdx.x, gridDim.x);   // neighbouring lines on one XCD
+    const int ngroups = ((HORIZ ? a.H : a.W) + KW - 1) / KW;   // KW = 1: one line per block
+    const int per_pair = ngroups * nchunks;
     const int b = blk / per_pair;
     const int lc = blk - b * per_pair;
-    L.line = lc / nchunks;
-    const int chunk = lc - L.line * nchunks;
+    // V sweeps, chunk-major (SM_CB_CHUNK_MAJOR_V): the blocks resident on one XCD are
+    // consecutive columns of ONE disparity chunk, whose other-image spans [u - c64 - 63, u - c64]
+    // overlap almost entirely, instead of 1/nchunks as many columns of every chunk
+    const bool cmaj = !HORIZ && SM_CB_CHUNK_MAJOR_V;
+    const int grp = cmaj ? lc % ngroups : lc / nchunks;
+    const int chunk = cmaj ? lc / ngroups : lc - grp * nchunks;
+    L.line = grp * KW + L.wv;
+    L.active = true;
+    if (KW > 1 && L.line >= (HORIZ ? a.H : a.W)) {   // spare wave: runs column W - 1, stores nothing
+        L.active = false;
+        L.line = (HORIZ ? a.H : a.W) - 1;
+    }
     const size_t npix = (size_t)a.H * a.W;
     const size_t first_pix = HORIZ ? (size_t)L.line * a.W : (size_t)L.line;
     L.pstride = HORIZ ? 1 : a.W;
@@ -475,7 +593,7 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     L.c64 = chunk * 64;
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
-    L.ring = cbca_ring(a.lag, HORIZ, MODE);
+    L.ring = cbca_ring(a.lag, HORIZ, MODE, KW);
     if (HORIZ && RV && !SM_CB_LDS_WIN) {
         // right view: the window before each set's first position p0 = -off holds, in lane l, the
         // left image's arm pair at p0 - 1 + c64 + l (0 outside the line)
@@ -485,17 +603,47 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
             L.sh[s] = buf_ld_u32(L.A1r[s], (unsigned)q < (unsigned)a.W ? (uint32_t)q * 4u : 0x80000000u, 0);
         }
     }
-    L.r1 = smem;
-    L.r2 = smem + (size_t)L.ring * 64;
-    L.ra = (uint16_t*)(smem + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
-    L.wown = (uint32_t*)(smem + cbca_ring_words(a.lag, HORIZ, MODE));
+    const int ring_words = cbca_ring_words(a.lag, HORIZ, MODE, KW);
+    float* const mine = KW > 1 ? smem + (size_t)L.wv * ring_words : smem;   // this wave's rings
+    L.r1 = mine;
+    L.r2 = mine + (size_t)L.ring * 64;
+    L.ra = (uint16_t*)(mine + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
+    L.wown = (uint32_t*)(smem + ring_words);
     L.wspan = L.wown + NSETS * T;
     L.scale = a.scale;
     {   // zero the rings: reads of positions before the line start then yield S = 0, area = 0
-        const int words = cbca_smem_words(a.lag, HORIZ, MODE);
-        for (int w = L.lane; w < words; w += 64) smem[w] = 0.f;
-        __syncthreads();  // one wave; also orders the float stores before the u16 ring reads
+        const int words = KW > 1 ? ring_words : cbca_smem_words(a.lag, HORIZ, MODE);
+        for (int w = L.lane; w < words; w += 64) mine[w] = 0.f;
     }
+    if constexpr (KW > 1) {
+        // staged word idx = m * 64 KW + tid of a tile: [set s][row k][KW own | KW + 63 other]
+        constexpr int SPW = cbca_spw(KW);
+        constexpr int NW = CbCfg<HORIZ, MODE, KW>::NW;
+        constexpr int NV = CbCfg<HORIZ, MODE, KW>::NV;
+        L.stg = (uint32_t*)(smem + (size_t)KW * ring_words);
+        L.sbuf = 1;
+        L.H = a.H;
+        L.rowb = (uint32_t)a.W * 4u;
+        L.Ar = buf_rsrc(a.arms + (size_t)b * 4 * npix, (int)(4 * npix * 4));
+        const int u0 = grp * KW;
+        const int own = RV ? 2 : 0, other = RV ? 0 : 2;
+        L.sok = 0;
+#pragma unroll
+        for (int m = 0; m < NV; m++) {
+            const int idx = m * 64 * KW + (int)threadIdx.x;
+            const int sset = idx / (T * SPW);
+            const int rem = idx - sset * (T * SPW);
+            const int k = rem / SPW;
+            const int c = rem - k * SPW;
+            const int pl = sset == 1 ? 0 : 1;   // V sweeps: pass pair = (U | D) plane 1, perpendicular = plane 0
+            const int plane = (c < KW ? own : other) + pl;
+            const int col = c < KW ? u0 + c : (RV ? u0 + L.c64 + (c - KW) : u0 - L.c64 - 63 + (c - KW));
+            L.skoff[m] = k - (sset == 0 ? a.lag : 0);
+            L.sboff[m] = ((uint32_t)plane * (uint32_t)npix + (uint32_t)(col < 0 ? 0 : col)) * 4u;
+            if (idx < NW && col >= 0 && col < a.W) L.sok |= 1u << m;
+        }
+    }
+    __syncthreads();  // orders the float ring stores before the u16 ring reads (and across waves)
     L.S1 = L.S2 = 0.f;
     L.Acc = 0;
     L.ws = 0;
@@ -515,8 +663,8 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
         }
     }
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    typename CbLine<HORIZ, MODE, FULL, SCALE, RV>::Tile ta, tb, tc, td;
-    if constexpr (CbCfg<HORIZ, MODE>::PF == 3) {
+    typename CbLine<HORIZ, MODE, FULL, SCALE, RV, KW>::Tile ta, tb, tc, td;
+    if constexpr (CbCfg<HORIZ, MODE, KW>::PF == 3) {
         L.load(ta, 0);
         L.load(tb, T);
         L.load(tc, 2 * T);
@@ -533,7 +681,7 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
             L.load(tc, j0 + 6 * T);
             L.process(td, j0 + 3 * T);
         }
-    } else if constexpr (CbCfg<HORIZ, MODE>::PF == 2) {
+    } else if constexpr (CbCfg<HORIZ, MODE, KW>::PF == 2) {
         L.load(ta, 0);
         L.load(tb, T);
         for (int j0 = 0; j0 < nst; j0 += 3 * T) {
@@ -558,20 +706,52 @@ __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     }
 }
 
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, bool PERSIST>
+__global__ __launch_bounds__(64 * KW) void k_cbca(const CbcaArgs a, const int nlines) {
+    extern __shared__ float smem[];
+    const int slot = xcd_swizzle(blockIdx.x, gridDim.x);   // neighbouring lines on one XCD
+    if (!PERSIST) {
+        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW>(a, slot, smem);
+        return;
+    }
+    for (int blk = slot; blk < nlines; blk += gridDim.x) {   // every block exits after its last line
+        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW>(a, blk, smem);
+        __syncthreads();   // the next line's ring zeroing follows this line's last ring reads
+    }
+}
+
+template <bool HORIZ, int MODE, bool SCALE, int KW>
+static void launch_kw(const CbcaArgs& a, int n, hipStream_t st) {
+    const int nchunks = (a.D + 63) / 64;
+    const int groups = ((HORIZ ? a.H : a.W) + KW - 1) / KW;
+    const int nlines = groups * nchunks * n;
+    const size_t shm = 4 * (size_t)(KW > 1 ? cbca_smem_words_vg(a.lag, MODE, KW) : cbca_smem_words(a.lag, HORIZ, MODE));
+    const bool full = a.D % 64 == 0;
+    constexpr bool PERSIST = !HORIZ && KW == 1 && SM_CB_PERSIST_V;
+    int nblk = nlines;
+    if (PERSIST) {
+        // resident blocks: LDS-bound (160 KiB per CU), at most 8 waves per CU
+        const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / std::max<size_t>(shm, 1))));
+        nblk = std::min(nlines, per_cu * a.num_cu);
+    }
+    dim3 grid(nblk);
+    if (a.view == 0) {
+        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, false, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
+        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, false, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
+    } else {
+        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, true, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
+        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, true, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
+    }
+}
+
 template <bool HORIZ, int MODE, bool SCALE>
 static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
-    const int nchunks = (a.D + 63) / 64;
-    const int lines = HORIZ ? a.H : a.W;
-    dim3 grid(lines * nchunks * n);
-    const size_t shm = 4 * (size_t)cbca_smem_words(a.lag, HORIZ, MODE);
-    const bool full = a.D % 64 == 0;
-    if (a.view == 0) {
-        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, false>), grid, dim3(64), shm, st, a);
-        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, false>), grid, dim3(64), shm, st, a);
-    } else {
-        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, true>), grid, dim3(64), shm, st, a);
-        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, true>), grid, dim3(64), shm, st, a);
+    constexpr int KW = cbca_kw(HORIZ, MODE);
+    if constexpr (KW > 1) {
+        // the group's rings and staging must fit one CU's 160 KiB of LDS (lag <= 34 does)
+        if (4 * (size_t)cbca_smem_words_vg(a.lag, MODE, KW) <= 160 * 1024) return launch_kw<HORIZ, MODE, SCALE, KW>(a, n, st);
     }
+    launch_kw<HORIZ, MODE, SCALE, 1>(a, n, st);
 }
 
 template <bool HORIZ, int MODE>

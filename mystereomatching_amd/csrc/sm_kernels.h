@@ -56,6 +56,7 @@ struct CbcaArgs {
     int apply_scale;
     float scale;                // SolveAll weight (fused into the last normalising pass)
     int view;                   // 0: vm[0] (left reference), 1: vm[1] (right reference, Do_refine)
+    int num_cu;                 // compute units of the device (persistent V sweeps)
 };
 
 struct SgmArgs {

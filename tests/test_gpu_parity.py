@@ -17,7 +17,8 @@ from mystereomatching_amd import synthetic as S
 
 pytestmark = pytest.mark.gpu
 
-GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
+                if not os.path.basename(p).startswith("large_"))   # large_*: test_gpu_large_fixtures.py
 
 
 def bits(a):

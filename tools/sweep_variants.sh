@@ -4,7 +4,7 @@
 TAG=$1; shift
 mkdir -p gpurun_out
 for v in "$@"; do
-  SM_HIP_LIB=tools/variants/libsm_hip_$v.so timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline $BENCH_ARGS \
+  SM_HIP_LIB=tools/variants/libsm_hip_$v.so timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity $BENCH_ARGS \
     > gpurun_out/${TAG}_$v.json 2> gpurun_out/${TAG}_$v.err || { echo "FAIL $v"; tail -3 gpurun_out/${TAG}_$v.err; exit 1; }
   python - "$v" "gpurun_out/${TAG}_$v.json" <<'PY'
 import json, sys

@@ -85,6 +85,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--no-parity", action="store_true", help="skip the pair-0 fixture comparison (timing probes)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="time the product multi-GPU path instead of resident batches: rank 0 holds the global "
+                         "batch on the host; each step broadcasts the header, scatters the pairs (RCCL), runs "
+                         "them and gathers the int16 maps back (mystereomatching_amd.batch.DistributedBatchRunner)")
     ap.add_argument("--opt", default="sgm", choices=["sgm", "so"],
                     help='optimization selector (h:53): "sgm" (default) or "so" scan-line DP (cpp:6272-6394)')
     ap.add_argument("--refine", action="store_true",
@@ -124,6 +128,9 @@ def main():
     from mystereomatching_amd import StereoBatch
     from mystereomatching_amd import synthetic as S
     from mystereomatching_amd.evaluate import cal_err
+
+    if args.e2e:
+        return run_e2e(args, world, rank, local, dist, backend)
 
     H, W, md, paths, B0, desc = WORKLOADS[args.workload]
     B = args.batch or B0
@@ -268,6 +275,62 @@ def main():
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(out))
     sb.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_e2e(args, world, rank, local, dist, backend):
+    """--e2e: DistributedBatchRunner.run timed end to end (host batch on rank 0 -> scatter ->
+    compute -> gather -> host maps on rank 0).  value = pairs of the global batch x H x W x D per
+    second.  No roofline / CPU baseline here: the resident-batch line is the kernel measurement."""
+    import torch
+    from mystereomatching_amd import synthetic as S
+    from mystereomatching_amd.batch import DistributedBatchRunner, hip_compute_fn
+
+    H, W, md, paths, B0, desc = WORKLOADS[args.workload]
+    B = args.batch or B0
+    D = md + 1
+    n = B * world
+    batch = S.make_batch(n, H, W, D) if rank == 0 else None
+    fn = hip_compute_fn(md, H, W, B, local, sgm_paths=paths)
+    runner = DistributedBatchRunner(fn)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        runner.run(batch, md, 0.3)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    maps = None
+    for _ in range(args.steps):
+        maps = runner.run(batch, md, 0.3)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    parity = None
+    if rank == 0 and not args.no_parity:
+        parity = fixture_check(args.workload, False, "sgm", maps[0])
+    value = n * H * W * D * args.steps / elapsed / 1e6
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 2), "unit": "Mdisp/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded piecewise-planar pairs, mystereomatching_amd/synthetic.py), host-resident on rank 0",
+            "config": {"workload": desc + " -- end to end: broadcast header, scatter pairs, compute, gather maps",
+                       "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": n, "sgm_paths": paths,
+                       "parallelism": f"dp{world} via DistributedBatchRunner ({backend})", "e2e": True},
+            "parity": parity,
+        }))
+    fn.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -22,6 +22,7 @@
  *   sm_get_arms        <- public member HVL[view]                    stereoMatching.h:2717
  *   sm_destroy         <- delete smPsy[p]                            main_.cpp:173-178
  *   sm_run / sm_run_batch  <- the whole main_.cpp:139-163 sequence for n independent pairs
+ *   sm_run_batch_multi     <- the same over several contexts / GPUs (one host thread each)
  * Threading: one sm_ctx per host thread; each ctx owns one HIP stream on its device.
  */
 #ifndef SM_CAPI_H
@@ -160,6 +161,14 @@ SM_API sm_status sm_download_disp(sm_ctx* ctx, int32_t n, int16_t* disp_out);
 SM_API sm_status sm_run_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
                               const uint8_t* lgray, const uint8_t* rgray, float reg_lambda,
                               int16_t* disp_out);
+/* Multi-device batch (SURVEY §8b/§8e without torch.distributed): the n packed host pairs are split
+ * into contiguous blocks of ceil(n / nctx), block i runs on ctxs[i] (each context on its own
+ * device, or several on one), one host thread per context; disp_out receives all n maps in order.
+ * Contexts must share rows / cols / num_disparities and hold batch_capacity >= the block size.
+ * Returns the first failing context's status (its sm_last_error has the message). */
+SM_API sm_status sm_run_batch_multi(sm_ctx* const* ctxs, int32_t nctx, int32_t n, const uint8_t* lbgr,
+                                    const uint8_t* rbgr, const uint8_t* lgray, const uint8_t* rgray,
+                                    float reg_lambda, int16_t* disp_out);
 SM_API sm_status sm_synchronize(sm_ctx* ctx);
 SM_API void* sm_stream(sm_ctx* ctx);      /* the ctx's hipStream_t */
 

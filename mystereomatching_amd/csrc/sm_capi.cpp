@@ -14,6 +14,7 @@
 #include <map>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sm_kernels.h"
@@ -1015,6 +1016,42 @@ sm_status sm_run_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8_t*
     sm_status s = sm_upload_batch(c, n, lbgr, rbgr, lgray, rgray);
     if (s) return s;
     return sm_run(c, n, reg_lambda, disp_out);
+}
+
+sm_status sm_run_batch_multi(sm_ctx* const* ctxs, int32_t nctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
+                             const uint8_t* lgray, const uint8_t* rgray, float reg_lambda, int16_t* disp_out) {
+    if (!ctxs || nctx < 1 || n < 1 || !lbgr || !rbgr || !lgray || !rgray || !disp_out) return SM_EINVAL;
+    for (int i = 0; i < nctx; i++) {
+        if (!ctxs[i]) return SM_EINVAL;
+        for (int j = 0; j < i; j++)
+            if (ctxs[j] == ctxs[i]) return fail(ctxs[i], SM_EINVAL, "sm_run_batch_multi: a context appears twice");
+        const sm_params& a = ctxs[i]->p;
+        const sm_params& b = ctxs[0]->p;
+        if (a.rows != b.rows || a.cols != b.cols || a.num_disparities != b.num_disparities)
+            return fail(ctxs[i], SM_EINVAL, "sm_run_batch_multi: contexts of different shapes");
+    }
+    // contiguous blocks of ceil(n / nctx) pairs: context i owns pairs [i * per, min(n, (i + 1) * per))
+    const int per = (n + nctx - 1) / nctx;
+    const size_t npix = (size_t)ctxs[0]->p.rows * ctxs[0]->p.cols;
+    for (int i = 0; i < nctx; i++) {
+        const int lo = std::min(n, i * per), cnt = std::min(n, lo + per) - lo;
+        if (cnt > ctxs[i]->cap) return fail(ctxs[i], SM_EINVAL, "sm_run_batch_multi: block larger than batch_capacity");
+    }
+    std::vector<sm_status> st(nctx, SM_OK);
+    auto work = [&](int i) {
+        const int lo = std::min(n, i * per), cnt = std::min(n, lo + per) - lo;
+        if (cnt <= 0) return;
+        st[i] = sm_run_batch(ctxs[i], cnt, lbgr + lo * npix * 3, rbgr + lo * npix * 3, lgray + lo * npix,
+                             rgray + lo * npix, reg_lambda, disp_out + lo * npix);
+    };
+    // one host thread per context (each context is used by one thread only, the C-ABI's rule)
+    std::vector<std::thread> th;
+    for (int i = 1; i < nctx; i++) th.emplace_back(work, i);
+    work(0);
+    for (auto& t : th) t.join();
+    for (int i = 0; i < nctx; i++)
+        if (st[i] != SM_OK) return st[i];
+    return SM_OK;
 }
 
 sm_status sm_synchronize(sm_ctx* c) {

@@ -341,3 +341,18 @@ class StereoBatch:
             nm = names.raw[i * 48:(i + 1) * 48].split(b"\0", 1)[0].decode()
             out[nm] = {"launches": launches[i], "total_ms": total[i], "bytes_per_launch": byts[i]}
         return out
+
+
+def run_batch_multi(batches: Sequence[StereoBatch], lbgr, rbgr, lgray, rgray, reg_lambda: float = 0.3) -> np.ndarray:
+    """sm_run_batch_multi: n host pairs split into contiguous blocks over the contexts of
+    `batches` (one per GPU, or several on one), one host thread per context; returns [n,H,W] int16."""
+    lib = _capi.load()
+    arrs = [np.ascontiguousarray(_to_numpy(a), np.uint8) for a in (lbgr, rbgr, lgray, rgray)]
+    n, H, W = arrs[2].shape
+    out = np.empty((n, H, W), np.int16)
+    ctxs = (C.c_void_p * len(batches))(*[b._ctx.value for b in batches])
+    st = lib.sm_run_batch_multi(ctxs, len(batches), n, *[_capi.ptr(a) for a in arrs], float(reg_lambda), _capi.ptr(out))
+    _capi.check(lib, batches[0]._ctx, st, "sm_run_batch_multi")
+    for b in batches:
+        b.n = 0   # each context now holds only its own block
+    return out

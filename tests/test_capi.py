@@ -114,3 +114,16 @@ def test_refine_validation(field, value, msg):
         assert msg in lib.sm_last_error(ctx)
     finally:
         lib.sm_destroy(ctx)
+
+
+def test_run_batch_multi_argument_checks():
+    """sm_run_batch_multi rejects bad arguments before touching a device."""
+    lib = _capi.load()
+    buf = (C.c_uint8 * 16)()
+    out = (C.c_int16 * 16)()
+    p = C.cast(buf, C.c_void_p)
+    assert lib.sm_run_batch_multi(None, 1, 1, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL
+    arr = (C.c_void_p * 1)(None)
+    assert lib.sm_run_batch_multi(arr, 1, 1, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL
+    assert lib.sm_run_batch_multi(arr, 0, 1, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL
+    assert lib.sm_run_batch_multi(arr, 1, 0, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL

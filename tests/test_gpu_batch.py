@@ -63,3 +63,19 @@ def test_multi_stream_sub_batches(oracle, sub_batch, num_streams):
         np.testing.assert_array_equal(sb.run(0.3), first)
     finally:
         sb.close()
+
+
+@pytest.mark.parametrize("n,caps", [(5, (3, 3)), (4, (2, 2, 2)), (1, (1, 1))])
+def test_run_batch_multi_contexts(oracle, n, caps):
+    """sm_run_batch_multi over several contexts on device 0 (one host thread each): contiguous
+    blocks of ceil(n / nctx) pairs, maps returned in pair order, equal to the oracle's."""
+    from mystereomatching_amd import run_batch_multi
+    H, W, md = 33, 47, 15
+    batch = S.make_batch(n, H, W, md + 1, first_index=360)
+    sbs = [StereoBatch(md, H, W, c, device=0) for c in caps]
+    try:
+        got = run_batch_multi(sbs, *(batch[k] for k in KEYS))
+        np.testing.assert_array_equal(got, _oracle_maps(oracle, batch, H, W, md))
+    finally:
+        for sb in sbs:
+            sb.close()

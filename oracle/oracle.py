@@ -34,6 +34,7 @@ class Config(C.Structure):
         ("do_refine", C.c_int), ("lr_max_diff", C.c_float), ("do_region_vote", C.c_int),
         ("region_vote_nums", C.c_int), ("rv_ratio", C.c_float), ("rv_s", C.c_int),
         ("do_proper_ipol", C.c_int), ("disp_occ", C.c_int), ("do_last_median", C.c_int),
+        ("gf_r", C.c_int), ("gf_eps", C.c_float), ("nl_sigma", C.c_double),
     ]
 
 
@@ -84,6 +85,15 @@ def load():
         lib.smo_bad_ratio.argtypes = [C.c_int, C.c_int, P, P, P, C.c_float, C.POINTER(C.c_float)]
         lib.smo_bad_ratio.restype = C.c_float
         lib.smo_expf_range.argtypes = [C.c_uint32, C.c_uint32, P]
+        lib.smo_box_filter.argtypes = [C.c_int, C.c_int, C.c_int, P, P, P]
+        lib.smo_guided_filter.argtypes = [C.POINTER(Config), P, P]
+        lib.smo_guided_filter.restype = C.c_int
+        lib.smo_nl_median3.argtypes = [C.c_int, C.c_int, P, P]
+        lib.smo_nl_tree.argtypes = [C.c_int, C.c_int, P, P, P, P, P, P]
+        lib.smo_nl_tree.restype = C.c_int
+        lib.smo_nl_table.argtypes = [C.c_double, P]
+        lib.smo_nl_aggregate.argtypes = [C.POINTER(Config), P, P]
+        lib.smo_nl_aggregate.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -248,3 +258,52 @@ def expf_libm(x: np.ndarray) -> np.ndarray:
     libm.expf.restype = C.c_float
     libm.expf.argtypes = [C.c_float]
     return np.array([libm.expf(float(v)) for v in np.asarray(x, np.float32).ravel()], np.float32)
+
+
+def box_filter(img: np.ndarray, r: int) -> np.ndarray:
+    """BoxFilter (cpp:5151-5202) of a float32 H x W image."""
+    a = np.ascontiguousarray(img, np.float32)
+    H, W = a.shape
+    out, tmp = np.empty_like(a), np.empty_like(a)
+    load().smo_box_filter(H, W, r, _p(a), _p(out), _p(tmp))
+    return out
+
+
+def guided_filter(vm: np.ndarray, bgr: np.ndarray, cfg: Config) -> np.ndarray:
+    """guideFilterCore_matlab over every slice of an H x W x D volume (MY_GUIDE form of GF)."""
+    out = np.ascontiguousarray(vm, np.float32).copy()
+    if load().smo_guided_filter(C.byref(cfg), _p(out), _p(np.ascontiguousarray(bgr, np.uint8))) != 0:
+        raise ValueError("guided filter needs H, W >= 2 r + 1")
+    return out
+
+
+def nl_median3(bgr: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(bgr, np.uint8)
+    out = np.empty_like(a)
+    load().smo_nl_median3(a.shape[0], a.shape[1], _p(a), _p(out))
+    return out
+
+
+def nl_tree(bgr: np.ndarray) -> dict:
+    """The MST / BFS tree of NLCCA (order, parent, weight, nchild, child[n, 4])."""
+    a = np.ascontiguousarray(bgr, np.uint8)
+    H, W = a.shape[:2]
+    n = H * W
+    t = {"order": np.empty(n, np.int32), "parent": np.empty(n, np.int32), "weight": np.empty(n, np.uint8),
+         "nchild": np.empty(n, np.int32), "child": np.full((n, 4), -1, np.int32)}
+    if load().smo_nl_tree(H, W, _p(a), *(_p(t[k]) for k in ("order", "parent", "weight", "nchild", "child"))) != 0:
+        raise ValueError("tree construction failed")
+    return t
+
+
+def nl_table(sigma: float = 0.1) -> np.ndarray:
+    t = np.empty(256, np.float64)
+    load().smo_nl_table(sigma, _p(t))
+    return t
+
+
+def nl_aggregate(vm: np.ndarray, bgr: np.ndarray, cfg: Config) -> np.ndarray:
+    out = np.ascontiguousarray(vm, np.float32).copy()
+    if load().smo_nl_aggregate(C.byref(cfg), _p(out), _p(np.ascontiguousarray(bgr, np.uint8))) != 0:
+        raise ValueError("NL aggregation failed")
+    return out

@@ -70,6 +70,9 @@ void smo_default_config(smo_config* c, int maxdisp, int H, int W) {
     c->do_proper_ipol = 1;       /* Do_properIpol (h:76) */
     c->disp_occ = -2 * 16;       /* DISP_OCC (h:216) */
     c->do_last_median = 1;       /* Do_lastMedianBlur (h:80) */
+    c->gf_r = 9;                 /* guideFilterCore_matlab(I[i], guideVm[i][d], 9, 0.0001) (cpp:4509) */
+    c->gf_eps = 0.0001f;
+    c->nl_sigma = 0.1;           /* NLCCA::aggreCV (NL/NLCCA.cpp:33) */
 }
 
 /* OpenCV borderInterpolate, BORDER_REFLECT_101 (used by copyMakeBorder, h:870-871). */
@@ -803,6 +806,10 @@ int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR, co
     }
     if (c->aggregation == 1)
         for (int i = 0; i < views; i++) smo_cbca_view(c, vm[i], aL, aR, i);   /* cbca_core LOR loop (cpp:5598) */
+    if (c->aggregation == 2)   /* GF: guideFilter(0, vm), num = Do_refine ? 2 : 1 (cpp:4499-4516) */
+        for (int i = 0; i < views; i++)
+            if (smo_guided_filter(c, vm[i], i == 0 ? bgrL : bgrR)) goto done;
+    if (c->aggregation == 3 && smo_nl_aggregate(c, vm[0], bgrL)) goto done;   /* NL(): vm[0] only (cpp:4898) */
     if (d->vol_agg) memcpy(d->vol_agg, vm[0], nvol * 4);
     if (refine && d->vol_agg_right) memcpy(d->vol_agg_right, vm[1], nvol * 4);
     t = now_ms(); ms[1] = t - t0; t0 = t;

@@ -39,7 +39,7 @@ typedef struct smo_config {
     int arm_L, arm_L_out;        /* cbca_crossL[0]=17, cbca_crossL_out[0]=34 (h:263,266) */
     int arm_cT, arm_cT_out;      /* cbca_cTresh[0]=20, cbca_cTresh_out[0]=6 (h:269,272) */
     int arm_minL;                /* cbca_minArmL = 1 (h:259) */
-    int aggregation;             /* 0 none, 1 CBCA (main:16) */
+    int aggregation;             /* 0 none, 1 CBCA (main:16), 2 GF (MY_GUIDE form), 3 NL */
     int cbca_iters;              /* cbca_iterationNum = 2 (h:260) */
     int solve_all;               /* apply SolveAll(PY_LEV=1) (main:158) */
     float reg_lambda;            /* REG_LAMBDA = 0.3 (main:157) */
@@ -58,9 +58,23 @@ typedef struct smo_config {
     int do_proper_ipol;          /* Do_properIpol = 1 (h:76) */
     int disp_occ;                /* DISP_OCC = -2 * 16 (h:216) */
     int do_last_median;          /* Do_lastMedianBlur = 1 (h:80) */
+    /* alternative aggregators (sm_oracle_agg.c): aggregation 2 = "GF", 3 = "NL" */
+    int gf_r;                    /* guideFilterCore_matlab(I, p, 9, 0.0001) (cpp:4509) */
+    float gf_eps;
+    double nl_sigma;             /* NLCCA::aggreCV sigma = 0.1 (NL/NLCCA.cpp:33) */
 } smo_config;
 
 void smo_default_config(smo_config* c, int maxdisp, int H, int W);
+
+/* sm_oracle_agg.c */
+void smo_box_filter(int H, int W, int r, const float* src, float* dst, float* tmp);
+int smo_guided_filter(const smo_config* c, float* vm, const uint8_t* bgr);
+void smo_nl_median3(int H, int W, const uint8_t* src, uint8_t* dst);
+int smo_nl_tree(int H, int W, const uint8_t* bgr, int* order, int* parent, uint8_t* weight, int* nchild, int* child);
+void smo_nl_table(double sigma, double* table);
+void smo_nl_filter(int n, int P, const int* order, const int* parent, const uint8_t* weight, const int* nchild,
+                   const int* child, const double* table, double* cost, double* backup);
+int smo_nl_aggregate(const smo_config* c, float* vm, const uint8_t* bgrL);
 
 /* OpenCV borderInterpolate(BORDER_REFLECT_101). */
 int smo_reflect101(int p, int len);

@@ -89,6 +89,9 @@ def parse():
                     help="time the product multi-GPU path instead of resident batches: rank 0 holds the global "
                          "batch on the host; each step broadcasts the header, scatters the pairs (RCCL), runs "
                          "them and gathers the int16 maps back (mystereomatching_amd.batch.DistributedBatchRunner)")
+    ap.add_argument("--agg", default="CBCA", choices=["CBCA", "GF", "NL"],
+                    help='aggregation selector (h:52): "CBCA" (default), "GF" guided filter (cpp:4492-4516, MY_GUIDE form), '
+                         '"NL" non-local MST filter (cpp:4892-4917)')
     ap.add_argument("--opt", default="sgm", choices=["sgm", "so"],
                     help='optimization selector (h:53): "sgm" (default) or "so" scan-line DP (cpp:6272-6394)')
     ap.add_argument("--refine", action="store_true",
@@ -137,7 +140,10 @@ def main():
     D = md + 1
     # this rank's shard of the global batch: pair indices [rank*B, rank*B + B)
     batch = S.make_batch(B, H, W, D, first_index=rank * B)
-    sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt)
+    sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt,
+                     aggregation=args.agg)
+    if args.agg != "CBCA":
+        desc = desc.replace("CBCA", args.agg, 1)
     if args.opt == "so":
         desc = desc.replace("SGM 4-path+WTA", "so (scan-line DP)").replace("SGM 8-path+WTA", "so (scan-line DP)")
     if args.refine:
@@ -185,7 +191,8 @@ def main():
         kernels = sb.profile_read()
         sb.profile(False)
     disp = sb.download()
-    parity = fixture_check(args.workload, args.refine, args.opt, disp[0]) if rank == 0 and not args.no_parity else None
+    parity = fixture_check(args.workload, args.refine or args.agg != "CBCA", args.opt, disp[0]) \
+        if rank == 0 and not args.no_parity else None
     bad2 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 2.0)[0] for i in range(B)]))
     bad1 = float(np.mean([cal_err(disp[i], batch["gt"][i], batch["nonocc"][i], 1.0)[0] for i in range(B)]))
 
@@ -212,7 +219,8 @@ def main():
                 tot_by.get(n[:-2] if n.endswith("_r") and n[:-2] in kern_out else n, 0.0) + kernels[n]["total_ms"]
         dom = max(tot_by, key=tot_by.get)
         traffic = None
-        tag = ("_refine" if args.refine else "") + ("_so" if args.opt == "so" else "")
+        tag = ("_refine" if args.refine else "") + ("_so" if args.opt == "so" else "") + \
+            ("" if args.agg == "CBCA" else "_" + args.agg.lower())
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}{tag}_b{B}.json")
         if os.path.exists(pmc):
             try:
@@ -229,7 +237,8 @@ def main():
         from oracle import oracle as O
         host = _host_cpu()
         if H * W * D <= CPU_FULL_PAIR_MAX:
-            cfg = O.config(H, W, md, sgm_paths=paths, do_refine=int(args.refine), optimization=2 if args.opt == "so" else 1)
+            cfg = O.config(H, W, md, sgm_paths=paths, do_refine=int(args.refine), optimization=2 if args.opt == "so" else 1,
+                           aggregation={"CBCA": 1, "GF": 2, "NL": 3}[args.agg])
             n, t_cpu = 0, 0.0
             while n == 0 or (t_cpu < args.cpu_seconds and n < B):
                 pair = {k: batch[k][n] for k in ("lbgr", "rbgr", "lgray", "rgray")}
@@ -249,7 +258,8 @@ def main():
             # (parity at this size: tests/test_gpu_fullres.py; the oracle itself: every smaller size).
             hc = max(8, min(H, CPU_FULL_PAIR_MAX // (W * D)))
             pair = {k: np.ascontiguousarray(batch[k][0][:hc]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
-            cfg = O.config(hc, W, md, sgm_paths=paths, do_refine=int(args.refine), optimization=2 if args.opt == "so" else 1)
+            cfg = O.config(hc, W, md, sgm_paths=paths, do_refine=int(args.refine), optimization=2 if args.opt == "so" else 1,
+                           aggregation={"CBCA": 1, "GF": 2, "NL": 3}[args.agg])
             t = time.perf_counter()
             O.run_ex(pair, cfg)
             t_cpu = time.perf_counter() - t
@@ -265,7 +275,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded piecewise-planar pairs, mystereomatching_amd/synthetic.py)",
             "config": {"workload": desc, "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": B * world,
-                       "sgm_paths": paths, "optimization": args.opt, "refine": bool(args.refine),
+                       "sgm_paths": paths, "aggregation": args.agg, "optimization": args.opt, "refine": bool(args.refine),
                        "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
             "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "kernels": kern_out,

@@ -60,6 +60,8 @@ typedef enum sm_cost_method {
 typedef enum sm_aggregation {
     SM_AGG_NONE = 0,
     SM_AGG_CBCA = 1,         /* "CBCA" (main:16; cpp:1002-1003) — default */
+    SM_AGG_GF = 2,           /* "GF"  guideFilter, MY_GUIDE form (cpp:4492-4516, 4975-5104); sgm / WTA only */
+    SM_AGG_NL = 3,           /* "NL"  non-local MST tree filter (cpp:4892-4917, NL/NLCCA.cpp:27-96) */
 } sm_aggregation;
 
 typedef enum sm_optimization {
@@ -112,6 +114,9 @@ typedef struct sm_params {
     int32_t num_streams;         /* 0/1: one stream; 2-4: groups alternate over that many streams,
                                   * group k + 1 starting once group k's CBCA is done */
     int32_t fuse_norm_scan;      /* 1: CBCA normalising sweep fused with the next scan (measured slower) */
+    /* alternative aggregators */
+    float gf_eps;                /* guideFilterCore_matlab eps = 0.0001 (cpp:4509; radius fixed at 9) */
+    double nl_sigma;             /* NLCCA sigma = 0.1 (NL/NLCCA.cpp:33): weights exp(-c / (255 sigma)) */
 } sm_params;
 
 typedef struct sm_ctx sm_ctx;

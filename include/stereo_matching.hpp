@@ -322,10 +322,14 @@ class StereoMatching {
                         : costcalculation == "AD"       ? SM_COST_AD
                                                         : -1;
         if (p.cost_method < 0) throw std::invalid_argument("unsupported costcalculation: " + costcalculation);
-        if (aggregation != "CBCA" && !aggregation.empty()) throw std::invalid_argument("unsupported aggregation: " + aggregation);
+        if (aggregation != "CBCA" && aggregation != "GF" && aggregation != "NL" && !aggregation.empty())
+            throw std::invalid_argument("unsupported aggregation: " + aggregation);
         if (optimization != "sgm" && optimization != "so" && !optimization.empty())
             throw std::invalid_argument("unsupported optimization: " + optimization);
-        p.aggregation = aggregation == "CBCA" ? SM_AGG_CBCA : SM_AGG_NONE;
+        p.aggregation = aggregation == "CBCA" ? SM_AGG_CBCA
+                        : aggregation == "GF" ? SM_AGG_GF
+                        : aggregation == "NL" ? SM_AGG_NL
+                                              : SM_AGG_NONE;
         p.optimization = optimization == "sgm" ? SM_OPT_SGM : (optimization == "so" ? SM_OPT_SO : SM_OPT_WTA);
         p.census_ring = param.censusFunc == 3;
         p.lam_cen = (float)param.lamCen;

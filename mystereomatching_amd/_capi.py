@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libsm_hip.so")
 
 SM_OK, SM_EINVAL, SM_ENOMEM, SM_EHIP, SM_ESTATE = 0, 1, 2, 3, 4
 COST_METHODS = {"censusGrad": 0, "Census": 1, "ADCensus": 2, "AD": 3}
-AGGREGATIONS = {"": 0, "none": 0, "CBCA": 1}
+AGGREGATIONS = {"": 0, "none": 0, "CBCA": 1, "GF": 2, "NL": 3}
 OPTIMIZATIONS = {"": 0, "wta": 0, "sgm": 1, "so": 2}
 
 
@@ -39,6 +39,7 @@ class sm_params(C.Structure):
         ("region_vote_nums", C.c_int32), ("rv_ratio", C.c_float), ("rv_s", C.c_int32),
         ("do_proper_ipol", C.c_int32), ("disp_occ", C.c_int32), ("do_last_median_blur", C.c_int32),
         ("sub_batch", C.c_int32), ("num_streams", C.c_int32), ("fuse_norm_scan", C.c_int32),
+        ("gf_eps", C.c_float), ("nl_sigma", C.c_double),
     ]
 
 

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "sm_kernels.h"
+#include "sm_nl_tree.h"
 
 namespace {
 
@@ -61,6 +62,18 @@ struct sm_ctx {
     uint8_t* so_trace = nullptr;   // [cap][npix][D] "so" choice codes
     uint16_t* so_cidx = nullptr;   // [cap][npix] "so" row-minimum indices
     uint32_t* px = nullptr;     // [cap][2][npix] packed BGR, then the pxh and pxv arm-walk planes (same shape)
+    // aggregation "GF": three scratch volumes (the SGM sum is the fourth), image planes, per-pixel terms
+    float* gf_s = nullptr;      // [3 (+1 without acc)][cap][nvol]
+    float* gf_planes = nullptr; // [cap][10][npix]
+    sm::GfPix* gf_pix = nullptr;// [cap][npix]
+    // aggregation "NL": median image, edge weights, the tree (uploaded per call), filter values
+    uint8_t* nl_med = nullptr;  // [cap][npix][3]
+    uint8_t* nl_ew = nullptr;   // [cap][ne]
+    int* nl_ints = nullptr;     // chain_nodes, chain_start, chain_len, order_up, order_down, parent, child[4]: [cap][npix] each
+    uint8_t* nl_bytes = nullptr;// weight, nchild, heavy: [cap][npix] each
+    double* nl_table = nullptr; // [256]
+    double* nl_val = nullptr;   // [cap][nvol]
+    float* nl_wsum = nullptr;   // [cap][npix]
     int n_loaded = 0;
     int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized, 5 refined
     float lut_a[1024], lut_b[1024];
@@ -163,7 +176,18 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (p.rows > 65535) return bad("rows must be <= 65535");
     if (p.num_disparities < 1 || p.num_disparities > 1024) return bad("num_disparities must be in [1, 1024]");
     if (p.cost_method < 0 || p.cost_method > 3) return bad("unknown cost_method");
-    if (p.aggregation < 0 || p.aggregation > 1) return bad("unknown aggregation");
+    if (p.aggregation < 0 || p.aggregation > 3) return bad("unknown aggregation");
+    if (p.aggregation == SM_AGG_GF) {
+        // BoxFilter's windows need 2 r + 1 = 19 rows and columns (cpp:5156 asserts only >= r, and
+        // reads outside the image below 2 r + 1); the "so" optimiser's minima assume costs >= 0
+        if (p.rows < 19 || p.cols < 19) return bad("aggregation GF needs rows, cols >= 19 (box radius 9)");
+        if (p.optimization == SM_OPT_SO) return bad("aggregation GF (costs may be negative) supports optimization sgm or WTA");
+    }
+    if (!(p.gf_eps > 0)) return bad("gf_eps must be > 0");
+    if (!(p.nl_sigma > 0)) return bad("nl_sigma must be > 0");
+    if (p.aggregation == SM_AGG_NL) {
+        if (p.rows <= 2 && p.cols <= 2) return bad("aggregation NL needs more than 2 x 2 pixels (qx_mst: no edges)");
+    }
     if (p.optimization < 0 || p.optimization > 2) return bad("unknown optimization");
     if (p.census_rv < 0 || p.census_ru < 0 || census_len(p) > 128) return bad("census code longer than 128 bits");
     if (p.arm_l_out < 0 || p.arm_l_out > 84 || p.arm_min_l < 0 || p.arm_min_l > 84 || p.arm_l < 0)
@@ -222,7 +246,9 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 
 void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
-                    c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx};
+                    c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
+                    c->gf_s, c->gf_planes, c->gf_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_bytes,
+                    c->nl_table, c->nl_val, c->nl_wsum};
     for (void* q : ptrs)
         if (q) hipFree(q);
     for (auto& r : c->recs) {
@@ -412,6 +438,151 @@ sm_status run_scale(sm_ctx* c, int n, int view, float w, const Bufs& B) {
 
 // dispOptimize (cpp:1046-1136) for one view: vm[0] with the left image's penalty flags
 // (leftFirst = true) -> DP[0]; vm[1] with the right image's (leftFirst = false) -> DP[1].
+// guideFilter(0, vm) on one view (cpp:4492-4516), MY_GUIDE form: sm_gf.hip
+sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B) {
+    const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, cap = c->cap, nv = c->nvol;
+    sm::GfArgs a{};
+    a.vm = view == 0 ? B.vm0 : B.vm1;
+    float* s0 = c->acc ? c->acc : c->gf_s + 3 * cap * nv;
+    a.s0 = s0 + off * nv;
+    a.s1 = c->gf_s + (0 * cap + off) * nv;
+    a.s2 = c->gf_s + (1 * cap + off) * nv;
+    a.s3 = c->gf_s + (2 * cap + off) * nv;
+    a.bgr = B.bgr + (size_t)view * c->npix * 3;   // I_c[view] (cpp:4502)
+    a.bgr_pair_stride = 2 * c->npix * 3;
+    a.planes = c->gf_planes + off * 10 * c->npix;
+    a.pix = c->gf_pix + off * c->npix;
+    a.H = c->p.rows;
+    a.W = c->p.cols;
+    a.D = c->p.num_disparities;
+    a.eps = c->p.gf_eps;
+    // four volume sweeps, each reading and writing four channels (V0: reads one)
+    const double bytes = (double)n * nv * (4 + 16 + 32 + 32 + 16 + 4);
+    return timed(c, view == 0 ? "gf" : "gf_r", bytes, [&] { sm::launch_gf(a, n, c->st); });
+}
+
+// NL() on vm[0] (cpp:4892-4917): edge weights on the GPU, the tree on the host, the tree filter
+// on the GPU (sm_nl.hip, sm_nl_tree.cpp)
+sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
+    const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, np = c->npix;
+    const int H = c->p.rows, W = c->p.cols, D = c->p.num_disparities;
+    const size_t ne = (size_t)H * (W - 1) + (size_t)(H - 1) * W;
+    sm_status s = timed(c, "nl_edges", (double)n * np * 4, [&] {
+        sm::launch_nl_edges(B.bgr, 2 * np * 3, c->nl_med + off * np * 3, c->nl_ew + off * ne, H, W, n, c->st);
+    });
+    if (s) return s;
+    std::vector<uint8_t> ew((size_t)n * ne);
+    HIP_TRY(c, hipMemcpyAsync(ew.data(), c->nl_ew + off * ne, ew.size(), hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    std::vector<sm::NlTree> trees(n);
+    {
+        std::vector<char> ok(n, 0);
+        const int nth = std::max(1, std::min(n, (int)std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (int t = 0; t < nth; t++)
+            th.emplace_back([&, t] {
+                for (int b = t; b < n; b += nth) ok[b] = sm::nl_build_tree(H, W, ew.data() + (size_t)b * ne, trees[b]);
+            });
+        for (auto& x : th) x.join();
+        for (int b = 0; b < n; b++)
+            if (!ok[b]) return fail(c, SM_EINVAL, "NL: spanning tree construction failed");
+    }
+    // concatenate the pairs' trees (node ids b * npix + pixel) and order the paths by round
+    std::vector<int> cn, cs, cl, par((size_t)n * np), chi((size_t)n * np * 4), ord_up, ord_dn;
+    std::vector<uint8_t> wgt((size_t)n * np), nch((size_t)n * np);
+    std::vector<int8_t> hv((size_t)n * np);
+    std::vector<int> upl, dnl;
+    int max_up = 0, max_dn = 0;
+    for (int b = 0; b < n; b++) {
+        const sm::NlTree& t = trees[b];
+        const int base = b * (int)np;
+        const int c0 = (int)cs.size();
+        for (size_t k = 0; k < t.chain_start.size(); k++) {
+            cs.push_back(t.chain_start[k] + (int)cn.size());
+            cl.push_back(t.chain_len[k]);
+            upl.push_back(t.up_level[k]);
+            dnl.push_back(t.down_level[k]);
+            max_up = std::max(max_up, t.up_level[k]);
+            max_dn = std::max(max_dn, t.down_level[k]);
+        }
+        (void)c0;
+        for (int x : t.chain_nodes) cn.push_back(x + base);
+        for (size_t i = 0; i < np; i++) {
+            par[base + i] = t.parent[i] + base;
+            wgt[base + i] = t.weight[i];
+            nch[base + i] = t.nchild[i];
+            hv[base + i] = t.heavy[i];
+            for (int j = 0; j < 4; j++) {
+                const int q = t.child[i * 4 + j];
+                chi[(base + i) * 4 + j] = q < 0 ? -1 : q + base;
+            }
+        }
+    }
+    const int nchain = (int)cs.size();
+    std::vector<int> up_off(max_up + 2, 0), dn_off(max_dn + 2, 0);
+    for (int k = 0; k < nchain; k++) {
+        up_off[upl[k] + 1]++;
+        dn_off[dnl[k] + 1]++;
+    }
+    for (int r = 0; r <= max_up; r++) up_off[r + 1] += up_off[r];
+    for (int r = 0; r <= max_dn; r++) dn_off[r + 1] += dn_off[r];
+    ord_up.resize(nchain);
+    ord_dn.resize(nchain);
+    {
+        std::vector<int> pu(up_off.begin(), up_off.end() - 1), pd(dn_off.begin(), dn_off.end() - 1);
+        for (int k = 0; k < nchain; k++) {
+            ord_up[pu[upl[k]]++] = k;
+            ord_dn[pd[dnl[k]]++] = k;
+        }
+    }
+    // device tables: ints [10][cap * npix]: cn, cs, cl, ord_up, ord_dn, parent, child (4)
+    const size_t slot = (size_t)c->cap * np;
+    int* I = c->nl_ints;
+    uint8_t* U = c->nl_bytes;
+    HIP_TRY(c, hipMemcpy(I + 0 * slot, cn.data(), cn.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 1 * slot, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 2 * slot, cl.data(), cl.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 3 * slot, ord_up.data(), ord_up.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 4 * slot, ord_dn.data(), ord_dn.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 5 * slot, par.data(), par.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 6 * slot, chi.data(), chi.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(U + 0 * slot, wgt.data(), wgt.size(), hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(U + 1 * slot, nch.data(), nch.size(), hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(U + 2 * slot, hv.data(), hv.size(), hipMemcpyHostToDevice));
+    sm::NlArgs a{};
+    a.chain_nodes = I;
+    a.chain_start = I + slot;
+    a.chain_len = I + 2 * slot;
+    a.order_up = I + 3 * slot;
+    a.order_down = I + 4 * slot;
+    a.parent = I + 5 * slot;
+    a.child = I + 6 * slot;
+    a.weight = U;
+    a.nchild = U + slot;
+    a.heavy = (const int8_t*)(U + 2 * slot);
+    a.table = c->nl_table;
+    a.val = c->nl_val;
+    a.vm = B.vm0;
+    a.wsum = c->nl_wsum;
+    // the ones pass (weight sums), then the cost volume; each pass: up rounds, then down rounds
+    const double bytes = (double)n * c->nvol * (4 + 8 + 8 + 8 + 8 + 4);
+    return timed(c, "nl_filter", bytes, [&] {
+        for (int P : {1, D}) {
+            for (int r = 0; r <= max_up; r++) sm::launch_nl_round(a, true, up_off[r], up_off[r + 1], P, c->st);
+            for (int r = 0; r <= max_dn; r++) sm::launch_nl_round(a, false, dn_off[r], dn_off[r + 1], P, c->st);
+        }
+    });
+}
+
+// aggregation other than CBCA: GF on every view (num = Do_refine ? 2 : 1, cpp:4499), NL on vm[0]
+sm_status run_other_agg(sm_ctx* c, int n, const Bufs& B) {
+    sm_status s = SM_OK;
+    if (c->p.aggregation == SM_AGG_GF)
+        for (int v = 0; v < n_views(c->p) && !s; v++) s = run_gf(c, n, v, B);
+    if (c->p.aggregation == SM_AGG_NL) s = run_nl(c, n, B);
+    return s;
+}
+
 sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
     const sm_params& p = c->p;
     float* vm = view == 0 ? B.vm0 : B.vm1;
@@ -437,6 +608,7 @@ sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
         a.cor_thres = p.sgm_cor_dif_thres;
         a.redu = p.sgm_redu_coeff;
         a.keep_final = p.keep_final_volume;
+        a.signed_costs = p.aggregation == SM_AGG_GF;   // the guided filter's output can be < 0
         for (int i = 0; i < p.sgm_paths; i++) {
             a.rv = RV[i];
             a.ru = RU[i];
@@ -588,6 +760,8 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->sub_batch = 0;
     p->num_streams = 1;
     p->fuse_norm_scan = 0;
+    p->gf_eps = 0.0001f;        // guideFilterCore_matlab(I, p, 9, 0.0001) (cpp:4509)
+    p->nl_sigma = 0.1;          // NLCCA::aggreCV (NL/NLCCA.cpp:33)
 }
 
 const char* sm_status_string(sm_status s) {
@@ -654,6 +828,25 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->disp_tmp, cap * c->npix))) return s;
     }
     if ((s = dalloc(c, &c->px, 3 * cap * 2 * c->npix))) return s;
+    if (p->aggregation == SM_AGG_GF) {
+        if ((s = dalloc(c, &c->gf_s, (c->acc ? 3 : 4) * cap * c->nvol))) return s;
+        if ((s = dalloc(c, &c->gf_planes, cap * 10 * c->npix))) return s;
+        if ((s = dalloc(c, &c->gf_pix, cap * c->npix))) return s;
+    }
+    if (p->aggregation == SM_AGG_NL) {
+        const size_t ne = (size_t)p->rows * (p->cols - 1) + (size_t)(p->rows - 1) * p->cols;
+        if ((s = dalloc(c, &c->nl_med, cap * c->npix * 3))) return s;
+        if ((s = dalloc(c, &c->nl_ew, cap * ne))) return s;
+        if ((s = dalloc(c, &c->nl_ints, cap * c->npix * 10))) return s;
+        if ((s = dalloc(c, &c->nl_bytes, cap * c->npix * 3))) return s;
+        if ((s = dalloc(c, &c->nl_table, 256))) return s;
+        if ((s = dalloc(c, &c->nl_val, cap * c->nvol))) return s;
+        if ((s = dalloc(c, &c->nl_wsum, cap * c->npix))) return s;
+        double table[256];
+        const double sg = p->nl_sigma < 0.01 ? 0.01 : p->nl_sigma;   // update_table (qx_tree_filter.cpp:23-24)
+        for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));
+        HIP_TRY(c, hipMemcpy(c->nl_table, table, sizeof(table), hipMemcpyHostToDevice));
+    }
     build_luts(c);
     {
         c->fuse_norm_scan = p->fuse_norm_scan != 0;
@@ -703,6 +896,7 @@ sm_status sm_cost_calculate(sm_ctx* c) {
     if (c->p.aggregation == SM_AGG_CBCA)
         for (int v = 0; v < n_views(c->p); v++)
             if ((s = run_cbca(c, n, v, false, 1.0f, B))) return s;
+    if ((s = run_other_agg(c, n, B))) return s;
     c->stage = 2;
     return SM_OK;
 }
@@ -968,6 +1162,7 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
         if ((s_out = run_prep(c, m2, B))) break;
         if ((s_out = run_cost(c, m2, 0, B))) break;
         if (right_view(c->p) && (s_out = run_cost(c, m2, 1, B))) break;
+        if ((s_out = run_other_agg(c, m2, B))) break;
         for (int v = 0; v < n_views(c->p) && !s_out; v++) {
             if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0)
                 s_out = run_cbca(c, m2, v, true, w, B);   // SolveAll fused into the last pass

@@ -1,0 +1,281 @@
+// sm_gf.hip — aggregation "GF" (guideFilter, stereoMatching.cpp:4492-4516) in its MY_GUIDE form:
+// per disparity slice p, guideFilterCore_matlab(I, p, 9, 0.0001) (cpp:4975-5104), the colour
+// guided filter of He et al. with the reference's own BoxFilter / CumSum (cpp:5107-5202):
+//
+//   BoxFilter(x) = column cumulative sums S (row 0 = 0 + x), out(y) = S(y + r) - S(y - r - 1)
+//                  (S(y + r) alone for y <= r, S(H - 1) for y + r >= H), then the same along rows
+//   mean_p = box(p) / N, mean_Ip[c] = box(I_c p) / N, cov[c] = mean_Ip[c] - mean_I[c] mean_p
+//   a = cov^T (Sigma + eps E)^-1  (double cofactors, per pixel), b = mean_p - sum_c a[c] mean_I[c]
+//   q = box(b) / N + sum_c box(a[c]) / N * I_c
+//
+// gfx950 mapping.  The p-independent per-pixel terms (N, mean_I, the 3x3 inverse's cofactors and
+// 1 / DET in double) come from 10 image planes box-filtered once per pair (k_gf_img_v / _h,
+// k_gf_pix).  The volume work is four line sweeps over [H][W][D] (lane = disparity, one wave per
+// (line, 64-disparity chunk)), each carrying four channels at once:
+//   V0: column box of (p, B p, G p, R p)           -> s0..s3
+//   H0: row box, then mean_p, cov, a[0..2], b      -> s0..s3 (in place, behind the read front)
+//   V1: column box of (a0, a1, a2, b)              -> s0..s3 (in place)
+//   H1: row box, then q                            -> vm
+// The cumulative sum of a line lives in a register ring of 2r + 2 = 20 slots (r = 9, the
+// reference's constant): the loop is unrolled by 20 so every slot index is static; positions past
+// the line end add 0, which leaves S(H - 1) in place for the last r outputs.  Every operation is
+// the reference's, in its order (float adds of the cumulative sums, IEEE divisions by N, the
+// double inverse as written, float products), so the volume is bit-exact to the restatement.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sm_device.h"
+#include "sm_kernels.h"
+
+namespace sm {
+
+namespace {
+
+constexpr int GF_R = 9;                // guideFilterCore_matlab(I, p, 9, eps) (cpp:4509)
+constexpr int GF_RING = 2 * GF_R + 2;  // S(j) .. S(j - 2r - 1)
+
+// ---------------------------------------------------------------------------------------------
+// Image planes: 0 = ones, 1..3 = B, G, R, 4..9 = BB, BG, BR, GG, GR, RR (var_I order, cpp:5005-5016)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float gf_plane(const uint8_t* px, int k) {
+    const float b = (float)px[0], g = (float)px[1], r = (float)px[2];
+    switch (k) {
+        case 0: return 1.0f;
+        case 1: return b;
+        case 2: return g;
+        case 3: return r;
+        case 4: return b * b;
+        case 5: return b * g;
+        case 6: return b * r;
+        case 7: return g * g;
+        case 8: return g * r;
+        default: return r * r;
+    }
+}
+
+// one thread per (pair, plane, column): column box of the plane into planes[b][k][H][W]
+__global__ __launch_bounds__(256) void k_gf_img_v(const uint8_t* __restrict__ bgr, float* __restrict__ planes, int H, int W,
+                                                  int n, size_t bgr_pair_stride) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * 10 * W) return;
+    const int x = t % W, k = (t / W) % 10, b = t / (W * 10);
+    const uint8_t* src = bgr + (size_t)b * bgr_pair_stride + (size_t)x * 3;
+    float* out = planes + ((size_t)b * 10 + k) * H * W + x;
+    float ring[GF_RING];
+    float S = 0.f;
+    for (int j0 = 0; j0 < H + GF_R; j0 += GF_RING) {
+#pragma unroll
+        for (int s = 0; s < GF_RING; s++) {
+            const int j = j0 + s;
+            if (j < H + GF_R) {
+                const float v = j < H ? gf_plane(src + (size_t)j * W * 3, k) : 0.f;
+                S = (j == 0 ? 0.f : S) + v;   // CumSum(., 1): 0 + x on row 0; past the end + 0 keeps S(H - 1)
+                ring[s] = S;
+                const int i = j - GF_R;
+                if (i >= 0) out[(size_t)i * W] = i >= GF_R + 1 ? S - ring[(s + 1) % GF_RING] : S;
+            }
+        }
+    }
+}
+
+// one thread per (pair, plane, row): row box in place
+__global__ __launch_bounds__(256) void k_gf_img_h(float* __restrict__ planes, int H, int W, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * 10 * H) return;
+    float* row = planes + (size_t)t * W;   // planes are [b][k][H][W]: thread t owns row t
+    float ring[GF_RING];
+    float S = 0.f;
+    for (int j0 = 0; j0 < W + GF_R; j0 += GF_RING) {
+#pragma unroll
+        for (int s = 0; s < GF_RING; s++) {
+            const int j = j0 + s;
+            if (j < W + GF_R) {
+                if (j < W) S = (j == 0) ? row[0] : S + row[j];   // CumSum(., 2): x = 0 copies
+                ring[s] = S;
+                const int i = j - GF_R;
+                if (i >= 0) row[i] = i >= GF_R + 1 ? S - ring[(s + 1) % GF_RING] : S;
+            }
+        }
+    }
+}
+
+// per pixel: N, mean_I, and the 3x3 inverse's p-independent doubles (cpp:5003-5078)
+__global__ __launch_bounds__(256) void k_gf_pix(const float* __restrict__ planes, GfPix* __restrict__ pix, int H, int W, int n,
+                                                float eps) {
+    const size_t npix = (size_t)H * W;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= npix * n) return;
+    const size_t b = t / npix, i = t - b * npix;
+    const float* pl = planes + b * 10 * npix + i;
+    const float N = pl[0];
+    float mI[3], var[6];
+#pragma unroll
+    for (int c = 0; c < 3; c++) mI[c] = pl[(1 + c) * npix] / N;
+    int vi = 0;
+#pragma unroll
+    for (int c0 = 0; c0 < 3; c0++)
+#pragma unroll
+        for (int c1 = c0; c1 < 3; c1++, vi++) {
+            float v = pl[(4 + vi) * npix] / N;
+            const float m = mI[c0] * mI[c1];
+            var[vi] = v - m;
+        }
+    const double a11 = var[0] + eps, a12 = var[1], a13 = var[2];
+    const double a21 = var[1], a22 = var[3] + eps, a23 = var[4];
+    const double a31 = var[2], a32 = var[4], a33 = var[5] + eps;
+    GfPix r;
+    const double DET = a11 * (a33 * a22 - a32 * a23) - a21 * (a33 * a12 - a32 * a13) + a31 * (a23 * a12 - a22 * a13);
+    r.cof[0] = a33 * a22 - a32 * a23;
+    r.cof[1] = a31 * a23 - a33 * a21;
+    r.cof[2] = a32 * a21 - a31 * a22;
+    r.cof[3] = a32 * a13 - a33 * a12;
+    r.cof[4] = a33 * a11 - a31 * a13;
+    r.cof[5] = a31 * a12 - a32 * a11;
+    r.cof[6] = a23 * a12 - a22 * a13;
+    r.cof[7] = a21 * a13 - a23 * a11;
+    r.cof[8] = a22 * a11 - a21 * a12;
+    r.idet = 1 / DET;
+    r.N = N;
+    r.mI[0] = mI[0];
+    r.mI[1] = mI[1];
+    r.mI[2] = mI[2];
+    pix[t] = r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Volume sweeps: one wave per (pair, line, 64-disparity chunk), lane = disparity
+// ---------------------------------------------------------------------------------------------
+template <bool HORIZ, int MODE>   // MODE 0: first box (from p), MODE 1: second box (from a, b)
+__global__ __launch_bounds__(64) void k_gf_sweep(const GfArgs a) {
+    const int lane = threadIdx.x;
+    const int nchunks = (a.D + 63) >> 6;
+    const int lines = HORIZ ? a.H : a.W;
+    const int blk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int b = blk / (lines * nchunks);
+    const int lc = blk - b * lines * nchunks;
+    const int line = lc / nchunks, chunk = lc - line * nchunks;
+    const int d = chunk * 64 + lane;
+    const bool live = d < a.D;
+    const int dd = live ? d : a.D - 1;
+    const size_t npix = (size_t)a.H * a.W;
+    const int len = HORIZ ? a.W : a.H;
+    const size_t pstep = HORIZ ? 1 : (size_t)a.W;            // pixels between positions
+    const size_t p0 = (size_t)b * npix + (HORIZ ? (size_t)line * a.W : (size_t)line);
+    const size_t vstep = pstep * a.D;
+    const size_t v0 = p0 * a.D + dd;
+    const uint8_t* px0 = a.bgr + (size_t)b * a.bgr_pair_stride + (HORIZ ? (size_t)line * a.W : (size_t)line) * 3;
+    float* const s[4] = {a.s0, a.s1, a.s2, a.s3};
+
+    float ring[4][GF_RING];
+    float S[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j0 = 0; j0 < len + GF_R; j0 += GF_RING) {
+        // inputs of this block of positions
+        float x[GF_RING][4];
+#pragma unroll
+        for (int sl = 0; sl < GF_RING; sl++) {
+            const int j = j0 + sl;
+            const bool in = j < len;
+            const size_t jv = (size_t)(in ? j : len - 1);
+            if (!HORIZ && MODE == 0) {
+                const float p = a.vm[v0 + jv * vstep];
+                const uint8_t* q = px0 + jv * pstep * 3;
+                x[sl][0] = p;
+                x[sl][1] = (float)q[0] * p;   // multiply(I_ch[c], p) (cpp:4992)
+                x[sl][2] = (float)q[1] * p;
+                x[sl][3] = (float)q[2] * p;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; c++) x[sl][c] = s[c][v0 + jv * vstep];
+            }
+            if (!in) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) x[sl][c] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int sl = 0; sl < GF_RING; sl++) {
+            const int j = j0 + sl;
+            if (j >= len + GF_R) break;
+            float bx[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                // CumSum: 0 + x at the first row (V), x itself at the first column (H); past the
+                // end + 0, which keeps S(len - 1) (S is never -0)
+                S[c] = (j == 0) ? (HORIZ ? x[sl][c] : 0.f + x[sl][c]) : S[c] + x[sl][c];
+                ring[c][sl] = S[c];
+            }
+            const int i = j - GF_R;
+            if (i < 0) continue;
+#pragma unroll
+            for (int c = 0; c < 4; c++) bx[c] = i >= GF_R + 1 ? S[c] - ring[c][(sl + 1) % GF_RING] : S[c];
+            const size_t vo = v0 + (size_t)i * vstep;
+            if (!HORIZ) {
+                if (live) {
+#pragma unroll
+                    for (int c = 0; c < 4; c++) s[c][vo] = bx[c];
+                }
+                continue;
+            }
+            const GfPix& P = a.pix[p0 + (size_t)i * pstep];
+            const float N = P.N;
+            if (MODE == 0) {
+                const float mean_p = bx[0] / N;
+                double cv[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float mIp = bx[1 + c] / N;
+                    const float m = P.mI[c] * mean_p;
+                    cv[c] = (double)(mIp - m);
+                }
+                float av[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+                    av[c] = (float)(P.idet * (cv[0] * P.cof[3 * c] + cv[1] * P.cof[3 * c + 1] + cv[2] * P.cof[3 * c + 2]));
+                float bb = mean_p;
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float m = av[c] * P.mI[c];
+                    bb -= m;
+                }
+                if (live) {
+                    s[0][vo] = av[0];
+                    s[1][vo] = av[1];
+                    s[2][vo] = av[2];
+                    s[3][vo] = bb;
+                }
+            } else {
+                const uint8_t* q = px0 + (size_t)i * 3;
+                float out = bx[3] / N;   // q = mean_b (cpp:5097)
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float ma = bx[c] / N;
+                    const float m = ma * (float)q[c];
+                    out += m;
+                }
+                if (live) a.vm[vo] = out;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+void launch_gf(const GfArgs& a, int n, hipStream_t st) {
+    {
+        const int th = n * 10 * a.W;
+        hipLaunchKernelGGL(k_gf_img_v, dim3((th + 255) / 256), dim3(256), 0, st, a.bgr, a.planes, a.H, a.W, n, a.bgr_pair_stride);
+        const int tr = n * 10 * a.H;
+        hipLaunchKernelGGL(k_gf_img_h, dim3((tr + 255) / 256), dim3(256), 0, st, a.planes, a.H, a.W, n);
+        const size_t tp = (size_t)n * a.H * a.W;
+        hipLaunchKernelGGL(k_gf_pix, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, st, a.planes, a.pix, a.H, a.W, n, a.eps);
+    }
+    GfArgs g = a;
+    const int nchunks = (a.D + 63) / 64;
+    hipLaunchKernelGGL((k_gf_sweep<false, 0>), dim3(a.W * nchunks * n), dim3(64), 0, st, g);
+    hipLaunchKernelGGL((k_gf_sweep<true, 0>), dim3(a.H * nchunks * n), dim3(64), 0, st, g);
+    hipLaunchKernelGGL((k_gf_sweep<false, 1>), dim3(a.W * nchunks * n), dim3(64), 0, st, g);
+    hipLaunchKernelGGL((k_gf_sweep<true, 1>), dim3(a.H * nchunks * n), dim3(64), 0, st, g);
+}
+
+}  // namespace sm

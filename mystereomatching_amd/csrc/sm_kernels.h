@@ -7,7 +7,8 @@
 namespace sm {
 
 enum { SM_M_CENSUS_GRAD = 0, SM_M_CENSUS = 1, SM_M_AD_CENSUS = 2, SM_M_AD = 3 };
-enum { SGM_FIRST = 1, SGM_LAST = 2, SGM_KEEP = 4 };  // KEEP: last path also writes the summed volume
+enum { SGM_FIRST = 1, SGM_LAST = 2, SGM_KEEP = 4, SGM_SIGNED = 8 };  // KEEP: last path also writes the summed volume;
+// SIGNED: costs may be negative (the guided filter's output), minima compare as floats
 enum { CB_SCAN = 0, CB_NORM = 1, CB_NORM_SCAN = 2 };
 constexpr int CBCA_TILE = 16;  // steps of lookahead per wave in the CBCA line sweeps
 
@@ -69,8 +70,47 @@ struct SgmArgs {
     int H, W, D, rv, ru, dir;
     float p1, p2;
     int cor_thres, redu, keep_final;
+    int signed_costs;           // 1: C may be < 0 (aggregation GF): k_sgm with float minima
     int n;                      // pairs in the launch
 };
+
+struct GfPix {                  // guided filter, p-independent terms of one pixel (sm_gf.hip)
+    double cof[9];              // the nine cofactor expressions of guideFilterCore_matlab (cpp:5060-5078)
+    double idet;                // 1 / DET
+    float N;                    // BoxFilter(ones)
+    float mI[3];                // mean_I[c], BGR
+};
+
+struct GfArgs {
+    float* vm;                  // [n][H][W][D], filtered in place
+    float *s0, *s1, *s2, *s3;   // four scratch volumes [n][H][W][D]
+    const uint8_t* bgr;         // the view's colour image of pair 0 ([n][2][H][W][3] + view offset)
+    size_t bgr_pair_stride;     // bytes between pairs
+    float* planes;              // [n][10][H][W] scratch
+    GfPix* pix;                 // [n][H][W]
+    int H, W, D;
+    float eps;
+};
+void launch_gf(const GfArgs& a, int n, hipStream_t st);
+
+struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids = pair * H W + pixel
+    const int* chain_nodes;     // heavy paths, each bottom -> top
+    const int* chain_start;
+    const int* chain_len;
+    const int* order_up;        // path indices sorted by up round
+    const int* order_down;      // path indices sorted by down round
+    const int* parent;          // [nodes] (the root is its own parent)
+    const uint8_t* weight;      // [nodes] edge weight to the parent
+    const uint8_t* nchild;      // [nodes]
+    const int* child;           // [nodes][4]
+    const int8_t* heavy;        // [nodes] child index continuing the path, -1 at leaves
+    const double* table;        // exp(-i / (255 sigma)), i = 0..255
+    double* val;                // [nodes][P] up sums, then final values (in place)
+    float* vm;                  // [nodes][D] costs in, normalised aggregated costs out
+    float* wsum;                // [nodes] the filtered ones (P = 1 pass)
+};
+void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8_t* ew, int H, int W, int n, hipStream_t st);
+void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_t st);
 
 struct SoArgs {                 // scan-line optimisation "so" (sm_so.hip)
     float* vm;                  // [n][H][W][D] costs (accumulated in place when keep_final)

@@ -1,0 +1,164 @@
+// sm_nl_tree.cpp — host side of aggregation "NL" (NL(), stereoMatching.cpp:4892-4917 ->
+// NLCCA::aggreCV, NL/NLCCA.cpp:27-96): the minimum spanning tree of the left colour image and its
+// breadth-first orientation (NL/qx_mst_kruskals_image.cpp:167-277), cut into heavy paths for the
+// GPU tree filter (sm_nl.hip).
+//
+// The tree is the reference's, edge for edge: the GPU's edge weights (max channel difference of
+// the 3x3-median-filtered image, horizontal edges row by row then vertical edges column by column)
+// are sorted stably by weight (a counting sort, qx_sort_increase_using_histogram), Kruskal accepts
+// an edge when its endpoints are in different components, and every accepted edge is appended to
+// both endpoints' neighbour lists; the breadth-first walk from pixel 0 then makes every neighbour
+// but the parent a child, in list order.  Kruskal's acceptance and the neighbour-list order depend
+// only on the edge order, not on the union-find details.
+//
+// Heavy paths: every node continues the path of its largest child (the first of equal sizes), so
+// any root path crosses at most log2(n) path boundaries.  The up pass of the filter runs the paths
+// in rounds of "up level" (1 + the largest level of a path hanging off it, 0 for none), the down
+// pass in rounds of depth in the path tree; each round is one launch in which a wave walks a whole
+// path sequentially, the child on its own path arriving in a register and the others from memory.
+// The per-node arithmetic and its order are the reference's (sm_nl.hip), so the rounds only
+// schedule work.  This graph construction is O(n) host work per pair (pairs run on parallel host
+// threads); the O(n D) filtering is on the GPU.
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "sm_nl_tree.h"
+
+namespace sm {
+
+// Builds the tree of one pair (pixel ids 0 .. H W - 1) into t; returns false if the graph is
+// not connected (cannot happen for a 4-neighbour grid with H W > 1).
+bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
+    const int n = H * W;
+    const int neh = H * (W - 1), ne = neh + (H - 1) * W;
+    t.n = n;
+    // stable counting sort of the edges by weight
+    std::vector<int> order_e((size_t)std::max(ne, 1));
+    {
+        int start[257];
+        memset(start, 0, sizeof(start));
+        for (int e = 0; e < ne; e++) start[ew[e] + 1]++;
+        for (int v = 0; v < 256; v++) start[v + 1] += start[v];
+        for (int e = 0; e < ne; e++) order_e[start[ew[e]]++] = e;
+    }
+    auto ends = [&](int e, int& u, int& v) {
+        if (e < neh) {   // horizontal: row y, columns x, x + 1
+            const int y = e / (W - 1), x = e - y * (W - 1);
+            u = y * W + x;
+            v = u + 1;
+        } else {         // vertical: column x, rows y, y + 1
+            const int k = e - neh, x = k / (H - 1), y = k - x * (H - 1);
+            u = y * W + x;
+            v = u + W;
+        }
+    };
+    // Kruskal: union-find with path halving and union by size (the accepted set is independent
+    // of how the components are merged)
+    std::vector<int> uf(n), sz(n, 1), nconn(n, 0), conn((size_t)n * 4);
+    std::vector<uint8_t> connw((size_t)n * 4);
+    for (int i = 0; i < n; i++) uf[i] = i;
+    auto find = [&](int x) {
+        while (uf[x] != x) {
+            uf[x] = uf[uf[x]];
+            x = uf[x];
+        }
+        return x;
+    };
+    int accepted = 0;
+    for (int j = 0; j < ne && accepted < n - 1; j++) {
+        const int e = order_e[j];
+        int u, v;
+        ends(e, u, v);
+        int ru = find(u), rv = find(v);
+        if (ru == rv) continue;
+        if (sz[ru] < sz[rv]) std::swap(ru, rv);
+        uf[rv] = ru;
+        sz[ru] += sz[rv];
+        conn[(size_t)u * 4 + nconn[u]] = v;
+        connw[(size_t)u * 4 + nconn[u]++] = ew[e];
+        conn[(size_t)v * 4 + nconn[v]] = u;
+        connw[(size_t)v * 4 + nconn[v]++] = ew[e];
+        accepted++;
+    }
+    if (accepted != n - 1) return false;
+    // breadth-first orientation from pixel 0 (build_tree)
+    t.parent.assign(n, -1);
+    t.weight.assign(n, 0);
+    t.nchild.assign(n, 0);
+    t.child.assign((size_t)n * 4, -1);
+    std::vector<int> bfs(n);
+    t.parent[0] = 0;
+    bfs[0] = 0;
+    int head = 0, len = 1;
+    while (head < len) {
+        const int p = bfs[head++];
+        for (int i = 0; i < nconn[p]; i++) {
+            const int q = conn[(size_t)p * 4 + i];
+            if (t.parent[q] != -1) continue;
+            t.parent[q] = p;
+            t.weight[q] = connw[(size_t)p * 4 + i];
+            t.child[(size_t)p * 4 + t.nchild[p]++] = q;
+            bfs[len++] = q;
+        }
+    }
+    if (len != n) return false;
+    // subtree sizes, heavy children
+    std::vector<int> size(n, 1);
+    for (int i = n - 1; i > 0; i--) size[t.parent[bfs[i]]] += size[bfs[i]];
+    t.heavy.assign(n, -1);
+    for (int x = 0; x < n; x++) {
+        int best = -1, bs = 0;
+        for (int j = 0; j < t.nchild[x]; j++)
+            if (size[t.child[(size_t)x * 4 + j]] > bs) {
+                bs = size[t.child[(size_t)x * 4 + j]];
+                best = j;
+            }
+        t.heavy[x] = (int8_t)best;
+    }
+    // heavy paths in BFS order of their tops; nodes stored bottom -> top
+    std::vector<int> chain_of(n, -1);
+    t.chain_start.clear();
+    t.chain_len.clear();
+    t.chain_nodes.clear();
+    t.chain_nodes.reserve(n);
+    std::vector<int> tops;
+    for (int i = 0; i < n; i++) {
+        const int x = bfs[i];
+        if (x != 0 && t.heavy[t.parent[x]] >= 0 && t.child[(size_t)t.parent[x] * 4 + t.heavy[t.parent[x]]] == x) continue;
+        tops.push_back(x);
+    }
+    const int nch = (int)tops.size();
+    std::vector<int> path;
+    for (int c = 0; c < nch; c++) {
+        path.clear();
+        for (int x = tops[c];; x = t.child[(size_t)x * 4 + t.heavy[x]]) {
+            path.push_back(x);
+            chain_of[x] = c;
+            if (t.heavy[x] < 0) break;
+        }
+        t.chain_start.push_back((int)t.chain_nodes.size());
+        t.chain_len.push_back((int)path.size());
+        for (int k = (int)path.size() - 1; k >= 0; k--) t.chain_nodes.push_back(path[k]);
+    }
+    // rounds: up level from the leaves' side (reverse top order), down level from the root
+    t.up_level.assign(nch, 0);
+    t.down_level.assign(nch, 0);
+    for (int c = nch - 1; c >= 0; c--) {
+        int lv = 0;
+        const int* nodes = t.chain_nodes.data() + t.chain_start[c];
+        for (int k = 0; k < t.chain_len[c]; k++) {
+            const int x = nodes[k];
+            for (int j = 0; j < t.nchild[x]; j++)
+                if (j != t.heavy[x]) lv = std::max(lv, t.up_level[chain_of[t.child[(size_t)x * 4 + j]]] + 1);
+        }
+        t.up_level[c] = lv;
+    }
+    for (int c = 1; c < nch; c++) t.down_level[c] = t.down_level[chain_of[t.parent[tops[c]]]] + 1;
+    return true;
+}
+
+}  // namespace sm

@@ -80,6 +80,7 @@ struct SgmTile {
 
 template <int K, int MODE, int T, bool FULL, bool VEC>
 __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
+    constexpr bool SG = (MODE & SGM_SIGNED) != 0;
     // VEC (D % 4 == 0, K % 4 == 0): each lane's K consecutive disparities move as K / 4 dwordx4
     // accesses, so a step of a line is one contiguous D * 4-byte access per volume
     constexpr int KV = VEC ? K / 4 : 1;
@@ -202,6 +203,8 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
 
     // All path costs are >= +0 (C >= 0; Lp - m >= 0; Lp[d +/- 1] + (P1 - m) >= 0 because
     // fl(P1 - m) >= -m; P2 > 0), so every min below is an exact unsigned min on the bit patterns.
+    // SIGNED (guided-filter costs, which can be negative but are never -0 or NaN, nor are the
+    // sums of them): v_min_f32 minima, which then equal the reference's std::min exactly.
     // Out-of-range neighbours (d - 1 < 0, d + 1 >= D) hold FLT_MAX from the DPP shift's bound
     // value or the padded lanes; FLT_MAX + (P1 - m) never undercuts P2 <= 3, so those terms
     // cannot win the min and need no separate select.
@@ -216,8 +219,8 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
             const float P1 = pen ? p1r : p1, P2 = pen ? p2r : p2;
             float lm = Lp[0];
 #pragma unroll
-            for (int k = 1; k < K; k++) lm = fmin_pos(lm, Lp[k]);
-            const float m = wave_min_pos(lm);           // wave-uniform
+            for (int k = 1; k < K; k++) lm = SG ? fminf(lm, Lp[k]) : fmin_pos(lm, Lp[k]);
+            const float m = SG ? wave_min(lm) : wave_min_pos(lm);   // wave-uniform
             const float P1m = P1 - m;
             const float left = dpp_shr1<K>(Lp[K - 1]);
             const float right = dpp_shl1<K>(Lp[0]);
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
                 const float S1 = Lp[k] - m;
                 const float S2 = prev + P1m;
                 const float S3 = next + P1m;
-                const float mm = fmin_pos(fmin_pos(S1, S2), fmin_pos(S3, P2));
+                const float mm = SG ? fminf(fminf(S1, S2), fminf(S3, P2)) : fmin_pos(fmin_pos(S1, S2), fmin_pos(S3, P2));
                 const float Lk = t.c[s][k] + mm;
                 L[k] = (FULL || val[k]) ? Lk : FLT_MAX;
             }
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(256) void k_sgm(const SgmArgs a) {
                 }
             // first minimum: lowest lane holding the wave minimum, then that lane's first index
             // (padded lanes hold FLT_MAX and only match when every cost is FLT_MAX -> -1)
-            const float wm = wave_min_pos(bm);
+            const float wm = SG ? wave_min(bm) : wave_min_pos(bm);
             const uint64_t hit = __ballot(bm == wm);
             const int widx = __builtin_amdgcn_readlane(bi, (int)__builtin_ctzll(hit));
             const int dsel = (wm < FLT_MAX) ? widx : -1;
@@ -536,8 +539,35 @@ static void launch_kf(const SgmArgs& a, int mode, int n, hipStream_t st) {
     }
 }
 
+template <int K, bool FULL, bool VEC = false>
+static void launch_kf_signed(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    const int nlines = a.rv == 0 ? a.H : (a.ru == 0 ? a.W : a.W + a.H - 1);
+    dim3 grid((nlines + 3) / 4, n);
+    constexpr int T = VEC ? (K == 4 ? SM_SGM_T_V4 : SM_SGM_T_BIG)
+                          : (K >= 8 ? SM_SGM_T_BIG : (K == 3 ? SM_SGM_T_K3 : (K == 4 ? SM_SGM_T_K4 : (K == 1 ? SM_SGM_T_K1 : 16 / K))));
+    constexpr int S = SGM_SIGNED;
+    if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
+    switch (mode) {
+        case SGM_FIRST: hipLaunchKernelGGL((k_sgm<K, S | SGM_FIRST, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST: hipLaunchKernelGGL((k_sgm<K, S | SGM_LAST, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST | SGM_KEEP: hipLaunchKernelGGL((k_sgm<K, S | SGM_LAST | SGM_KEEP, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm<K, S | SGM_FIRST | SGM_LAST, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST | SGM_KEEP:
+            hipLaunchKernelGGL((k_sgm<K, S | SGM_FIRST | SGM_LAST | SGM_KEEP, T, FULL, VEC>), grid, dim3(256), 0, st, a);
+            break;
+        default: hipLaunchKernelGGL((k_sgm<K, S, T, FULL, VEC>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
 template <int K>
 static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    if (a.signed_costs) {
+        if (a.D == 64 * K)
+            launch_kf_signed<K, true>(a, mode, n, st);
+        else
+            launch_kf_signed<K, false>(a, mode, n, st);
+        return;
+    }
     if (a.D == 64 * K)
         launch_kf<K, true>(a, mode, n, st);
     else
@@ -552,7 +582,7 @@ static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
 // (tools/ubench_sgm.hip, KITTI D = 192: 3.5 TB/s with 4 lines per wave vs 5.0 TB/s with one).
 static int rows_kv(const SgmArgs& a, int mode) {
     static const int mask = [] { const char* e = getenv("SM_SGM_ROWS"); return e ? (int)strtol(e, nullptr, 0) : -1; }();
-    if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > SM_SGM_VEC_MIN_D) return 0;
+    if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > SM_SGM_VEC_MIN_D || a.signed_costs) return 0;
     const bool use = mask >= 0 ? ((mask >> a.dir) & 1) : (a.ru == 0 || (mode & SGM_LAST));
     if (!use) return 0;
     const int K = (a.D + 15) / 16;
@@ -570,6 +600,13 @@ void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {
         default: break;
     }
     if (a.D > SM_SGM_VEC_MIN_D && a.D <= 256 && a.D % 4 == 0) {  // one line per wave, dwordx4 per lane
+        if (a.signed_costs) {
+            if (a.D == 256)
+                launch_kf_signed<4, true, true>(b, mode, n, st);
+            else
+                launch_kf_signed<4, false, true>(b, mode, n, st);
+            return;
+        }
         if (a.D == 256)
             launch_kf<4, true, true>(b, mode, n, st);
         else

@@ -33,12 +33,20 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_params_struct_layout_and_defaults():
-    # every field of struct sm_params is 4 bytes; the header's field count must match ctypes
+    # struct sm_params: 4-byte fields and one double; the header's C layout must match ctypes
     txt = open(os.path.join(ROOT, "include", "sm_capi.h")).read()
     body = txt[txt.index("typedef struct sm_params {"):txt.index("} sm_params;")]
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    nfields = sum(len(re.findall(r"\b\w+\s*(?:,|;)", ln)) for ln in body.splitlines()[1:])
-    assert C.sizeof(_capi.sm_params) == 4 * nfields
+    off, align = 0, 4
+    for ln in body.splitlines()[1:]:
+        ln = ln.strip()
+        if not ln:
+            continue
+        size = 8 if ln.startswith("double") else 4
+        for _ in re.findall(r"\b\w+\s*(?:,|;)", ln):
+            off = (off + size - 1) // size * size + size
+            align = max(align, size)
+    assert C.sizeof(_capi.sm_params) == (off + align - 1) // align * align
     p = _capi.default_params(59, 375, 450)
     assert p.num_disparities == 60
     assert (p.census_rv, p.census_ru, p.census_ring) == (3, 4, 1)
@@ -50,6 +58,7 @@ def test_params_struct_layout_and_defaults():
     assert (p.do_proper_ipol, p.disp_occ, p.do_last_median_blur) == (1, -32, 1)
     assert np.float32(p.rv_ratio) == np.float32(0.4)
     assert (p.sub_batch, p.num_streams, p.fuse_norm_scan) == (0, 1, 0)
+    assert np.float32(p.gf_eps) == np.float32(1e-4) and p.nl_sigma == 0.1
 
 
 @pytest.mark.parametrize("field,value,msg", [
@@ -59,7 +68,8 @@ def test_params_struct_layout_and_defaults():
     ("lam_g", -1.0, b"lambda"), ("grad_trunc", -5.0, b"truncation"), ("sgm_p2", -1.0, b"penalties"),
     ("sgm_redu_coeff", -4, b"penalties"), ("sgm_p2", -0.0, b"penalties"), ("sgm_p1", -0.0, b"penalties"),
     ("grad_trunc", -0.0, b"truncation"), ("ad_trunc_ad", -0.0, b"truncation"), ("num_streams", 5, b"num_streams"),
-    ("sub_batch", -1, b"sub_batch"),
+    ("sub_batch", -1, b"sub_batch"), ("aggregation", 4, b"aggregation"), ("gf_eps", 0.0, b"gf_eps"),
+    ("nl_sigma", 0.0, b"nl_sigma"),
 ])
 def test_validation_rejects_before_device(field, value, msg):
     lib = _capi.load()
@@ -127,3 +137,19 @@ def test_run_batch_multi_argument_checks():
     assert lib.sm_run_batch_multi(arr, 1, 1, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL
     assert lib.sm_run_batch_multi(arr, 0, 1, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL
     assert lib.sm_run_batch_multi(arr, 1, 0, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL
+
+
+@pytest.mark.parametrize("over,msg", [(dict(aggregation=2, rows=18), b"GF"), (dict(aggregation=2, optimization=2), b"GF"),
+                                      (dict(aggregation=3, rows=2, cols=2), b"NL")])
+def test_alternative_aggregator_domain(over, msg):
+    lib = _capi.load()
+    p = _capi.default_params(15, 32, 32)
+    for k, v in over.items():
+        setattr(p, k, v)
+    ctx = C.c_void_p()
+    st = lib.sm_create(C.byref(ctx), C.byref(p), 0)
+    try:
+        assert st == _capi.SM_EINVAL
+        assert msg in lib.sm_last_error(ctx)
+    finally:
+        lib.sm_destroy(ctx)

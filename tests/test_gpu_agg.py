@@ -1,0 +1,108 @@
+"""GPU parity of the alternative aggregators against the CPU restatement, bit for bit.
+
+"GF": guideFilter (stereoMatching.cpp:4492-4516) in its MY_GUIDE form, guideFilterCore_matlab
+(cpp:4975-5104) with the reference's BoxFilter / CumSum (cpp:5107-5202), r = 9, eps = 1e-4;
+its costs can be negative, so SGM runs its float-minimum variant.  "NL": NL() (cpp:4892-4917),
+the MST tree filter of NL/ (Kruskal tree built on the host, filter on the GPU).
+PARITY UNPINNED (the oracle restates the reference text; tests/test_oracle_agg.py cross-checks
+it against an independent numpy restatement).
+"""
+import numpy as np
+import pytest
+
+from mystereomatching_amd import SolveAll, StereoBatch, StereoMatching
+from mystereomatching_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("lbgr", "rbgr", "lgray", "rgray")
+AGG = {"GF": 2, "NL": 3}
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _agg_volume(pair, H, W, md, agg, cost="censusGrad"):
+    StereoMatching.costcalculation, StereoMatching.aggregation, StereoMatching.optimization = cost, agg, "sgm"
+    try:
+        sm = StereoMatching(pair["lbgr"], pair["rbgr"], pair["lgray"], pair["rgray"], None, None, None, None,
+                            StereoMatching.Parameters(md, H, W), device=0)
+        sm.costCalculate()
+        return sm.vm[0]
+    finally:
+        StereoMatching.aggregation = "CBCA"
+        StereoMatching.costcalculation = "censusGrad"
+
+
+@pytest.mark.parametrize("agg", ["GF", "NL"])
+@pytest.mark.parametrize("H,W,md,idx", [(24, 30, 7, 500), (40, 61, 63, 501), (33, 47, 69, 502), (21, 19, 255, 503)])
+def test_aggregated_volume_bits(oracle, agg, H, W, md, idx):
+    pair = S.make_pair(H, W, md + 1, idx)
+    cfg = oracle.config(H, W, md)
+    vm = oracle.cost_volume(pair, cfg)
+    want = oracle.guided_filter(vm, pair["lbgr"], cfg) if agg == "GF" else oracle.nl_aggregate(vm, pair["lbgr"], cfg)
+    got = _agg_volume(pair, H, W, md, agg)
+    np.testing.assert_array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("agg", ["GF", "NL"])
+@pytest.mark.parametrize("H,W,md,paths,cost", [(48, 64, 31, 4, "censusGrad"), (37, 70, 15, 8, "Census"),
+                                               (30, 44, 127, 4, "censusGrad")])
+def test_batch_maps_match_oracle(oracle, agg, H, W, md, paths, cost):
+    n = 3
+    batch = S.make_batch(n, H, W, md + 1, first_index=510)
+    sb = StereoBatch(md, H, W, n, device=0, aggregation=AGG[agg], sgm_paths=paths, cost_method=cost)
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        got = sb.run(0.3)
+    finally:
+        sb.close()
+    cfg = oracle.config(H, W, md, cost=cost, aggregation=AGG[agg], sgm_paths=paths)
+    for i in range(n):
+        want = oracle.run({k: batch[k][i] for k in KEYS}, cfg)["disp"]
+        np.testing.assert_array_equal(got[i], want)
+
+
+def test_gf_with_refine_both_views(oracle):
+    """Do_refine: guideFilter runs on both views (num = 2, cpp:4499) with each view's colours."""
+    H, W, md = 40, 56, 23
+    pair = S.make_pair(H, W, md + 1, 520)
+    sb = StereoBatch(md, H, W, 1, device=0, aggregation=2, do_refine=1)
+    try:
+        sb.upload(*(pair[k][None] for k in KEYS))
+        got = sb.run(0.3)[0]
+    finally:
+        sb.close()
+    want = oracle.run(pair, oracle.config(H, W, md, aggregation=2, do_refine=1))["disp"]
+    np.testing.assert_array_equal(got, want)
+
+
+def test_reference_ordered_api_nl(oracle):
+    H, W, md = 36, 50, 31
+    pair = S.make_pair(H, W, md + 1, 530)
+    StereoMatching.aggregation = "NL"
+    try:
+        sm = StereoMatching(pair["lbgr"], pair["rbgr"], pair["lgray"], pair["rgray"], None, None, None, None,
+                            StereoMatching.Parameters(md, H, W), device=0)
+        sm.costCalculate()
+        SolveAll([sm], 1, 0.3)
+        got = sm.dispOptimize()
+    finally:
+        StereoMatching.aggregation = "CBCA"
+    np.testing.assert_array_equal(got, oracle.run(pair, oracle.config(H, W, md, aggregation=3))["disp"])
+
+
+@pytest.mark.parametrize("agg", ["GF", "NL"])
+def test_teddy_size_maps(oracle, agg):
+    """BASELINE configs[1] shape (450x375, D = 64) with GF / NL in place of CBCA."""
+    H, W, md = 375, 450, 63
+    pair = S.make_pair(H, W, md + 1, 0)
+    sb = StereoBatch(md, H, W, 1, device=0, aggregation=AGG[agg])
+    try:
+        sb.upload(*(pair[k][None] for k in KEYS))
+        got = sb.run(0.3)[0]
+    finally:
+        sb.close()
+    want = oracle.run(pair, oracle.config(H, W, md, aggregation=AGG[agg]))["disp"]
+    np.testing.assert_array_equal(got, want)

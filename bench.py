@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--no-parity", action="store_true", help="skip the pair-0 fixture comparison (timing probes)")
+    ap.add_argument("--fuse-norm-scan", action="store_true",
+                    help="CBCA: fuse iteration k's normalising sweep with iteration k+1's scan (sm_params.fuse_norm_scan)")
     ap.add_argument("--e2e", action="store_true",
                     help="time the product multi-GPU path instead of resident batches: rank 0 holds the global "
                          "batch on the host; each step broadcasts the header, scatters the pairs (RCCL), runs "
@@ -141,7 +143,7 @@ def main():
     # this rank's shard of the global batch: pair indices [rank*B, rank*B + B)
     batch = S.make_batch(B, H, W, D, first_index=rank * B)
     sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt,
-                     aggregation=args.agg)
+                     aggregation=args.agg, fuse_norm_scan=int(args.fuse_norm_scan))
     if args.agg != "CBCA":
         desc = desc.replace("CBCA", args.agg, 1)
     if args.opt == "so":

@@ -102,6 +102,12 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #ifndef SM_CB_WIN_RING
 #define SM_CB_WIN_RING 1
 #endif
+// V sweeps take the pixel's own arm pair of position k by v_readlane from the tile's lane-vector
+// load instead of staging it in LDS (SM_CB_V_READLANE): their other-image words are register
+// gathers, so the sweep's tile then has a single LDS round trip (the S / area rings) instead of two.
+#ifndef SM_CB_V_READLANE
+#define SM_CB_V_READLANE 1
+#endif
 #ifndef SM_CB_PROBE_NOVG
 #define SM_CB_PROBE_NOVG 0   // timing probe only (wrong results): V sweeps skip the other image's arm gather
 #endif
@@ -224,7 +230,6 @@ struct CbLine {
     const char* A1v[NSETS];     // V: right-image plane, row 0 (uniform)
     int pstride, line, len, lag, ring;
     int c64;                  // first disparity of the chunk
-    uint32_t vmask;           // V sweeps: all ones if u - d >= 0 else 0 (constant along the line)
     uint32_t sh[NSETS];       // H sweeps: shifted right-arm window per set
     uint32_t* wown;           // LDS window: own arm words of the tile, T per set
     uint32_t* wspan;          // LDS window (H): the other image's span, 64 + T - 1 per set
@@ -340,15 +345,19 @@ struct CbLine {
             const uint32_t* row = stg + sbuf * NW + (s * T + k) * SPW;
             return pkmin(row[wv], row[KW + (RV ? wv + lane : wv + 63 - lane)]);
         }
+        if (!HORIZ && SM_CB_V_READLANE) {
+            const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
+            return pkmin(a0, t.a1[s][k]);
+        }
         if (SM_CB_LDS_WIN) {
             const uint32_t a0 = wown[s * T + k];   // broadcast read
             const uint32_t a1 = HORIZ ? (SM_CB_WIN_RING ? wspan[s * 2 * cbca_win_ring(T) + wrs + (RV ? k + lane : k + 63 - lane)]
                                                         : wspan[s * (64 + T - 1) + (RV ? k + lane : k + 63 - lane)])
-                                      : (t.a1[s][k] & vmask);
+                                      : t.a1[s][k];
             return pkmin(a0, a1);
         }
         const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
-        const uint32_t a1 = HORIZ ? sh[s] : (t.a1[s][k] & vmask);
+        const uint32_t a1 = HORIZ ? sh[s] : t.a1[s][k];
         return pkmin(a0, a1);
     }
     // stage the tile's arm words in LDS (one wave: its LDS accesses complete in order)
@@ -364,7 +373,7 @@ struct CbLine {
             __syncthreads();
             return;
         }
-        if (!SM_CB_LDS_WIN) return;
+        if (!SM_CB_LDS_WIN || (!HORIZ && SM_CB_V_READLANE)) return;
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             if (lane < T) wown[s * T + lane] = t.a0[s];
@@ -583,13 +592,14 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         L.sh[s] = 0u;
     }
     if (!HORIZ) {
-        // other image's column: u - d (left view) or u + d (right view), clamped; vmask zeroes
-        // the pairs outside the image
-        const uint32_t col = RV ? (uint32_t)min(L.line + dl, a.W - 1) * 4u : (uint32_t)(L.line - min(dl, L.line)) * 4u;
+        // other image's column: u - d (left view) or u + d (right view); lanes whose column lies
+        // outside the image get an out-of-range offset, so their gathers return the reference's
+        // zeroed intersection (cpp:2794-2845) without a mask per position
+        const bool out = RV ? L.line + dl >= a.W : L.line - dl < 0;
+        const uint32_t col = (uint32_t)(RV ? L.line + dl : L.line - dl) * 4u;
 #pragma unroll
-        for (int k = 0; k < (HORIZ ? 1 : T); k++) L.ao[k] = col + (uint32_t)(k * a.W * 4);
+        for (int k = 0; k < (HORIZ ? 1 : T); k++) L.ao[k] = out ? 0x80000000u : col + (uint32_t)(k * a.W * 4);
     }
-    L.vmask = (!HORIZ && (RV ? L.line + dl >= a.W : L.line - dl < 0)) ? 0u : 0xffffffffu;
     L.c64 = chunk * 64;
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;

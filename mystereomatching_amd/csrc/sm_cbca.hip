@@ -262,8 +262,13 @@ struct CbLine {
         return buf_rsrc(xline + (long)pos0 * (long)vsb);
     }
     __device__ __forceinline__ static __amdgpu_buffer_rsrc_t bounded_rsrc(const char* base, const char* end) {
+        // the clamp of end - base to [0, 2^31 - 1] on 32-bit halves: 64-bit signed compares of
+        // scalars would go through the VALU
         const long room = end - base;
-        return buf_rsrc(base, room <= 0 ? 0 : (room > 0x7fffffffL ? 0x7fffffff : (int)room));
+        const int hi = (int)(room >> 32);
+        const uint32_t lo = (uint32_t)room;
+        const int range = hi < 0 ? 0 : ((hi > 0 || lo > 0x7fffffffu) ? 0x7fffffff : (int)lo);
+        return buf_rsrc(base, range);
     }
     __device__ __forceinline__ void store_tile(const __amdgpu_buffer_rsrc_t& r, int k, float v) const {
         if (KW > 1 && !active) return;
@@ -464,15 +469,17 @@ struct CbLine {
             // division (a uniform branch that never runs on real costs)
             float dv[T], qv[T];
             uint32_t av[T];
-            uint64_t tiny = 0;
+            // dividends are >= +0 (prefix sums of costs >= 0; S - S = +0), so "0 < dv < 2^-110"
+            // is "bits(dv) - 1 < 0x087fffff" (unsigned); the tile's minimum of bits - 1 decides it
+            uint32_t tmin = 0xffffffffu;
 #pragma unroll
             for (int k = 0; k < T; k++) {
                 dv[k] = shv[k] - stv[k];
                 av[k] = (ahv[k] - atv[k]) & 0xffffu;
                 qv[k] = div_area(dv[k], av[k]);
-                tiny |= __ballot(div_area_needs_ieee(dv[k]));
+                tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
             }
-            if (tiny) {
+            if (__ballot(tmin < 0x087fffffu)) {
 #pragma unroll
                 for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)av[k];
             }

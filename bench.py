@@ -46,6 +46,25 @@ FIXTURE = {"fullres": "large_fullres_d256", "hd": "large_hd1080_d256", "kitti": 
            "teddy": "teddy_censusgrad_d64"}
 
 
+SGM_RV = (+1, -1, 0, 0, +1, +1, -1, -1)   # direction table, stereoMatching.cpp:6207-6208
+SGM_RU = (0, 0, +1, -1, -1, +1, +1, -1)
+
+
+def kernel_symbol(name, D, paths):
+    """The kernel a profile name's launches run (sm_capi.cpp names -> sm_*.hip symbols).  The
+    middle SGM paths share one symbol (k_sgm<K, 0, ..>) except the straight vertical ones with
+    D % 4 == 0 and D <= 128, which run k_sgm_rows (sm_sgm.hip rows_kv); the right view's SGM
+    launches (suffix _r) run the left view's kernels, its CBCA sweeps a separate instantiation."""
+    base = name[:-2] if name.endswith("_r") else name
+    if base.startswith("sgm_path"):
+        i = int(base[len("sgm_path"):])
+        if 0 < i < paths - 1:
+            rows = SGM_RV[i] != 0 and SGM_RU[i] == 0 and D % 4 == 0 and D <= 128
+            return "k_sgm_rows<mid>" if rows else "k_sgm<mid>"
+        return base
+    return base if base.startswith("sgm") else name
+
+
 def fixture_check(workload, refine, opt, disp0):
     """Compare rank 0's pair-0 map with the committed oracle map of that pair (no oracle run)."""
     name = FIXTURE.get(workload)
@@ -85,6 +104,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--no-parity", action="store_true", help="skip the pair-0 fixture comparison (timing probes)")
+    ap.add_argument("--sub-batch", type=int, default=0, help="sm_params.sub_batch: run the pairs in groups of k")
+    ap.add_argument("--streams", type=int, default=1, help="sm_params.num_streams: groups alternate over s streams")
     ap.add_argument("--fuse-norm-scan", action="store_true",
                     help="CBCA: fuse iteration k's normalising sweep with iteration k+1's scan (sm_params.fuse_norm_scan)")
     ap.add_argument("--e2e", action="store_true",
@@ -143,7 +164,8 @@ def main():
     # this rank's shard of the global batch: pair indices [rank*B, rank*B + B)
     batch = S.make_batch(B, H, W, D, first_index=rank * B)
     sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt,
-                     aggregation=args.agg, fuse_norm_scan=int(args.fuse_norm_scan))
+                     aggregation=args.agg, fuse_norm_scan=int(args.fuse_norm_scan), sub_batch=args.sub_batch,
+                     num_streams=args.streams)
     if args.agg != "CBCA":
         desc = desc.replace("CBCA", args.agg, 1)
     if args.opt == "so":
@@ -213,26 +235,32 @@ def main():
             kern_out[name] = {"avg_ms": round(avg, 4), "share": round(k["total_ms"] / tot, 4),
                               "GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                               "bytes_per_launch": k["bytes_per_launch"]}
-        # dominant kernel by total time, the right view's launches (suffix _r) counted with the
-        # left view's kernel of the same name
-        tot_by = {}
+        # Dominant kernel = the code object with the largest share of the step, as rocprofv3
+        # --stats ranks kernels: profile names whose launches run the same kernel symbol are one
+        # group (kernel_symbol); achieved = the group's algorithmic bytes / its HIP-event time.
+        groups = {}
         for n in kern_out:
-            tot_by[n[:-2] if n.endswith("_r") and n[:-2] in kern_out else n] = \
-                tot_by.get(n[:-2] if n.endswith("_r") and n[:-2] in kern_out else n, 0.0) + kernels[n]["total_ms"]
+            groups.setdefault(kernel_symbol(n, D, paths), []).append(n)
+        tot_by = {g: sum(kernels[n]["total_ms"] for n in ns) for g, ns in groups.items()}
         dom = max(tot_by, key=tot_by.get)
+        members = groups[dom]
+        launches = sum(kernels[n]["launches"] for n in members)
+        gbytes = sum(kernels[n]["bytes_per_launch"] * kernels[n]["launches"] for n in members)
+        ach = gbytes / (tot_by[dom] * 1e-3) / 1e9
         traffic = None
         tag = ("_refine" if args.refine else "") + ("_so" if args.opt == "so" else "") + \
             ("" if args.agg == "CBCA" else "_" + args.agg.lower())
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}{tag}_b{B}.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
-            except Exception:
+                pk = json.load(open(pmc)).get("kernels", {})
+                tr = [pk[n]["hbm_bytes_per_launch"] * kernels[n]["launches"] for n in members]
+                traffic = round(sum(tr) / launches, 1)
+            except (KeyError, ValueError, TypeError):
                 traffic = None
-        ach = kern_out[dom]["GB_s"]
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "bytes_per_launch": kern_out[dom]["bytes_per_launch"]}
+        roofline = {"bound": "hbm", "kernel": dom, "profile_names": members, "achieved": round(ach, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "bytes_per_launch": gbytes / launches}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

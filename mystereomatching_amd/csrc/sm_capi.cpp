@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <map>
 #include <new>
@@ -69,8 +70,9 @@ struct sm_ctx {
     // aggregation "NL": median image, edge weights, the tree (uploaded per call), filter values
     uint8_t* nl_med = nullptr;  // [cap][npix][3]
     uint8_t* nl_ew = nullptr;   // [cap][ne]
-    int* nl_ints = nullptr;     // chain_nodes, chain_start, chain_len, order_up, order_down, parent, child[4]: [cap][npix] each
-    uint8_t* nl_bytes = nullptr;// weight, nchild, heavy: [cap][npix] each
+    int* nl_ints = nullptr;     // chain_start, chain_len, order_up, order_down: [cap][npix] each
+    int* nl_rec = nullptr;      // path-node records (4 ints) [cap][npix], zero padding on both sides
+    double nl_table_h[256];     // the weight table (host copy)
     double* nl_table = nullptr; // [256]
     double* nl_val = nullptr;   // [cap][nvol]
     float* nl_wsum = nullptr;   // [cap][npix]
@@ -247,7 +249,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
-                    c->gf_s, c->gf_planes, c->gf_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_bytes,
+                    c->gf_s, c->gf_planes, c->gf_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
                     c->nl_table, c->nl_val, c->nl_wsum};
     for (void* q : ptrs)
         if (q) hipFree(q);
@@ -471,53 +473,57 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
         sm::launch_nl_edges(B.bgr, 2 * np * 3, c->nl_med + off * np * 3, c->nl_ew + off * ne, H, W, n, c->st);
     });
     if (s) return s;
+    // SM_NL_TRACE=1: host phase times on stderr (diagnostics)
+    static const bool trace = getenv("SM_NL_TRACE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!trace) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[nl] %-8s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
     std::vector<uint8_t> ew((size_t)n * ne);
     HIP_TRY(c, hipMemcpyAsync(ew.data(), c->nl_ew + off * ne, ew.size(), hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
+    phase("edges");
     std::vector<sm::NlTree> trees(n);
+    std::vector<int32_t> rec((size_t)n * np * 4);
+    std::vector<float> wsum((size_t)n * np);
     {
+        // one host thread per pair group: tree, its records and its weight sums (disjoint slices)
         std::vector<char> ok(n, 0);
         const int nth = std::max(1, std::min(n, (int)std::thread::hardware_concurrency()));
         std::vector<std::thread> th;
         for (int t = 0; t < nth; t++)
             th.emplace_back([&, t] {
-                for (int b = t; b < n; b += nth) ok[b] = sm::nl_build_tree(H, W, ew.data() + (size_t)b * ne, trees[b]);
+                for (int b = t; b < n; b += nth) {
+                    ok[b] = sm::nl_build_tree(H, W, ew.data() + (size_t)b * ne, trees[b]);
+                    if (!ok[b]) continue;
+                    sm::nl_pack_records(trees[b], W, b * (int)np, rec.data() + (size_t)b * np * 4);
+                    sm::nl_weight_sums(trees[b], c->nl_table_h, wsum.data() + (size_t)b * np);
+                }
             });
         for (auto& x : th) x.join();
         for (int b = 0; b < n; b++)
             if (!ok[b]) return fail(c, SM_EINVAL, "NL: spanning tree construction failed");
     }
-    // concatenate the pairs' trees (node ids b * npix + pixel) and order the paths by round
-    std::vector<int> cn, cs, cl, par((size_t)n * np), chi((size_t)n * np * 4), ord_up, ord_dn;
-    std::vector<uint8_t> wgt((size_t)n * np), nch((size_t)n * np);
-    std::vector<int8_t> hv((size_t)n * np);
-    std::vector<int> upl, dnl;
+    phase("trees");
+    // concatenate the pairs' paths (records of pair b start at b * npix) and order them by round
+    std::vector<int> cs, cl, ord_up, ord_dn, upl, dnl;
     int max_up = 0, max_dn = 0;
     for (int b = 0; b < n; b++) {
         const sm::NlTree& t = trees[b];
-        const int base = b * (int)np;
-        const int c0 = (int)cs.size();
+        const size_t r0 = (size_t)b * np;
         for (size_t k = 0; k < t.chain_start.size(); k++) {
-            cs.push_back(t.chain_start[k] + (int)cn.size());
+            cs.push_back(t.chain_start[k] + (int)r0);
             cl.push_back(t.chain_len[k]);
             upl.push_back(t.up_level[k]);
             dnl.push_back(t.down_level[k]);
             max_up = std::max(max_up, t.up_level[k]);
             max_dn = std::max(max_dn, t.down_level[k]);
         }
-        (void)c0;
-        for (int x : t.chain_nodes) cn.push_back(x + base);
-        for (size_t i = 0; i < np; i++) {
-            par[base + i] = t.parent[i] + base;
-            wgt[base + i] = t.weight[i];
-            nch[base + i] = t.nchild[i];
-            hv[base + i] = t.heavy[i];
-            for (int j = 0; j < 4; j++) {
-                const int q = t.child[i * 4 + j];
-                chi[(base + i) * 4 + j] = q < 0 ? -1 : q + base;
-            }
-        }
     }
+    phase("records");
     const int nchain = (int)cs.size();
     std::vector<int> up_off(max_up + 2, 0), dn_off(max_dn + 2, 0);
     for (int k = 0; k < nchain; k++) {
@@ -535,42 +541,36 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
             ord_dn[pd[dnl[k]]++] = k;
         }
     }
-    // device tables: ints [10][cap * npix]: cn, cs, cl, ord_up, ord_dn, parent, child (4)
+    // device tables: ints [4][cap * npix]: chain_start, chain_len, order_up, order_down; the
+    // records between their zero paddings; the weight sums
     const size_t slot = (size_t)c->cap * np;
     int* I = c->nl_ints;
-    uint8_t* U = c->nl_bytes;
-    HIP_TRY(c, hipMemcpy(I + 0 * slot, cn.data(), cn.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 1 * slot, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 2 * slot, cl.data(), cl.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 3 * slot, ord_up.data(), ord_up.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 4 * slot, ord_dn.data(), ord_dn.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 5 * slot, par.data(), par.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 6 * slot, chi.data(), chi.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(U + 0 * slot, wgt.data(), wgt.size(), hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(U + 1 * slot, nch.data(), nch.size(), hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(U + 2 * slot, hv.data(), hv.size(), hipMemcpyHostToDevice));
+    int* rec_d = c->nl_rec + sm::NL_REC_PAD * 4;
+    HIP_TRY(c, hipMemcpy(I, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 1 * slot, cl.data(), cl.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 2 * slot, ord_up.data(), ord_up.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(I + 3 * slot, ord_dn.data(), ord_dn.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(rec_d, rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->nl_wsum, wsum.data(), wsum.size() * 4, hipMemcpyHostToDevice));
+    phase("upload");
     sm::NlArgs a{};
-    a.chain_nodes = I;
-    a.chain_start = I + slot;
-    a.chain_len = I + 2 * slot;
-    a.order_up = I + 3 * slot;
-    a.order_down = I + 4 * slot;
-    a.parent = I + 5 * slot;
-    a.child = I + 6 * slot;
-    a.weight = U;
-    a.nchild = U + slot;
-    a.heavy = (const int8_t*)(U + 2 * slot);
+    a.chain_start = I;
+    a.chain_len = I + slot;
+    a.order_up = I + 2 * slot;
+    a.order_down = I + 3 * slot;
+    a.rec = (const int4*)rec_d;
     a.table = c->nl_table;
     a.val = c->nl_val;
     a.vm = B.vm0;
     a.wsum = c->nl_wsum;
-    // the ones pass (weight sums), then the cost volume; each pass: up rounds, then down rounds
+    a.W = W;
+    // the cost volume (the weight sums came from the host): up rounds, then down rounds; per
+    // voxel: cost in, up sum out; up sum in, final out, float out (+ the light children's sums,
+    // about one per node)
     const double bytes = (double)n * c->nvol * (4 + 8 + 8 + 8 + 8 + 4);
     return timed(c, "nl_filter", bytes, [&] {
-        for (int P : {1, D}) {
-            for (int r = 0; r <= max_up; r++) sm::launch_nl_round(a, true, up_off[r], up_off[r + 1], P, c->st);
-            for (int r = 0; r <= max_dn; r++) sm::launch_nl_round(a, false, dn_off[r], dn_off[r + 1], P, c->st);
-        }
+        for (int r = 0; r <= max_up; r++) sm::launch_nl_round(a, true, up_off[r], up_off[r + 1], D, c->st);
+        for (int r = 0; r <= max_dn; r++) sm::launch_nl_round(a, false, dn_off[r], dn_off[r + 1], D, c->st);
     });
 }
 
@@ -837,15 +837,16 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         const size_t ne = (size_t)p->rows * (p->cols - 1) + (size_t)(p->rows - 1) * p->cols;
         if ((s = dalloc(c, &c->nl_med, cap * c->npix * 3))) return s;
         if ((s = dalloc(c, &c->nl_ew, cap * ne))) return s;
-        if ((s = dalloc(c, &c->nl_ints, cap * c->npix * 10))) return s;
-        if ((s = dalloc(c, &c->nl_bytes, cap * c->npix * 3))) return s;
+        if ((s = dalloc(c, &c->nl_ints, cap * c->npix * 4))) return s;
+        if ((s = dalloc(c, &c->nl_rec, (cap * c->npix + 2 * sm::NL_REC_PAD) * 4))) return s;
+        HIP_TRY(c, hipMemset(c->nl_rec, 0, (cap * c->npix + 2 * sm::NL_REC_PAD) * 16));
         if ((s = dalloc(c, &c->nl_table, 256))) return s;
         if ((s = dalloc(c, &c->nl_val, cap * c->nvol))) return s;
         if ((s = dalloc(c, &c->nl_wsum, cap * c->npix))) return s;
-        double table[256];
+        double* table = c->nl_table_h;
         const double sg = p->nl_sigma < 0.01 ? 0.01 : p->nl_sigma;   // update_table (qx_tree_filter.cpp:23-24)
         for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));
-        HIP_TRY(c, hipMemcpy(c->nl_table, table, sizeof(table), hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemcpy(c->nl_table, table, 256 * sizeof(double), hipMemcpyHostToDevice));
     }
     build_luts(c);
     {

@@ -94,21 +94,20 @@ struct GfArgs {
 void launch_gf(const GfArgs& a, int n, hipStream_t st);
 
 struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids = pair * H W + pixel
-    const int* chain_nodes;     // heavy paths, each bottom -> top
-    const int* chain_start;
+    const int4* rec;            // path nodes, each path bottom -> top: {x, meta, child weights, parent}
+                                //   meta = nchild | (heavy + 1) << 3 | child directions << 6 (2 bits
+                                //   each: +1, -1, +W, -W) | own edge weight << 16
+    const int* chain_start;     // first record of each path
     const int* chain_len;
     const int* order_up;        // path indices sorted by up round
     const int* order_down;      // path indices sorted by down round
-    const int* parent;          // [nodes] (the root is its own parent)
-    const uint8_t* weight;      // [nodes] edge weight to the parent
-    const uint8_t* nchild;      // [nodes]
-    const int* child;           // [nodes][4]
-    const int8_t* heavy;        // [nodes] child index continuing the path, -1 at leaves
     const double* table;        // exp(-i / (255 sigma)), i = 0..255
-    double* val;                // [nodes][P] up sums, then final values (in place)
+    double* val;                // [nodes][D] up sums, then final values (in place)
     float* vm;                  // [nodes][D] costs in, normalised aggregated costs out
-    float* wsum;                // [nodes] the filtered ones (P = 1 pass)
+    const float* wsum;          // [nodes] the filtered ones (host, nl_weight_sums)
+    int W;
 };
+constexpr int NL_REC_PAD = 64;  // zero records after the last path (blocked reads past a path's end)
 void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8_t* ew, int H, int W, int n, hipStream_t st);
 void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_t st);
 

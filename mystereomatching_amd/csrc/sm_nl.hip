@@ -7,7 +7,8 @@
 //   filter     qx_tree_filter::filter (NL/qx_tree_filter.cpp:61-117) in double, w = exp(-c / 25.5):
 //                up(x)  = C(x) + sum_j up(child_j) * w(child_j)           children in list order
 //                fin(x) = w(x) * (fin(parent) - w(x) * up(x)) + up(x),    fin(root) = up(root)
-//   NL()       vm = (float)fin(C) / (float)fin(1)   (the ones volume, cpp:4899-4910)
+//   NL()       vm = (float)fin(C) / (float)fin(1)   (the ones volume, cpp:4899-4910; fin(1) depends
+//              only on the tree and is filtered on the host with the tree, sm_nl_tree.cpp)
 //
 // gfx950 mapping: one wave per (heavy path, 64-disparity chunk), lane = disparity, walking the path
 // node by node; the child on the same path arrives in a register, the other children (their paths
@@ -21,7 +22,19 @@
 #include "sm_device.h"
 #include "sm_kernels.h"
 
+#ifndef SM_NL_BLOCK
+#define SM_NL_BLOCK 4   // path nodes whose loads are issued together (tuning)
+#endif
+#ifndef SM_NL_PIPE
+#define SM_NL_PIPE 1    // issue the next block's loads before this block's arithmetic (tuning)
+#endif
+#ifndef SM_NL_WAVES
+#define SM_NL_WAVES 1   // waves (independent paths) per workgroup (tuning)
+#endif
+
 namespace sm {
+
+static_assert(3 * SM_NL_BLOCK <= NL_REC_PAD, "the passes read up to two blocks past a path's ends");
 
 namespace {
 
@@ -90,64 +103,200 @@ __global__ __launch_bounds__(256) void k_nl_edges(const uint8_t* __restrict__ me
     ew[t] = (uint8_t)w;
 }
 
-// up pass over the paths chains[lo, hi): bottom -> top
-__global__ __launch_bounds__(64) void k_nl_up(const NlArgs a, int lo, int P) {
-    const int nchunks = (P + 63) >> 6;
-    const int ci = a.order_up[lo + blockIdx.x / nchunks];
-    const int d = (blockIdx.x % nchunks) * 64 + threadIdx.x;
-    if (d >= P) return;
-    const int* nodes = a.chain_nodes + a.chain_start[ci];
-    const int len = a.chain_len[ci];
-    double carry = 0.0;
-    for (int t = 0; t < len; t++) {
-        const int x = nodes[t];
-        double v = P == 1 ? 1.0 : (double)a.vm[(size_t)x * P + d];
-        const int nc = a.nchild[x];
-        const int hv = a.heavy[x];
-        for (int j = 0; j < nc; j++) {
-            const int c = a.child[(size_t)x * 4 + j];
-            const double w = a.table[a.weight[c]];
-            const double cv = (j == hv) ? carry : a.val[(size_t)c * P + d];
-            const double m = cv * w;
+// Child j of node x from its direction code (NlArgs::rec): 0 = x + 1, 1 = x - 1, 2 = x + W, 3 = x - W
+// (tree edges join 4-neighbours, and node ids are pair * H W + pixel).
+__device__ __forceinline__ int nl_child(int x, int meta, int j, int W) {
+    const int code = (meta >> (6 + 2 * j)) & 3;
+    const int step = (code & 2) ? W : 1;
+    return (code & 1) ? x - step : x + step;
+}
+
+// Up pass over the paths order_up[lo, ...): bottom -> top.  A path is walked in blocks of K nodes:
+// every load of a block (the node's cost, its other children's finished sums, the edge weights)
+// is issued before the block's sequential arithmetic, and with SM_NL_PIPE the next block's loads
+// are issued before this block's arithmetic, so a long path pays a memory latency per K nodes or
+// less instead of a chain of dependent loads per node.  The branches around the loads are uniform
+// (scalar); the records themselves are read past the path's end (the next path or zero padding,
+// NL_REC_PAD) so that a block's records arrive in one go.
+template <int K>
+struct NlUpBlock {
+    int4 r[K];
+    float cost[K];
+    double wh[K], lm[K][4];
+};
+
+// issue the block's loads (uniform branches; nothing here waits for them)
+template <int K>
+__device__ __forceinline__ void nl_up_load(NlUpBlock<K>& B, const NlArgs& a, const int4* __restrict__ R, int b, int len,
+                                           int P, int d) {
+#pragma unroll
+    for (int k = 0; k < K; k++) B.r[k] = R[b + k];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int4 r = B.r[k];
+        const int nc = r.y & 7, hv = ((r.y >> 3) & 7) - 1;
+        B.cost[k] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; j++) B.lm[k][j] = 0.0;
+        if (b + k >= len) continue;                     // no loads past the path
+        B.cost[k] = a.vm[(size_t)r.x * P + d];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (j < nc && j != hv) B.lm[k][j] = a.val[(size_t)nl_child(r.x, r.y, j, a.W) * P + d];
+    }
+}
+
+// weights (scalar loads of the table) and the other children's products, once the loads are in
+template <int K>
+__device__ __forceinline__ void nl_up_weigh(NlUpBlock<K>& B, const double* __restrict__ table) {
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int4 r = B.r[k];
+        const int hv = ((r.y >> 3) & 7) - 1;
+        B.wh[k] = hv >= 0 ? table[(r.z >> (8 * hv)) & 255] : 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) B.lm[k][j] = B.lm[k][j] * table[(r.z >> (8 * j)) & 255];
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void nl_up_compute(const NlUpBlock<K>& B, const NlArgs& a, int b, int len, int P, int d,
+                                              double& carry) {
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        if (b + k >= len) break;
+        const int4 r = B.r[k];
+        const int nc = r.y & 7, hv = ((r.y >> 3) & 7) - 1;
+        double v = (double)B.cost[k];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (j >= nc) break;
+            const double m = (j == hv) ? carry * B.wh[k] : B.lm[k][j];
             v = v + m;
         }
-        a.val[(size_t)x * P + d] = v;
+        a.val[(size_t)r.x * P + d] = v;
         carry = v;
     }
 }
 
-// down pass over the paths chains[lo, hi): top -> bottom; writes the final doubles in place and
-// the normalised float volume (P = D) or the float weight sums (P = 1)
-__global__ __launch_bounds__(64) void k_nl_down(const NlArgs a, int lo, int P) {
+// rec and table arrive as restrict kernel arguments so that their uniform loads become scalar
+// loads (the struct members carry no aliasing guarantee against the stores to val).
+template <int K>
+__global__ __launch_bounds__(64 * SM_NL_WAVES) void k_nl_up(const NlArgs a, const int4* __restrict__ rec,
+                                                            const double* __restrict__ table, int lo, int nunits, int P) {
     const int nchunks = (P + 63) >> 6;
-    const int ci = a.order_down[lo + blockIdx.x / nchunks];
-    const int d = (blockIdx.x % nchunks) * 64 + threadIdx.x;
+    const int u = blockIdx.x * SM_NL_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (path, chunk)
+    if (u >= nunits) return;
+    const int ci = a.order_up[lo + u / nchunks];
+    const int d = (u % nchunks) * 64 + (threadIdx.x & 63);
     if (d >= P) return;
-    const int* nodes = a.chain_nodes + a.chain_start[ci];
+    const int4* __restrict__ R = rec + a.chain_start[ci];
     const int len = a.chain_len[ci];
     double carry = 0.0;
-    for (int t = len - 1; t >= 0; t--) {
-        const int x = nodes[t];
-        const double up = a.val[(size_t)x * P + d];
-        const int p = a.parent[x];
-        double fin;
-        if (p == x) {
-            fin = up;                                   // the root
-        } else {
-            const double w = a.table[a.weight[x]];
-            const double fp = (t == len - 1) ? a.val[(size_t)p * P + d] : carry;
-            const double m = w * up;
-            const double q = fp - m;
-            const double r = w * q;
-            fin = r + up;
-        }
-        a.val[(size_t)x * P + d] = fin;
-        carry = fin;
-        if (P == 1)
-            a.wsum[x] = (float)fin;
-        else
-            a.vm[(size_t)x * P + d] = (float)fin / a.wsum[x];
+#if SM_NL_PIPE
+    NlUpBlock<K> X, Y;
+    nl_up_load(X, a, R, 0, len, P, d);
+    for (int b = 0; b < len; b += 2 * K) {
+        nl_up_load(Y, a, R, b + K, len, P, d);
+        nl_up_weigh(X, table);
+        nl_up_compute(X, a, b, len, P, d, carry);
+        if (b + K >= len) break;
+        nl_up_load(X, a, R, b + 2 * K, len, P, d);
+        nl_up_weigh(Y, table);
+        nl_up_compute(Y, a, b + K, len, P, d, carry);
     }
+#else
+    for (int b = 0; b < len; b += K) {
+        NlUpBlock<K> X;
+        nl_up_load(X, a, R, b, len, P, d);
+        nl_up_weigh(X, table);
+        nl_up_compute(X, a, b, len, P, d, carry);
+    }
+#endif
+}
+
+// Down pass over the paths order_down[lo, ...): top -> bottom, blocked like the up pass; writes
+// the final doubles in place and the normalised float volume.  Records before a path's first
+// node are the previous path's or zero padding.
+template <int K>
+struct NlDownBlock {
+    int4 r[K];
+    double up[K];
+    float ws[K];
+};
+
+template <int K>
+__device__ __forceinline__ void nl_down_load(NlDownBlock<K>& B, const NlArgs& a, const int4* __restrict__ R, int b, int P,
+                                             int d) {
+#pragma unroll
+    for (int k = 0; k < K; k++) B.r[k] = R[b - k];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int4 r = B.r[k];
+        B.up[k] = 0.0;
+        B.ws[k] = 1.0f;
+        if (b - k < 0) continue;                        // no loads before the path
+        B.up[k] = a.val[(size_t)r.x * P + d];
+        B.ws[k] = a.wsum[r.x];
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void nl_down_compute(const NlDownBlock<K>& B, const NlArgs& a, const double* __restrict__ table,
+                                                int b, int P, int d, double& carry) {
+    double w[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) w[k] = table[(B.r[k].y >> 16) & 255];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        if (b - k < 0) break;
+        const int4 r = B.r[k];
+        double fin;
+        if (r.w == r.x) {
+            fin = B.up[k];                              // the root
+        } else {
+            const double m = w[k] * B.up[k];
+            const double q = carry - m;
+            const double s = w[k] * q;
+            fin = s + B.up[k];
+        }
+        a.val[(size_t)r.x * P + d] = fin;
+        carry = fin;
+        a.vm[(size_t)r.x * P + d] = (float)fin / B.ws[k];
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(64 * SM_NL_WAVES) void k_nl_down(const NlArgs a, const int4* __restrict__ rec,
+                                                              const double* __restrict__ table, int lo, int nunits, int P) {
+    const int nchunks = (P + 63) >> 6;
+    const int u = blockIdx.x * SM_NL_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (path, chunk)
+    if (u >= nunits) return;
+    const int ci = a.order_down[lo + u / nchunks];
+    const int d = (u % nchunks) * 64 + (threadIdx.x & 63);
+    if (d >= P) return;
+    const int4* __restrict__ R = rec + a.chain_start[ci];
+    const int len = a.chain_len[ci];
+    const int4 top = R[len - 1];
+    // the top's parent is on a path finished in an earlier round (or the top is the root)
+    double carry = top.w == top.x ? 0.0 : a.val[(size_t)top.w * P + d];
+#if SM_NL_PIPE
+    NlDownBlock<K> X, Y;
+    nl_down_load(X, a, R, len - 1, P, d);
+    for (int b = len - 1; b >= 0; b -= 2 * K) {
+        nl_down_load(Y, a, R, b - K, P, d);
+        nl_down_compute(X, a, table, b, P, d, carry);
+        if (b - K < 0) break;
+        nl_down_load(X, a, R, b - 2 * K, P, d);
+        nl_down_compute(Y, a, table, b - K, P, d, carry);
+    }
+#else
+    for (int b = len - 1; b >= 0; b -= K) {
+        NlDownBlock<K> X;
+        nl_down_load(X, a, R, b, P, d);
+        nl_down_compute(X, a, table, b, P, d, carry);
+    }
+#endif
 }
 
 }  // namespace
@@ -161,12 +310,13 @@ void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8
 
 void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_t st) {
     if (hi <= lo) return;
-    const int nchunks = (P + 63) / 64;
-    const dim3 grid((unsigned)((hi - lo) * nchunks));
+    const int nchunks = (P + 63) / 64, nunits = (hi - lo) * nchunks;
+    const dim3 grid((unsigned)((nunits + SM_NL_WAVES - 1) / SM_NL_WAVES)), block(64 * SM_NL_WAVES);
+    constexpr int K = SM_NL_BLOCK;
     if (up)
-        hipLaunchKernelGGL(k_nl_up, grid, dim3(64), 0, st, a, lo, P);
+        hipLaunchKernelGGL((k_nl_up<K>), grid, block, 0, st, a, a.rec, a.table, lo, nunits, P);
     else
-        hipLaunchKernelGGL(k_nl_down, grid, dim3(64), 0, st, a, lo, P);
+        hipLaunchKernelGGL((k_nl_down<K>), grid, block, 0, st, a, a.rec, a.table, lo, nunits, P);
 }
 
 }  // namespace sm

@@ -158,7 +158,52 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         t.up_level[c] = lv;
     }
     for (int c = 1; c < nch; c++) t.down_level[c] = t.down_level[chain_of[t.parent[tops[c]]]] + 1;
+    t.order = std::move(bfs);
     return true;
+}
+
+void nl_pack_records(const NlTree& t, int W, int base, int32_t* rec) {
+    for (int k = 0; k < t.n; k++) {
+        const int x = t.chain_nodes[k];
+        const int nc = t.nchild[x];
+        int meta = nc | (t.heavy[x] + 1) << 3 | t.weight[x] << 16;
+        uint32_t wp = 0;
+        for (int j = 0; j < nc; j++) {
+            const int q = t.child[(size_t)x * 4 + j], dq = q - x;
+            const int code = dq == 1 ? 0 : dq == -1 ? 1 : dq == W ? 2 : 3;   // +1, -1, +W, -W
+            meta |= code << (6 + 2 * j);
+            wp |= (uint32_t)t.weight[q] << (8 * j);
+        }
+        int32_t* r = rec + (size_t)k * 4;
+        r[0] = x + base;
+        r[1] = meta;
+        r[2] = (int32_t)wp;
+        r[3] = t.parent[x] + base;
+    }
+}
+
+void nl_weight_sums(const NlTree& t, const double* table, float* wsum) {
+    const int n = t.n;
+    std::vector<double> v(n);
+    for (int i = n - 1; i >= 0; i--) {     // up: children before parents
+        const int x = t.order[i];
+        double s = 1.0;
+        for (int j = 0; j < t.nchild[x]; j++) {
+            const int c = t.child[(size_t)x * 4 + j];
+            const double m = v[c] * table[t.weight[c]];
+            s = s + m;
+        }
+        v[x] = s;
+    }
+    for (int i = 1; i < n; i++) {          // down: parents before children (the root keeps its sum)
+        const int x = t.order[i];
+        const double w = table[t.weight[x]];
+        const double m = w * v[x];
+        const double q = v[t.parent[x]] - m;
+        const double r = w * q;
+        v[x] = r + v[x];
+    }
+    for (int x = 0; x < n; x++) wsum[x] = (float)v[x];
 }
 
 }  // namespace sm

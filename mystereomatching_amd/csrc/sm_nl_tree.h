@@ -16,10 +16,19 @@ struct NlTree {
     std::vector<int> chain_nodes;   // paths concatenated, each bottom -> top
     std::vector<int> chain_start, chain_len;
     std::vector<int> up_level, down_level;   // rounds of the filter's two passes
+    std::vector<int> order;         // breadth-first order from the root
 };
 
 // ew: the pair's edge weights, H (W - 1) horizontal edges row by row, then (H - 1) W vertical
 // edges column by column (qx_mst_compute_edges_4neighbor).
 bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t);
+
+// The tree's nodes as the filter kernels' records (NlArgs::rec), in path order: rec[4 k ..] =
+// {node + base, meta, child weights, parent + base} for the k-th entry of t.chain_nodes.
+void nl_pack_records(const NlTree& t, int W, int base, int32_t* rec);
+
+// The filtered ones (the NL() weight sums, cpp:4899-4910) as floats: the tree filter of a constant
+// 1 in double, with the GPU kernels' (and the reference's) arithmetic and order.  O(n) per pair.
+void nl_weight_sums(const NlTree& t, const double* table, float* wsum);
 
 }  // namespace sm

@@ -73,6 +73,9 @@ struct sm_ctx {
     int* nl_ints = nullptr;     // chain_start, chain_len, order_up, order_down: [cap][npix] each
     int* nl_rec = nullptr;      // path-node records (4 ints) [cap][npix], zero padding on both sides
     double nl_table_h[256];     // the weight table (host copy)
+    void* nl_host = nullptr;    // pinned staging: edge weights, records, path tables, weight sums
+    std::vector<sm::NlTree> nl_trees;   // per pair, kept so that rebuilding reuses their memory
+    size_t nl_host_bytes = 0;
     double* nl_table = nullptr; // [256]
     double* nl_val = nullptr;   // [cap][nvol]
     float* nl_wsum = nullptr;   // [cap][npix]
@@ -253,6 +256,8 @@ void free_all(sm_ctx* c) {
                     c->nl_table, c->nl_val, c->nl_wsum};
     for (void* q : ptrs)
         if (q) hipFree(q);
+    if (c->nl_host) hipHostFree(c->nl_host);
+    c->nl_host = nullptr;
     for (auto& r : c->recs) {
         if (r.start) hipEventDestroy(r.start);
         if (r.stop) hipEventDestroy(r.stop);
@@ -473,22 +478,30 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
         sm::launch_nl_edges(B.bgr, 2 * np * 3, c->nl_med + off * np * 3, c->nl_ew + off * ne, H, W, n, c->st);
     });
     if (s) return s;
-    // SM_NL_TRACE=1: host phase times on stderr (diagnostics)
+    // SM_NL_TRACE=1: host phase times on stderr (diagnostics); "outside" = since the last call's end
     static const bool trace = getenv("SM_NL_TRACE") != nullptr;
-    auto t_last = std::chrono::steady_clock::now();
+    static auto t_prev_end = std::chrono::steady_clock::now();
+    auto t_last = t_prev_end;
     auto phase = [&](const char* what) {
         if (!trace) return;
         const auto now = std::chrono::steady_clock::now();
         fprintf(stderr, "[nl] %-8s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
         t_last = now;
     };
-    std::vector<uint8_t> ew((size_t)n * ne);
-    HIP_TRY(c, hipMemcpyAsync(ew.data(), c->nl_ew + off * ne, ew.size(), hipMemcpyDeviceToHost, c->st));
+    phase("outside");
+    // pinned staging (sm_alloc): [records n np x 4][chain_start, chain_len, order_up, order_down:
+    // cap np each][weight sums n np][edge weights n ne]; the uploads are asynchronous on the stream,
+    // and every previous use of the staging has completed by the synchronisation below
+    int32_t* rec = (int32_t*)c->nl_host;
+    const size_t slot = (size_t)c->cap * np;
+    int32_t* tabs = rec + slot * 4;
+    float* wsum = (float*)(tabs + slot * 4);
+    uint8_t* ew = (uint8_t*)(wsum + slot);
+    HIP_TRY(c, hipMemcpyAsync(ew, c->nl_ew + off * ne, (size_t)n * ne, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     phase("edges");
-    std::vector<sm::NlTree> trees(n);
-    std::vector<int32_t> rec((size_t)n * np * 4);
-    std::vector<float> wsum((size_t)n * np);
+    if ((int)c->nl_trees.size() < n) c->nl_trees.resize(n);
+    std::vector<sm::NlTree>& trees = c->nl_trees;
     {
         // one host thread per pair group: tree, its records and its weight sums (disjoint slices)
         std::vector<char> ok(n, 0);
@@ -497,10 +510,10 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
         for (int t = 0; t < nth; t++)
             th.emplace_back([&, t] {
                 for (int b = t; b < n; b += nth) {
-                    ok[b] = sm::nl_build_tree(H, W, ew.data() + (size_t)b * ne, trees[b]);
+                    ok[b] = sm::nl_build_tree(H, W, ew + (size_t)b * ne, trees[b]);
                     if (!ok[b]) continue;
-                    sm::nl_pack_records(trees[b], W, b * (int)np, rec.data() + (size_t)b * np * 4);
-                    sm::nl_weight_sums(trees[b], c->nl_table_h, wsum.data() + (size_t)b * np);
+                    sm::nl_pack_records(trees[b], W, b * (int)np, rec + (size_t)b * np * 4);
+                    sm::nl_weight_sums(trees[b], c->nl_table_h, wsum + (size_t)b * np);
                 }
             });
         for (auto& x : th) x.join();
@@ -543,15 +556,15 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     }
     // device tables: ints [4][cap * npix]: chain_start, chain_len, order_up, order_down; the
     // records between their zero paddings; the weight sums
-    const size_t slot = (size_t)c->cap * np;
     int* I = c->nl_ints;
     int* rec_d = c->nl_rec + sm::NL_REC_PAD * 4;
-    HIP_TRY(c, hipMemcpy(I, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 1 * slot, cl.data(), cl.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 2 * slot, ord_up.data(), ord_up.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(I + 3 * slot, ord_dn.data(), ord_dn.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(rec_d, rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(c->nl_wsum, wsum.data(), wsum.size() * 4, hipMemcpyHostToDevice));
+    memcpy(tabs, cs.data(), cs.size() * 4);
+    memcpy(tabs + slot, cl.data(), cl.size() * 4);
+    memcpy(tabs + 2 * slot, ord_up.data(), ord_up.size() * 4);
+    memcpy(tabs + 3 * slot, ord_dn.data(), ord_dn.size() * 4);
+    HIP_TRY(c, hipMemcpyAsync(I, tabs, slot * 4 * 4, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipMemcpyAsync(rec_d, rec, (size_t)n * np * 16, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->nl_wsum, wsum, (size_t)n * np * 4, hipMemcpyHostToDevice, c->st));
     phase("upload");
     sm::NlArgs a{};
     a.chain_start = I;
@@ -568,10 +581,13 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     // voxel: cost in, up sum out; up sum in, final out, float out (+ the light children's sums,
     // about one per node)
     const double bytes = (double)n * c->nvol * (4 + 8 + 8 + 8 + 8 + 4);
-    return timed(c, "nl_filter", bytes, [&] {
+    s = timed(c, "nl_filter", bytes, [&] {
         for (int r = 0; r <= max_up; r++) sm::launch_nl_round(a, true, up_off[r], up_off[r + 1], D, c->st);
         for (int r = 0; r <= max_dn; r++) sm::launch_nl_round(a, false, dn_off[r], dn_off[r + 1], D, c->st);
     });
+    phase("launch");
+    t_prev_end = t_last;
+    return s;
 }
 
 // aggregation other than CBCA: GF on every view (num = Do_refine ? 2 : 1, cpp:4499), NL on vm[0]
@@ -843,6 +859,11 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->nl_table, 256))) return s;
         if ((s = dalloc(c, &c->nl_val, cap * c->nvol))) return s;
         if ((s = dalloc(c, &c->nl_wsum, cap * c->npix))) return s;
+        c->nl_host_bytes = cap * c->npix * (16 + 16 + 4) + cap * ne;
+        if (hipHostMalloc(&c->nl_host, c->nl_host_bytes, hipHostMallocDefault) != hipSuccess) {
+            c->nl_host = nullptr;
+            return fail(c, SM_ENOMEM, "pinned NL staging");
+        }
         double* table = c->nl_table_h;
         const double sg = p->nl_sigma < 0.01 ? 0.01 : p->nl_sigma;   // update_table (qx_tree_filter.cpp:23-24)
         for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));

@@ -37,7 +37,8 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
     const int neh = H * (W - 1), ne = neh + (H - 1) * W;
     t.n = n;
     // stable counting sort of the edges by weight
-    std::vector<int> order_e((size_t)std::max(ne, 1));
+    std::vector<int>& order_e = t.s_order_e;
+    order_e.resize((size_t)std::max(ne, 1));
     {
         int start[257];
         memset(start, 0, sizeof(start));
@@ -58,8 +59,13 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
     };
     // Kruskal: union-find with path halving and union by size (the accepted set is independent
     // of how the components are merged)
-    std::vector<int> uf(n), sz(n, 1), nconn(n, 0), conn((size_t)n * 4);
-    std::vector<uint8_t> connw((size_t)n * 4);
+    std::vector<int>&uf = t.s_uf, &sz = t.s_sz, &nconn = t.s_nconn, &conn = t.s_conn;
+    std::vector<uint8_t>& connw = t.s_connw;
+    uf.resize(n);
+    sz.assign(n, 1);
+    nconn.assign(n, 0);
+    conn.resize((size_t)n * 4);
+    connw.resize((size_t)n * 4);
     for (int i = 0; i < n; i++) uf[i] = i;
     auto find = [&](int x) {
         while (uf[x] != x) {
@@ -90,7 +96,8 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
     t.weight.assign(n, 0);
     t.nchild.assign(n, 0);
     t.child.assign((size_t)n * 4, -1);
-    std::vector<int> bfs(n);
+    std::vector<int>& bfs = t.order;
+    bfs.resize(n);
     t.parent[0] = 0;
     bfs[0] = 0;
     int head = 0, len = 1;
@@ -107,7 +114,8 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
     }
     if (len != n) return false;
     // subtree sizes, heavy children
-    std::vector<int> size(n, 1);
+    std::vector<int>& size = t.s_size;
+    size.assign(n, 1);
     for (int i = n - 1; i > 0; i--) size[t.parent[bfs[i]]] += size[bfs[i]];
     t.heavy.assign(n, -1);
     for (int x = 0; x < n; x++) {
@@ -120,19 +128,21 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         t.heavy[x] = (int8_t)best;
     }
     // heavy paths in BFS order of their tops; nodes stored bottom -> top
-    std::vector<int> chain_of(n, -1);
+    std::vector<int>& chain_of = t.s_chain_of;
+    chain_of.assign(n, -1);
     t.chain_start.clear();
     t.chain_len.clear();
     t.chain_nodes.clear();
     t.chain_nodes.reserve(n);
-    std::vector<int> tops;
+    std::vector<int>& tops = t.s_tops;
+    tops.clear();
     for (int i = 0; i < n; i++) {
         const int x = bfs[i];
         if (x != 0 && t.heavy[t.parent[x]] >= 0 && t.child[(size_t)t.parent[x] * 4 + t.heavy[t.parent[x]]] == x) continue;
         tops.push_back(x);
     }
     const int nch = (int)tops.size();
-    std::vector<int> path;
+    std::vector<int>& path = t.s_path;
     for (int c = 0; c < nch; c++) {
         path.clear();
         for (int x = tops[c];; x = t.child[(size_t)x * 4 + t.heavy[x]]) {
@@ -158,7 +168,6 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         t.up_level[c] = lv;
     }
     for (int c = 1; c < nch; c++) t.down_level[c] = t.down_level[chain_of[t.parent[tops[c]]]] + 1;
-    t.order = std::move(bfs);
     return true;
 }
 
@@ -182,9 +191,10 @@ void nl_pack_records(const NlTree& t, int W, int base, int32_t* rec) {
     }
 }
 
-void nl_weight_sums(const NlTree& t, const double* table, float* wsum) {
+void nl_weight_sums(NlTree& t, const double* table, float* wsum) {
     const int n = t.n;
-    std::vector<double> v(n);
+    std::vector<double>& v = t.s_v;
+    v.resize(n);
     for (int i = n - 1; i >= 0; i--) {     // up: children before parents
         const int x = t.order[i];
         double s = 1.0;

@@ -17,6 +17,10 @@ struct NlTree {
     std::vector<int> chain_start, chain_len;
     std::vector<int> up_level, down_level;   // rounds of the filter's two passes
     std::vector<int> order;         // breadth-first order from the root
+    // scratch kept with the tree so that repeated builds reuse their memory (no page faults)
+    std::vector<int> s_order_e, s_uf, s_sz, s_nconn, s_conn, s_size, s_chain_of, s_tops, s_path;
+    std::vector<uint8_t> s_connw;
+    std::vector<double> s_v;
 };
 
 // ew: the pair's edge weights, H (W - 1) horizontal edges row by row, then (H - 1) W vertical
@@ -29,6 +33,6 @@ void nl_pack_records(const NlTree& t, int W, int base, int32_t* rec);
 
 // The filtered ones (the NL() weight sums, cpp:4899-4910) as floats: the tree filter of a constant
 // 1 in double, with the GPU kernels' (and the reference's) arithmetic and order.  O(n) per pair.
-void nl_weight_sums(const NlTree& t, const double* table, float* wsum);
+void nl_weight_sums(NlTree& t, const double* table, float* wsum);
 
 }  // namespace sm

@@ -22,4 +22,6 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --time
  && timeout -k 10 300 python bench.py --workload teddy --opt so --no-cpu-baseline > $O/bench_so.json 2>> $O/bench.err \
  && timeout -k 10 300 python bench.py --workload kitti --no-cpu-baseline > $O/bench_kitti.json 2>> $O/bench.err \
  && timeout -k 10 300 python bench.py --workload hd --no-cpu-baseline > $O/bench_hd.json 2>> $O/bench.err \
+ && timeout -k 10 300 python bench.py --workload teddy --agg GF --no-cpu-baseline > $O/bench_gf.json 2>> $O/bench.err \
+ && timeout -k 10 300 python bench.py --workload teddy --agg NL --no-cpu-baseline > $O/bench_nl.json 2>> $O/bench.err \
  && echo "round_gpu $TAG done"

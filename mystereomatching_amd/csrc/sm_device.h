@@ -24,6 +24,9 @@
      0x3feee89f995ad3adULL, 0x3feeff76f2fb5e47ULL, 0x3fef199bdd85529cULL, 0x3fef3720dcef9069ULL, \
      0x3fef5818dcfba487ULL, 0x3fef7c97337b9b5fULL, 0x3fefa4afa2a490daULL, 0x3fefd0765b6e4540ULL}
 
+#ifndef SM_EXPF_VEC
+#define SM_EXPF_VEC 1   // assemble 2^(k/32) from two 32-bit words (4 VALU fewer per call than 64-bit ops)
+#endif
 #ifndef SM_EXPF_FMA_SHIFT
 #define SM_EXPF_FMA_SHIFT 1
 #endif
@@ -53,11 +56,17 @@ __host__ __device__ inline float expf_glibc_core(float x, const Tab& tab) {
     uint64_t ki = __builtin_bit_cast(uint64_t, kd);
     kd -= SHIFT;
     double r = __builtin_fma(InvLn2N, xd, -kd);
-    uint64_t t = tab[ki % 32];
+    const uint64_t t = tab[ki % 32];
     // t += ki << 47: the shifted term's low word is 0, so only the high word changes (one
-    // 32-bit add instead of a 64-bit shift and add)
-    t = (t & 0xffffffffull) | ((uint64_t)((uint32_t)(t >> 32) + ((uint32_t)ki << 15)) << 32);
-    double s = __builtin_bit_cast(double, t);
+    // 32-bit add instead of a 64-bit shift and add); the words are assembled as a 2-vector so
+    // that no 64-bit shift / or is emitted for the pair
+#if SM_EXPF_VEC
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 tw = {(uint32_t)t, (uint32_t)(t >> 32) + ((uint32_t)ki << 15)};
+    double s = __builtin_bit_cast(double, tw);
+#else
+    double s = __builtin_bit_cast(double, (t & 0xffffffffull) | ((uint64_t)((uint32_t)(t >> 32) + ((uint32_t)ki << 15)) << 32));
+#endif
     double zz = __builtin_fma(C0, r, C1);
     double r2 = r * r;
     double y = __builtin_fma(C2, r, 1.0);

@@ -147,6 +147,9 @@ __host__ __device__ inline int prep_strip_words(int Lo) {
     return PREP_TY * (PREP_TX + 2 * Lo) + (PREP_TY + 2 * Lo) * PREP_TX;
 }
 
+#ifndef SM_PREP_WALK
+#define SM_PREP_WALK 1    // arm-walk steps whose LDS reads are issued together (tuning)
+#endif
 #ifndef SM_PREP_PROBE
 #define SM_PREP_PROBE 0   // timing probes: 1 = no arms, 2 = no census, 3 = neither (results wrong)
 #endif
@@ -200,8 +203,12 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
     if (STRIPS && a.do_arms) {
         const uint32_t* PH = a.pxh + img * npix;
         const uint32_t* PV = a.pxv + img * npix;
+        // hs rows are hsw = 64 + 2 Lo words long (runtime): row index by a float reciprocal
+        // instead of an integer division (exact for i < 2^22: the +0.5 keeps the product's
+        // rounding from crossing an integer)
+        const float rinv = 1.0f / (float)hsw;
         fill(hs, PREP_TY * hsw, [&](int i) -> uint32_t {
-            const int r = i / hsw, vv = v0 + r, uu = u0 - Lo + (i - r * hsw);
+            const int r = (int)(((float)i + 0.5f) * rinv), vv = v0 + r, uu = u0 - Lo + (i - r * hsw);
             return (vv < H && (unsigned)uu < (unsigned)W) ? PH[(size_t)vv * W + uu] : 0u;
         });
         fill(vs, (PREP_TY + 2 * Lo) * PREP_TX, [&](int i) -> uint32_t {
@@ -329,11 +336,30 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
                     auto pass = [&](uint32_t p, uint32_t ca, uint32_t cb) {
                         return ((((ca - p) & ~(cb - p)) & ARM_B9) | (p & fb)) == want;
                     };
+#if SM_PREP_WALK > 1
+                    // chunks of SM_PREP_WALK steps: a chunk's LDS reads are issued together, then
+                    // its first failing step (or Lo + 1) ends the walk
+                    for (;;) {
+                        uint32_t pw[SM_PREP_WALK];
+#pragma unroll
+                        for (int j = 0; j < SM_PREP_WALK; j++) pw[j] = sp[min(arm + j, Lo) * sst];
+                        int ff = SM_PREP_WALK;
+#pragma unroll
+                        for (int j = SM_PREP_WALK - 1; j >= 0; j--) {
+                            const int st = arm + j;
+                            const bool in1 = st <= Lin;
+                            if (st > Lo || !pass(pw[j], in1 ? ca1 : ca2, in1 ? cb1 : cb2)) ff = j;
+                        }
+                        arm += ff;
+                        if (ff < SM_PREP_WALK) break;
+                    }
+#else
                     for (; arm <= Lin; arm++)
                         if (!pass(sp[arm * sst], ca1, cb1)) break;
                     if (arm > Lin)
                         for (; arm <= Lo; arm++)
                             if (!pass(sp[arm * sst], ca2, cb2)) break;
+#endif
                 } else {
                     const int off = dv * W + du;
                     uint32_t prev = center;
@@ -436,7 +462,7 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 #define SM_COST_SPLIT 1
 #endif
 #ifndef SM_COST_UNROLL
-#define SM_COST_UNROLL 1
+#define SM_COST_UNROLL 2
 #endif
 // Pixels of a row segment per block: D <= 64 amortises the P + D - 1 moving-pixel staging over
 // 128 pixels (Teddy x16: 0.277 -> 0.255 ms); larger D gains nothing from it (full-res: 3.84 vs

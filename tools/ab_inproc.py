@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Interleaved in-process A/B of library variants (tools/build_variants.sh) on one GPU.
+
+Box clocks drift within a call by more than the effects being measured, so timing variant A in
+one process and B in the next compares different clocks.  This loads every variant into one
+process (each StereoBatch keeps the library it was created with), then alternates short timed
+rounds A, B, C, A, B, C, ... and reports each variant's median per-kernel HIP-event time and
+median ms per step over the rounds.
+
+usage: python tools/ab_inproc.py [--workload teddy] [--rounds 8] [--steps 5] v1 v2 ...
+       (variant v = tools/variants/libsm_hip_<v>.so; "base" = the in-tree library)
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="teddy")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--kernels", default="", help="comma-separated profile-name filter")
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import bench
+    from mystereomatching_amd import _capi, StereoBatch
+    from mystereomatching_amd import synthetic as S
+
+    H, W, md, paths, B, _ = bench.WORKLOADS[a.workload]
+    batch = S.make_batch(B, H, W, md + 1)
+    sbs = {}
+    for v in a.variants:
+        _capi._lib = None
+        if v == "base":
+            os.environ.pop("SM_HIP_LIB", None)
+        else:
+            os.environ["SM_HIP_LIB"] = os.path.join(ROOT, "tools", "variants", f"libsm_hip_{v}.so")
+        sb = StereoBatch(md, H, W, B, sgm_paths=paths)
+        sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
+        sb.run(0.3, download=False)
+        sb.synchronize()
+        sbs[v] = sb
+    _capi._lib = None
+    step_ms = {v: [] for v in a.variants}
+    kern = {v: {} for v in a.variants}
+    for r in range(a.rounds):
+        for v, sb in sbs.items():
+            sb.profile(True)
+            sb.profile_reset()
+            sb.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                sb.run(0.3, download=False)
+            sb.synchronize()
+            step_ms[v].append((time.perf_counter() - t0) * 1e3 / a.steps)
+            for name, rec in sb.profile_read().items():
+                kern[v].setdefault(name, []).append(rec["total_ms"] / max(1, rec["launches"]))
+        print(f"round {r + 1}/{a.rounds} done", flush=True)
+    want = [k for k in a.kernels.split(",") if k]
+    for v in a.variants:
+        ks = " ".join(f"{n}={statistics.median(x):.4f}" for n, x in kern[v].items() if not want or any(w in n for w in want))
+        print(f"{v:10s} step={statistics.median(step_ms[v]):.3f} ms  {ks}")
+
+
+if __name__ == "__main__":
+    main()

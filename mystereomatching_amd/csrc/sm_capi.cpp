@@ -869,6 +869,9 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));
         HIP_TRY(c, hipMemcpy(c->nl_table, table, 256 * sizeof(double), hipMemcpyHostToDevice));
     }
+    if (getenv("SM_TRACE_ALLOC"))   // diagnostics: where the large buffers landed
+        fprintf(stderr, "[alloc] vm0 %p vm1 %p acc %p arms %p code %p gx %p px %p\n", (void*)c->vm0, (void*)c->vm1,
+                (void*)c->acc, (void*)c->arms, (void*)c->code, (void*)c->gx, (void*)c->px);
     build_luts(c);
     {
         c->fuse_norm_scan = p->fuse_norm_scan != 0;

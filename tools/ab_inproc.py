@@ -8,7 +8,8 @@ rounds A, B, C, A, B, C, ... and reports each variant's median per-kernel HIP-ev
 median ms per step over the rounds.
 
 usage: python tools/ab_inproc.py [--workload teddy] [--rounds 8] [--steps 5] v1 v2 ...
-       (variant v = tools/variants/libsm_hip_<v>.so; "base" = the in-tree library)
+       (variant v = tools/variants/libsm_hip_<v>.so; "base" = the in-tree library; v:ENV=VAL,...
+       sets environment variables while that instance is created)
 """
 import argparse
 import os
@@ -35,7 +36,13 @@ def main():
     H, W, md, paths, B, _ = bench.WORKLOADS[a.workload]
     batch = S.make_batch(B, H, W, md + 1)
     sbs = {}
-    for v in a.variants:
+    names = [f"{v}#{i}" if a.variants.count(v) > 1 else v for i, v in enumerate(a.variants)]
+    for spec, key in zip(a.variants, names):
+        # spec = lib[:ENV=VAL[,ENV=VAL]]: environment set while this instance is created
+        v, _, envs = spec.partition(":")
+        for kv in filter(None, envs.split(",")):
+            k, _, val = kv.partition("=")
+            os.environ[k] = val
         _capi._lib = None
         if v == "base":
             os.environ.pop("SM_HIP_LIB", None)
@@ -45,10 +52,12 @@ def main():
         sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
         sb.run(0.3, download=False)
         sb.synchronize()
-        sbs[v] = sb
+        sbs[key] = sb
+        for kv in filter(None, envs.split(",")):
+            os.environ.pop(kv.partition("=")[0], None)
     _capi._lib = None
-    step_ms = {v: [] for v in a.variants}
-    kern = {v: {} for v in a.variants}
+    step_ms = {v: [] for v in names}
+    kern = {v: {} for v in names}
     for r in range(a.rounds):
         for v, sb in sbs.items():
             sb.profile(True)
@@ -63,7 +72,7 @@ def main():
                 kern[v].setdefault(name, []).append(rec["total_ms"] / max(1, rec["launches"]))
         print(f"round {r + 1}/{a.rounds} done", flush=True)
     want = [k for k in a.kernels.split(",") if k]
-    for v in a.variants:
+    for v in names:
         ks = " ".join(f"{n}={statistics.median(x):.4f}" for n, x in kern[v].items() if not want or any(w in n for w in want))
         print(f"{v:10s} step={statistics.median(step_ms[v]):.3f} ms  {ks}")
 

@@ -65,11 +65,18 @@ __global__ __launch_bounds__(256) void k_gf_img_v(const uint8_t* __restrict__ bg
     float ring[GF_RING];
     float S = 0.f;
     for (int j0 = 0; j0 < H + GF_R; j0 += GF_RING) {
+        // the block's inputs first: one memory latency per block, not per row
+        float vin[GF_RING];
+#pragma unroll
+        for (int s = 0; s < GF_RING; s++) {
+            const int j = j0 + s;
+            vin[s] = j < H ? gf_plane(src + (size_t)j * W * 3, k) : 0.f;
+        }
 #pragma unroll
         for (int s = 0; s < GF_RING; s++) {
             const int j = j0 + s;
             if (j < H + GF_R) {
-                const float v = j < H ? gf_plane(src + (size_t)j * W * 3, k) : 0.f;
+                const float v = vin[s];
                 S = (j == 0 ? 0.f : S) + v;   // CumSum(., 1): 0 + x on row 0; past the end + 0 keeps S(H - 1)
                 ring[s] = S;
                 const int i = j - GF_R;
@@ -87,11 +94,15 @@ __global__ __launch_bounds__(256) void k_gf_img_h(float* __restrict__ planes, in
     float ring[GF_RING];
     float S = 0.f;
     for (int j0 = 0; j0 < W + GF_R; j0 += GF_RING) {
+        // the block's inputs first (originals: the in-place outputs so far reach only j0 - 10)
+        float vin[GF_RING];
+#pragma unroll
+        for (int s = 0; s < GF_RING; s++) vin[s] = j0 + s < W ? row[j0 + s] : 0.f;
 #pragma unroll
         for (int s = 0; s < GF_RING; s++) {
             const int j = j0 + s;
             if (j < W + GF_R) {
-                if (j < W) S = (j == 0) ? row[0] : S + row[j];   // CumSum(., 2): x = 0 copies
+                if (j < W) S = (j == 0) ? vin[0] : S + vin[s];   // CumSum(., 2): x = 0 copies
                 ring[s] = S;
                 const int i = j - GF_R;
                 if (i >= 0) row[i] = i >= GF_R + 1 ? S - ring[(s + 1) % GF_RING] : S;

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--kernels", default="", help="comma-separated profile-name filter")
+    ap.add_argument("--agg", default="CBCA", help="aggregation (CBCA, GF, NL)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import bench
@@ -48,7 +49,7 @@ def main():
             os.environ.pop("SM_HIP_LIB", None)
         else:
             os.environ["SM_HIP_LIB"] = os.path.join(ROOT, "tools", "variants", f"libsm_hip_{v}.so")
-        sb = StereoBatch(md, H, W, B, sgm_paths=paths)
+        sb = StereoBatch(md, H, W, B, sgm_paths=paths, aggregation=a.agg)
         sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
         sb.run(0.3, download=False)
         sb.synchronize()

@@ -32,6 +32,13 @@ namespace sm {
 
 namespace {
 
+#ifndef SM_GF_PARTS
+#define SM_GF_PARTS 2   // parts a block of GF_RING positions is loaded and processed in (1, 2, 4, 5)
+// (same-process A/B, Teddy x16 GF: 1 part 5.05 / 4.56 ms, 2 parts 4.72 / 4.18 ms, 4 parts 5.13 /
+// 4.62 ms, 5 parts 4.71 / 4.69 ms; a software-pipelined variant with the next block's inputs in
+// flight needed 264-288 VGPRs, one wave per SIMD, and ran 7.5-7.8 ms)
+#endif
+
 constexpr int GF_R = 9;                // guideFilterCore_matlab(I, p, 9, eps) (cpp:4509)
 constexpr int GF_RING = 2 * GF_R + 2;  // S(j) .. S(j - 2r - 1)
 
@@ -180,11 +187,19 @@ __global__ __launch_bounds__(64) void k_gf_sweep(const GfArgs a) {
 
     float ring[4][GF_RING];
     float S[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int j0 = 0; j0 < len + GF_R; j0 += GF_RING) {
-        // inputs of this block of positions
-        float x[GF_RING][4];
+    // blocks of GF_RING positions, each processed in SM_GF_PARTS parts of GF_RING / SM_GF_PARTS
+    // (fewer input registers per part: more waves per SIMD; the ring slots stay static)
+    constexpr int PART = GF_RING / SM_GF_PARTS;
+    for (int j00 = 0; j00 < len + GF_R; j00 += GF_RING)
 #pragma unroll
-        for (int sl = 0; sl < GF_RING; sl++) {
+    for (int part = 0; part < SM_GF_PARTS; part++) {
+        const int j0 = j00 + part * PART;
+        if (j0 >= len + GF_R) break;
+        // inputs of this part of the block
+        float x[PART][4];
+#pragma unroll
+        for (int sp = 0; sp < PART; sp++) {
+            const int sl = sp;
             const int j = j0 + sl;
             const bool in = j < len;
             const size_t jv = (size_t)(in ? j : len - 1);
@@ -205,15 +220,16 @@ __global__ __launch_bounds__(64) void k_gf_sweep(const GfArgs a) {
             }
         }
 #pragma unroll
-        for (int sl = 0; sl < GF_RING; sl++) {
-            const int j = j0 + sl;
+        for (int sp = 0; sp < PART; sp++) {
+            const int sl = part * PART + sp;   // ring slot (static)
+            const int j = j00 + sl;
             if (j >= len + GF_R) break;
             float bx[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 // CumSum: 0 + x at the first row (V), x itself at the first column (H); past the
                 // end + 0, which keeps S(len - 1) (S is never -0)
-                S[c] = (j == 0) ? (HORIZ ? x[sl][c] : 0.f + x[sl][c]) : S[c] + x[sl][c];
+                S[c] = (j == 0) ? (HORIZ ? x[sp][c] : 0.f + x[sp][c]) : S[c] + x[sp][c];
                 ring[c][sl] = S[c];
             }
             const int i = j - GF_R;

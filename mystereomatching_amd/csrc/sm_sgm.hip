@@ -312,6 +312,13 @@ __device__ __forceinline__ uint32_t row_umin(uint32_t v) {  // every lane: min o
     return umin_dpp<DPP_ROW_MIRROR>(v);
 }
 
+__device__ __forceinline__ float row_fmin(float v) {  // every lane: min over its row of 16 (any sign)
+    v = fminf(v, dpp_f<DPP_QUAD_1032>(v));
+    v = fminf(v, dpp_f<DPP_QUAD_2301>(v));
+    v = fminf(v, dpp_f<DPP_ROW_HALF_MIRROR>(v));
+    return fminf(v, dpp_f<DPP_ROW_MIRROR>(v));
+}
+
 template <int KV, int T>
 struct RowTile {
     float c[T][4 * KV];
@@ -322,6 +329,9 @@ struct RowTile {
 template <int KV, int MODE, int T, bool FULLC>
 __global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
     constexpr int K = 4 * KV;
+    constexpr bool SG = (MODE & SGM_SIGNED) != 0;   // costs of either sign (GF): float mins
+    auto mn = [](float x, float y) { return SG ? fminf(x, y) : fmin_pos(x, y); };
+    auto rmin = [](float x) { return SG ? row_fmin(x) : __builtin_bit_cast(float, row_umin(__builtin_bit_cast(uint32_t, x))); };
     const int lane = threadIdx.x & 63, row = lane >> 4, l16 = lane & 15;
     const int H = a.H, W = a.W, D = a.D;
     const bool vert = a.ru == 0;                      // lines are columns
@@ -416,8 +426,8 @@ __global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
             const float P1 = pen ? p1r : p1, P2 = pen ? p2r : p2;
             float lm = Lp[0];
 #pragma unroll
-            for (int k = 1; k < K; k++) lm = fmin_pos(lm, Lp[k]);
-            const float m = __builtin_bit_cast(float, row_umin(__builtin_bit_cast(uint32_t, lm)));
+            for (int k = 1; k < K; k++) lm = mn(lm, Lp[k]);
+            const float m = rmin(lm);
             const float P1m = P1 - m;
             const float left = row_shift<DPP_ROW_SHR1>(Lp[K - 1]);
             const float right = row_shift<DPP_ROW_SHL1>(Lp[0]);
@@ -428,7 +438,7 @@ __global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
                 const float S1 = Lp[k] - m;
                 const float S2 = prev + P1m;
                 const float S3 = next + P1m;
-                const float mm = fmin_pos(fmin_pos(S1, S2), fmin_pos(S3, P2));
+                const float mm = mn(mn(S1, S2), mn(S3, P2));
                 const float Lk = t.c[s][k] + mm;
                 L[k] = cval[k / 4] ? Lk : FLT_MAX;
             }
@@ -468,7 +478,7 @@ __global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
                         bm = f[k];
                         bi = d0 + k;
                     }
-                const float wm = __builtin_bit_cast(float, row_umin(__builtin_bit_cast(uint32_t, bm)));
+                const float wm = rmin(bm);
                 const uint64_t hit = __ballot(bm == wm);
                 const uint32_t rmask = (uint32_t)(hit >> (row * 16)) & 0xffffu;
                 const int src = row * 16 + __builtin_ctz(rmask);
@@ -493,23 +503,31 @@ __global__ __launch_bounds__(256) void k_sgm_rows(const SgmArgs a) {
     }
 }
 
+template <int KV, bool FULLC, int S>
+static void launch_rows_m(const SgmArgs& a, int mode, dim3 grid, hipStream_t st) {
+    constexpr int T = KV == 1 ? SM_SGM_ROWS_T1 : (KV == 2 ? SM_SGM_ROWS_T2 : (KV == 3 ? SM_SGM_ROWS_T3 : SM_SGM_ROWS_T4));
+    switch (mode) {
+        case SGM_FIRST: hipLaunchKernelGGL((k_sgm_rows<KV, S | SGM_FIRST, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST: hipLaunchKernelGGL((k_sgm_rows<KV, S | SGM_LAST, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_LAST | SGM_KEEP: hipLaunchKernelGGL((k_sgm_rows<KV, S | SGM_LAST | SGM_KEEP, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm_rows<KV, S | SGM_FIRST | SGM_LAST, T, FULLC>), grid, dim3(256), 0, st, a); break;
+        case SGM_FIRST | SGM_LAST | SGM_KEEP:
+            hipLaunchKernelGGL((k_sgm_rows<KV, S | SGM_FIRST | SGM_LAST | SGM_KEEP, T, FULLC>), grid, dim3(256), 0, st, a);
+            break;
+        default: hipLaunchKernelGGL((k_sgm_rows<KV, S, T, FULLC>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
 template <int KV, bool FULLC>
 static void launch_rows_f(const SgmArgs& a, int mode, int n, hipStream_t st) {
     const int nl = a.ru == 0 ? a.W : a.H;
     const int waves = (nl + 3) / 4 * n;
     dim3 grid((waves + 3) / 4);
-    constexpr int T = KV == 1 ? SM_SGM_ROWS_T1 : (KV == 2 ? SM_SGM_ROWS_T2 : (KV == 3 ? SM_SGM_ROWS_T3 : SM_SGM_ROWS_T4));
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
-    switch (mode) {
-        case SGM_FIRST: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_FIRST, T, FULLC>), grid, dim3(256), 0, st, a); break;
-        case SGM_LAST: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_LAST, T, FULLC>), grid, dim3(256), 0, st, a); break;
-        case SGM_LAST | SGM_KEEP: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_LAST | SGM_KEEP, T, FULLC>), grid, dim3(256), 0, st, a); break;
-        case SGM_FIRST | SGM_LAST: hipLaunchKernelGGL((k_sgm_rows<KV, SGM_FIRST | SGM_LAST, T, FULLC>), grid, dim3(256), 0, st, a); break;
-        case SGM_FIRST | SGM_LAST | SGM_KEEP:
-            hipLaunchKernelGGL((k_sgm_rows<KV, SGM_FIRST | SGM_LAST | SGM_KEEP, T, FULLC>), grid, dim3(256), 0, st, a);
-            break;
-        default: hipLaunchKernelGGL((k_sgm_rows<KV, 0, T, FULLC>), grid, dim3(256), 0, st, a); break;
-    }
+    if (a.signed_costs)
+        launch_rows_m<KV, FULLC, SGM_SIGNED>(a, mode, grid, st);
+    else
+        launch_rows_m<KV, FULLC, 0>(a, mode, grid, st);
 }
 
 template <int KV>
@@ -582,7 +600,7 @@ static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
 // (tools/ubench_sgm.hip, KITTI D = 192: 3.5 TB/s with 4 lines per wave vs 5.0 TB/s with one).
 static int rows_kv(const SgmArgs& a, int mode) {
     static const int mask = [] { const char* e = getenv("SM_SGM_ROWS"); return e ? (int)strtol(e, nullptr, 0) : -1; }();
-    if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > SM_SGM_VEC_MIN_D || a.signed_costs) return 0;
+    if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > SM_SGM_VEC_MIN_D) return 0;
     const bool use = mask >= 0 ? ((mask >> a.dir) & 1) : (a.ru == 0 || (mode & SGM_LAST));
     if (!use) return 0;
     const int K = (a.D + 15) / 16;

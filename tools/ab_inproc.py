@@ -9,7 +9,7 @@ median ms per step over the rounds.
 
 usage: python tools/ab_inproc.py [--workload teddy] [--rounds 8] [--steps 5] v1 v2 ...
        (variant v = tools/variants/libsm_hip_<v>.so; "base" = the in-tree library; v:ENV=VAL,...
-       sets environment variables while that instance is created)
+       sets environment variables while that instance is created, v:key=N overrides sm_params)
 """
 import argparse
 import os
@@ -41,21 +41,26 @@ def main():
     for spec, key in zip(a.variants, names):
         # spec = lib[:ENV=VAL[,ENV=VAL]]: environment set while this instance is created
         v, _, envs = spec.partition(":")
+        params = {}
         for kv in filter(None, envs.split(",")):
             k, _, val = kv.partition("=")
-            os.environ[k] = val
+            if k.islower():   # lower-case keys are sm_params overrides (integers)
+                params[k] = int(val)
+            else:
+                os.environ[k] = val
         _capi._lib = None
         if v == "base":
             os.environ.pop("SM_HIP_LIB", None)
         else:
             os.environ["SM_HIP_LIB"] = os.path.join(ROOT, "tools", "variants", f"libsm_hip_{v}.so")
-        sb = StereoBatch(md, H, W, B, sgm_paths=paths, aggregation=a.agg)
+        sb = StereoBatch(md, H, W, B, sgm_paths=paths, aggregation=a.agg, **params)
         sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
         sb.run(0.3, download=False)
         sb.synchronize()
         sbs[key] = sb
         for kv in filter(None, envs.split(",")):
-            os.environ.pop(kv.partition("=")[0], None)
+            if not kv.partition("=")[0].islower():
+                os.environ.pop(kv.partition("=")[0], None)
     _capi._lib = None
     step_ms = {v: [] for v in names}
     kern = {v: {} for v in names}

@@ -106,3 +106,24 @@ def test_teddy_size_maps(oracle, agg):
         sb.close()
     want = oracle.run(pair, oracle.config(H, W, md, aggregation=AGG[agg]))["disp"]
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("agg", ["GF", "NL"])
+@pytest.mark.parametrize("sub_batch,num_streams", [(2, 2), (1, 3), (2, 1)])
+def test_sub_batches_and_streams(oracle, agg, sub_batch, num_streams):
+    """Groups of pairs on alternating streams (sm_params.sub_batch / num_streams) only reschedule
+    sm_run: GF's scratch is per pair, NL's trees, records and staging are shared by the groups and
+    reused across runs — the maps of both runs must equal the oracle's."""
+    H, W, md, n = 29, 41, 15, 5
+    batch = S.make_batch(n, H, W, md + 1, first_index=530)
+    sb = StereoBatch(md, H, W, n, device=0, aggregation=AGG[agg], sub_batch=sub_batch, num_streams=num_streams)
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        first = sb.run(0.3)
+        second = sb.run(0.3)
+    finally:
+        sb.close()
+    cfg = oracle.config(H, W, md, aggregation=AGG[agg])
+    for i in range(n):
+        np.testing.assert_array_equal(first[i], oracle.run({k: batch[k][i] for k in KEYS}, cfg)["disp"])
+    np.testing.assert_array_equal(second, first)

@@ -36,27 +36,23 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
     const int n = H * W;
     const int neh = H * (W - 1), ne = neh + (H - 1) * W;
     t.n = n;
-    // stable counting sort of the edges by weight
+    // stable counting sort of the edges by weight; an edge is stored as its first endpoint u
+    // and its direction (u << 1 | vertical), generated in edge-index order without divisions
     std::vector<int>& order_e = t.s_order_e;
     order_e.resize((size_t)std::max(ne, 1));
+    int bstart[257];
     {
-        int start[257];
-        memset(start, 0, sizeof(start));
-        for (int e = 0; e < ne; e++) start[ew[e] + 1]++;
-        for (int v = 0; v < 256; v++) start[v + 1] += start[v];
-        for (int e = 0; e < ne; e++) order_e[start[ew[e]]++] = e;
+        int pos[257];
+        memset(pos, 0, sizeof(pos));
+        for (int e = 0; e < ne; e++) pos[ew[e] + 1]++;
+        for (int v = 0; v < 256; v++) pos[v + 1] += pos[v];
+        memcpy(bstart, pos, sizeof(pos));
+        int e = 0;
+        for (int y = 0; y < H; y++)            // horizontal: row by row, (y, x) - (y, x + 1)
+            for (int x = 0; x < W - 1; x++, e++) order_e[pos[ew[e]]++] = (y * W + x) << 1;
+        for (int x = 0; x < W; x++)            // vertical: column by column, (y, x) - (y + 1, x)
+            for (int y = 0; y < H - 1; y++, e++) order_e[pos[ew[e]]++] = ((y * W + x) << 1) | 1;
     }
-    auto ends = [&](int e, int& u, int& v) {
-        if (e < neh) {   // horizontal: row y, columns x, x + 1
-            const int y = e / (W - 1), x = e - y * (W - 1);
-            u = y * W + x;
-            v = u + 1;
-        } else {         // vertical: column x, rows y, y + 1
-            const int k = e - neh, x = k / (H - 1), y = k - x * (H - 1);
-            u = y * W + x;
-            v = u + W;
-        }
-    };
     // Kruskal: union-find with path halving and union by size (the accepted set is independent
     // of how the components are merged)
     std::vector<int>&uf = t.s_uf, &sz = t.s_sz, &nconn = t.s_nconn, &conn = t.s_conn;
@@ -75,19 +71,19 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         return x;
     };
     int accepted = 0;
-    for (int j = 0; j < ne && accepted < n - 1; j++) {
-        const int e = order_e[j];
-        int u, v;
-        ends(e, u, v);
+    for (int w = 0; w < 256 && accepted < n - 1; w++)   // weight buckets in order
+    for (int j = bstart[w]; j < bstart[w + 1] && accepted < n - 1; j++) {
+        const int pe = order_e[j];
+        const int u = pe >> 1, v = u + ((pe & 1) ? W : 1);
         int ru = find(u), rv = find(v);
         if (ru == rv) continue;
         if (sz[ru] < sz[rv]) std::swap(ru, rv);
         uf[rv] = ru;
         sz[ru] += sz[rv];
         conn[(size_t)u * 4 + nconn[u]] = v;
-        connw[(size_t)u * 4 + nconn[u]++] = ew[e];
+        connw[(size_t)u * 4 + nconn[u]++] = (uint8_t)w;
         conn[(size_t)v * 4 + nconn[v]] = u;
-        connw[(size_t)v * 4 + nconn[v]++] = ew[e];
+        connw[(size_t)v * 4 + nconn[v]++] = (uint8_t)w;
         accepted++;
     }
     if (accepted != n - 1) return false;

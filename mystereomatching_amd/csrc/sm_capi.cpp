@@ -480,7 +480,7 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     if (s) return s;
     // SM_NL_TRACE=1: host phase times on stderr (diagnostics); "outside" = since the last call's end
     static const bool trace = getenv("SM_NL_TRACE") != nullptr;
-    static auto t_prev_end = std::chrono::steady_clock::now();
+    static thread_local auto t_prev_end = std::chrono::steady_clock::now();
     auto t_last = t_prev_end;
     auto phase = [&](const char* what) {
         if (!trace) return;

@@ -109,61 +109,68 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         }
     }
     if (len != n) return false;
-    // subtree sizes, heavy children
+    // Subtree sizes and heavy children in one reverse breadth-first pass (a node's children come
+    // after it, so their sizes are final when it is reached): the heavy child is the first of
+    // the largest children.
     std::vector<int>& size = t.s_size;
     size.assign(n, 1);
-    for (int i = n - 1; i > 0; i--) size[t.parent[bfs[i]]] += size[bfs[i]];
-    t.heavy.assign(n, -1);
-    for (int x = 0; x < n; x++) {
+    t.heavy.resize(n);
+    for (int i = n - 1; i >= 0; i--) {
+        const int x = bfs[i];
         int best = -1, bs = 0;
-        for (int j = 0; j < t.nchild[x]; j++)
-            if (size[t.child[(size_t)x * 4 + j]] > bs) {
-                bs = size[t.child[(size_t)x * 4 + j]];
+        for (int j = 0; j < t.nchild[x]; j++) {
+            const int cs = size[t.child[(size_t)x * 4 + j]];
+            if (cs > bs) {
+                bs = cs;
                 best = j;
             }
+        }
         t.heavy[x] = (int8_t)best;
+        if (i > 0) size[t.parent[x]] += size[x];
     }
-    // heavy paths in BFS order of their tops; nodes stored bottom -> top
+    // Heavy paths, numbered in breadth-first order of their tops (forward pass): a node continues
+    // its parent's path when it is the parent's heavy child; pos = its depth below the path's top.
+    // Down level = 1 + that of the path its top hangs off (0 for the root's path).
     std::vector<int>& chain_of = t.s_chain_of;
-    chain_of.assign(n, -1);
-    t.chain_start.clear();
+    std::vector<int>& pos = t.s_path;
+    chain_of.resize(n);
+    pos.resize(n);
     t.chain_len.clear();
-    t.chain_nodes.clear();
-    t.chain_nodes.reserve(n);
-    std::vector<int>& tops = t.s_tops;
-    tops.clear();
+    t.down_level.clear();
     for (int i = 0; i < n; i++) {
         const int x = bfs[i];
-        if (x != 0 && t.heavy[t.parent[x]] >= 0 && t.child[(size_t)t.parent[x] * 4 + t.heavy[t.parent[x]]] == x) continue;
-        tops.push_back(x);
-    }
-    const int nch = (int)tops.size();
-    std::vector<int>& path = t.s_path;
-    for (int c = 0; c < nch; c++) {
-        path.clear();
-        for (int x = tops[c];; x = t.child[(size_t)x * 4 + t.heavy[x]]) {
-            path.push_back(x);
+        const int p = t.parent[x];
+        if (i > 0 && t.heavy[p] >= 0 && t.child[(size_t)p * 4 + t.heavy[p]] == x) {
+            const int c = chain_of[p];
             chain_of[x] = c;
-            if (t.heavy[x] < 0) break;
+            pos[x] = pos[p] + 1;
+            t.chain_len[c]++;
+        } else {
+            const int c = (int)t.chain_len.size();
+            chain_of[x] = c;
+            pos[x] = 0;
+            t.chain_len.push_back(1);
+            t.down_level.push_back(i == 0 ? 0 : t.down_level[chain_of[p]] + 1);
         }
-        t.chain_start.push_back((int)t.chain_nodes.size());
-        t.chain_len.push_back((int)path.size());
-        for (int k = (int)path.size() - 1; k >= 0; k--) t.chain_nodes.push_back(path[k]);
     }
-    // rounds: up level from the leaves' side (reverse top order), down level from the root
+    const int nch = (int)t.chain_len.size();
+    t.chain_start.resize(nch);
+    for (int c = 0, o = 0; c < nch; c++) {
+        t.chain_start[c] = o;
+        o += t.chain_len[c];
+    }
+    // Nodes stored bottom -> top, and up levels (1 + the largest up level of a path hanging off
+    // the path, 0 for none) in one reverse pass: the paths hanging off a node lie below it, so
+    // their levels are final when it is reached.
+    t.chain_nodes.resize(n);
     t.up_level.assign(nch, 0);
-    t.down_level.assign(nch, 0);
-    for (int c = nch - 1; c >= 0; c--) {
-        int lv = 0;
-        const int* nodes = t.chain_nodes.data() + t.chain_start[c];
-        for (int k = 0; k < t.chain_len[c]; k++) {
-            const int x = nodes[k];
-            for (int j = 0; j < t.nchild[x]; j++)
-                if (j != t.heavy[x]) lv = std::max(lv, t.up_level[chain_of[t.child[(size_t)x * 4 + j]]] + 1);
-        }
-        t.up_level[c] = lv;
+    for (int i = n - 1; i >= 0; i--) {
+        const int x = bfs[i];
+        const int c = chain_of[x];
+        t.chain_nodes[t.chain_start[c] + t.chain_len[c] - 1 - pos[x]] = x;
+        for (int j = 0; j < t.nchild[x]; j++)
+            if (j != t.heavy[x]) t.up_level[c] = std::max(t.up_level[c], t.up_level[chain_of[t.child[(size_t)x * 4 + j]]] + 1);
     }
-    for (int c = 1; c < nch; c++) t.down_level[c] = t.down_level[chain_of[t.parent[tops[c]]]] + 1;
     return true;
 }
 

@@ -18,7 +18,7 @@ struct NlTree {
     std::vector<int> up_level, down_level;   // rounds of the filter's two passes
     std::vector<int> order;         // breadth-first order from the root
     // scratch kept with the tree so that repeated builds reuse their memory (no page faults)
-    std::vector<int> s_order_e, s_uf, s_sz, s_nconn, s_conn, s_size, s_chain_of, s_tops, s_path;
+    std::vector<int> s_order_e, s_uf, s_sz, s_nconn, s_conn, s_size, s_chain_of, s_path;
     std::vector<uint8_t> s_connw;
     std::vector<double> s_v;
 };

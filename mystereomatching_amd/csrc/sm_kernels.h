@@ -31,6 +31,7 @@ struct PrepArgs {
 
 struct CostArgs {
     float* vm;                  // [n][H][W][D] destination (view's volume)
+    int seg;                    // pixels of a row per block (set by launch_cost: <= the LDS capacity)
     const ulonglong2* code;     // [n][2][H][W]
     const float* gx;            // [n][2][H][W]
     const float* gy;

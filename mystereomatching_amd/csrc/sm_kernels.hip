@@ -572,11 +572,13 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 #ifndef SM_COST_UNROLL
 #define SM_COST_UNROLL 1
 #endif
-// Pixels of a row segment per block: D <= 64 amortises the P + D - 1 moving-pixel staging over
-// 128 pixels (Teddy x16: 0.277 -> 0.255 ms); larger D gains nothing from it (full-res: 3.84 vs
-// 3.89 ms) and keeps 64.
+// Pixels of a row segment per block (at most; launch_cost splits a row into equal segments of
+// at most this many): D <= 64 amortises the P + D - 1 moving-pixel staging over up to 240 pixels
+// (Teddy x16, same-process A/B: 128 -> 0.195-0.203 ms, 160 -> 0.186, 192 -> 0.187-0.191, 225 (two
+// equal segments of the 450-pixel row) -> 0.170-0.179, 240 -> 0.182-0.188, 256 (256 + 194) ->
+// 0.205-0.213); larger D gains nothing from it (full-res: 3.84 vs 3.89 ms) and keeps 64.
 #ifndef SM_COST_P_ONE
-#define SM_COST_P_ONE 128
+#define SM_COST_P_ONE 240
 #endif
 #ifndef SM_COST_P_MULTI
 #define SM_COST_P_MULTI 64
@@ -612,12 +614,12 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     constexpr int COST_P = cost_p(ONE);
     constexpr bool NOSEL = METHOD == SM_M_CENSUS_GRAD && OORZ && CW >= 3;
     const int D = a.D, W = a.W, H = a.H;
-    const int nbx = (W + COST_P - 1) / COST_P;
+    const int nbx = (W + a.seg - 1) / a.seg;
     const int blk = xcd_swizzle(blockIdx.x, gridDim.x);  // neighbouring segments share an XCD's L2
     const int bx = blk % nbx, rest = blk / nbx;
     const int v = rest % H, b = rest / H;
-    const int u0 = bx * COST_P;
-    const int np = min(COST_P, W - u0);
+    const int u0 = bx * a.seg;
+    const int np = min(a.seg, W - u0);         // <= COST_P, the LDS layout's capacity
     const int nm = np + D - 1;                      // moving pixels needed
     const int sgn = a.view == 0 ? 1 : -1;           // moving position = u - sgn * d
     const int mbase = a.view == 0 ? u0 - (D - 1) : u0;
@@ -938,9 +940,13 @@ static void launch_cost_m(const CostArgs& a, dim3 grid, dim3 block, size_t shm, 
         launch_cost_nw<METHOD, LAM1, 4>(a, grid, block, shm, st);
 }
 
-void launch_cost(const CostArgs& a, int method, int n, hipStream_t st) {
+void launch_cost(const CostArgs& a0, int method, int n, hipStream_t st) {
+    // equal segments of at most cost_p pixels (a 450-pixel row: two of 225, not 128 x 3 + 66)
+    CostArgs a = a0;
     const int P = cost_p(a.D <= 64);
-    dim3 grid((unsigned)((a.W + P - 1) / P * a.H * n));
+    const int nb = (a.W + P - 1) / P;
+    a.seg = (a.W + nb - 1) / nb;
+    dim3 grid((unsigned)(nb * a.H * n));
     dim3 block(64, 4);
     const size_t shm = cost_smem_bytes(a.D, method == SM_M_AD ? 2 : a.cwords);
     switch (method) {

@@ -576,12 +576,13 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 // at most this many): D <= 64 amortises the P + D - 1 moving-pixel staging over up to 240 pixels
 // (Teddy x16, same-process A/B: 128 -> 0.195-0.203 ms, 160 -> 0.186, 192 -> 0.187-0.191, 225 (two
 // equal segments of the 450-pixel row) -> 0.170-0.179, 240 -> 0.182-0.188, 256 (256 + 194) ->
-// 0.205-0.213); larger D gains nothing from it (full-res: 3.84 vs 3.89 ms) and keeps 64.
+// 0.205-0.213); larger D takes up to 192 (full res, same process: 64 -> 3.26-3.34 ms, 96 -> 3.24,
+// 128 -> 3.21-3.25, 192 -> 3.13-3.25; KITTI D = 192: 0.366 -> 0.360 ms).
 #ifndef SM_COST_P_ONE
 #define SM_COST_P_ONE 240
 #endif
 #ifndef SM_COST_P_MULTI
-#define SM_COST_P_MULTI 64
+#define SM_COST_P_MULTI 192
 #endif
 __host__ __device__ constexpr int cost_p(bool one) { return one ? SM_COST_P_ONE : SM_COST_P_MULTI; }
 constexpr int LUT_A_N = 129, LUT_B_N = 766;

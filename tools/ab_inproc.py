@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--kernels", default="", help="comma-separated profile-name filter")
     ap.add_argument("--agg", default="CBCA", help="aggregation (CBCA, GF, NL)")
+    ap.add_argument("--copies", type=int, default=1,
+                    help="instances per variant, created interleaved (A B A B ...): device allocations fall into "
+                         "fast and slow placements (DESIGN §6), so compare medians over several instances")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import bench
@@ -37,6 +40,8 @@ def main():
     H, W, md, paths, B, _ = bench.WORKLOADS[a.workload]
     batch = S.make_batch(B, H, W, md + 1)
     sbs = {}
+    if a.copies > 1:
+        a.variants = [v for _ in range(a.copies) for v in a.variants]
     names = [f"{v}#{i}" if a.variants.count(v) > 1 else v for i, v in enumerate(a.variants)]
     for spec, key in zip(a.variants, names):
         # spec = lib[:ENV=VAL[,ENV=VAL]]: environment set while this instance is created
@@ -81,6 +86,17 @@ def main():
     for v in names:
         ks = " ".join(f"{n}={statistics.median(x):.4f}" for n, x in kern[v].items() if not want or any(w in n for w in want))
         print(f"{v:10s} step={statistics.median(step_ms[v]):.3f} ms  {ks}")
+    if a.copies > 1:   # per variant: median over its instances of the per-instance medians
+        print("-- medians over instances --")
+        for v in dict.fromkeys(a.variants):
+            inst = [nm for nm, sp in zip(names, a.variants) if sp == v]
+            ks = {}
+            for nm in inst:
+                for n, x in kern[nm].items():
+                    if not want or any(w in n for w in want):
+                        ks.setdefault(n, []).append(statistics.median(x))
+            st = statistics.median(statistics.median(step_ms[nm]) for nm in inst)
+            print(f"{v:10s} step={st:.3f} ms  " + " ".join(f"{n}={statistics.median(x):.4f}" for n, x in ks.items()))
 
 
 if __name__ == "__main__":

@@ -13,11 +13,13 @@
 #include <chrono>
 #include <cmath>
 #include <map>
+#include <memory>
 #include <new>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "sm_host_pool.h"
 #include "sm_kernels.h"
 #include "sm_nl_tree.h"
 
@@ -75,6 +77,7 @@ struct sm_ctx {
     double nl_table_h[256];     // the weight table (host copy)
     void* nl_host = nullptr;    // pinned staging: edge weights, records, path tables, weight sums
     std::vector<sm::NlTree> nl_trees;   // per pair, kept so that rebuilding reuses their memory
+    std::unique_ptr<sm::HostPool> pool; // host workers of the NL tree builds (created on first use)
     size_t nl_host_bytes = 0;
     double* nl_table = nullptr; // [256]
     double* nl_val = nullptr;   // [cap][nvol]
@@ -502,67 +505,82 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     phase("edges");
     if ((int)c->nl_trees.size() < n) c->nl_trees.resize(n);
     std::vector<sm::NlTree>& trees = c->nl_trees;
-    {
-        // one host thread per pair group: tree, its records and its weight sums (disjoint slices)
-        std::vector<char> ok(n, 0);
-        const int nth = std::max(1, std::min(n, (int)std::thread::hardware_concurrency()));
-        std::vector<std::thread> th;
-        for (int t = 0; t < nth; t++)
-            th.emplace_back([&, t] {
-                for (int b = t; b < n; b += nth) {
-                    ok[b] = sm::nl_build_tree(H, W, ew + (size_t)b * ne, trees[b]);
-                    if (!ok[b]) continue;
-                    sm::nl_pack_records(trees[b], W, b * (int)np, rec + (size_t)b * np * 4);
-                    sm::nl_weight_sums(trees[b], c->nl_table_h, wsum + (size_t)b * np);
-                }
-            });
-        for (auto& x : th) x.join();
-        for (int b = 0; b < n; b++)
-            if (!ok[b]) return fail(c, SM_EINVAL, "NL: spanning tree construction failed");
-    }
+    // host threads over the pairs (disjoint slices of the staging): phase 1 builds each pair's
+    // tree, its records and its weight sums; phase 2 writes the concatenated path tables (paths
+    // of pair b: records from b * npix) and the paths of every round, ordered by round, then
+    // pair, then path (a counting sort whose offsets are summed between the phases)
+    if (!c->pool) c->pool.reset(new sm::HostPool(std::max(1, std::min(c->cap, (int)std::thread::hardware_concurrency()))));
+    auto parallel = [&](const std::function<void(int)>& body) { c->pool->run(n, body); };
+    std::vector<char> ok(n, 0);
+    parallel([&](int b) {
+        ok[b] = sm::nl_build_tree(H, W, ew + (size_t)b * ne, trees[b]);
+        if (!ok[b]) return;
+        sm::nl_pack_records(trees[b], W, b * (int)np, rec + (size_t)b * np * 4);
+        sm::nl_weight_sums(trees[b], c->nl_table_h, wsum + (size_t)b * np);
+    });
+    for (int b = 0; b < n; b++)
+        if (!ok[b]) return fail(c, SM_EINVAL, "NL: spanning tree construction failed");
     phase("trees");
-    // concatenate the pairs' paths (records of pair b start at b * npix) and order them by round
-    std::vector<int> cs, cl, ord_up, ord_dn, upl, dnl;
     int max_up = 0, max_dn = 0;
+    std::vector<int> coff(n + 1, 0);
     for (int b = 0; b < n; b++) {
         const sm::NlTree& t = trees[b];
-        const size_t r0 = (size_t)b * np;
-        for (size_t k = 0; k < t.chain_start.size(); k++) {
-            cs.push_back(t.chain_start[k] + (int)r0);
-            cl.push_back(t.chain_len[k]);
-            upl.push_back(t.up_level[k]);
-            dnl.push_back(t.down_level[k]);
+        for (size_t k = 0; k < t.up_level.size(); k++) {
             max_up = std::max(max_up, t.up_level[k]);
             max_dn = std::max(max_dn, t.down_level[k]);
         }
+        coff[b + 1] = coff[b] + (int)t.chain_len.size();
     }
-    phase("records");
-    const int nchain = (int)cs.size();
-    std::vector<int> up_off(max_up + 2, 0), dn_off(max_dn + 2, 0);
-    for (int k = 0; k < nchain; k++) {
-        up_off[upl[k] + 1]++;
-        dn_off[dnl[k] + 1]++;
-    }
-    for (int r = 0; r <= max_up; r++) up_off[r + 1] += up_off[r];
-    for (int r = 0; r <= max_dn; r++) dn_off[r + 1] += dn_off[r];
-    ord_up.resize(nchain);
-    ord_dn.resize(nchain);
-    {
-        std::vector<int> pu(up_off.begin(), up_off.end() - 1), pd(dn_off.begin(), dn_off.end() - 1);
-        for (int k = 0; k < nchain; k++) {
-            ord_up[pu[upl[k]]++] = k;
-            ord_dn[pd[dnl[k]]++] = k;
+    const int nchain = coff[n];
+    // per round: [pair][round] counts -> round offsets (up_off) and each pair's first slot in a round
+    const int nu = max_up + 1, nd = max_dn + 1;
+    std::vector<int> cu((size_t)n * nu, 0), cd((size_t)n * nd, 0);
+    parallel([&](int b) {
+        const sm::NlTree& t = trees[b];
+        for (size_t k = 0; k < t.up_level.size(); k++) {
+            cu[(size_t)b * nu + t.up_level[k]]++;
+            cd[(size_t)b * nd + t.down_level[k]]++;
         }
-    }
-    // device tables: ints [4][cap * npix]: chain_start, chain_len, order_up, order_down; the
-    // records between their zero paddings; the weight sums
+    });
+    std::vector<int> up_off(nu + 1, 0), dn_off(nd + 1, 0);
+    auto offsets = [n](std::vector<int>& cnt, std::vector<int>& off, int nr) {
+        int o = 0;
+        for (int r = 0; r < nr; r++) {
+            off[r] = o;
+            for (int b = 0; b < n; b++) {
+                const int x = cnt[(size_t)b * nr + r];
+                cnt[(size_t)b * nr + r] = o;   // pair b's first slot in round r
+                o += x;
+            }
+        }
+        off[nr] = o;
+    };
+    offsets(cu, up_off, nu);
+    offsets(cd, dn_off, nd);
+    // device tables: ints [4][cap * npix]: chain_start, chain_len, order_up, order_down, written
+    // straight into the staging
+    int* cs = tabs;
+    int* cl = tabs + slot;
+    int* ord_up = tabs + 2 * slot;
+    int* ord_dn = tabs + 3 * slot;
+    parallel([&](int b) {
+        const sm::NlTree& t = trees[b];
+        const int r0 = b * (int)np, c0 = coff[b];
+        int* pu = &cu[(size_t)b * nu];
+        int* pd = &cd[(size_t)b * nd];
+        for (size_t k = 0; k < t.chain_len.size(); k++) {
+            const int g = c0 + (int)k;
+            cs[g] = t.chain_start[k] + r0;
+            cl[g] = t.chain_len[k];
+            ord_up[pu[t.up_level[k]]++] = g;
+            ord_dn[pd[t.down_level[k]]++] = g;
+        }
+    });
+    phase("records");
     int* I = c->nl_ints;
     int* rec_d = c->nl_rec + sm::NL_REC_PAD * 4;
-    memcpy(tabs, cs.data(), cs.size() * 4);
-    memcpy(tabs + slot, cl.data(), cl.size() * 4);
-    memcpy(tabs + 2 * slot, ord_up.data(), ord_up.size() * 4);
-    memcpy(tabs + 3 * slot, ord_dn.data(), ord_dn.size() * 4);
-    HIP_TRY(c, hipMemcpyAsync(I, tabs, slot * 4 * 4, hipMemcpyHostToDevice, c->st));
+    for (int k = 0; k < 4; k++)   // the tables' used heads only
+        HIP_TRY(c, hipMemcpyAsync(I + k * slot, tabs + k * slot, (size_t)nchain * 4, hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, hipMemcpyAsync(rec_d, rec, (size_t)n * np * 16, hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, hipMemcpyAsync(c->nl_wsum, wsum, (size_t)n * np * 4, hipMemcpyHostToDevice, c->st));
     phase("upload");

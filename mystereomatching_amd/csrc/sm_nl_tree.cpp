@@ -19,6 +19,11 @@
 // The per-node arithmetic and its order are the reference's (sm_nl.hip), so the rounds only
 // schedule work.  This graph construction is O(n) host work per pair (pairs run on parallel host
 // threads); the O(n D) filtering is on the GPU.
+//
+// Layout: Kruskal records each pixel's accepted edges as 2-bit directions + weight bytes (8 bytes
+// a pixel), the walk renumbers the nodes in breadth-first order, and every later pass (sizes,
+// paths, levels, records, weight sums) is a linear sweep over that numbering: a node's children
+// are consecutive and follow it, its parent precedes it.
 #include <stdint.h>
 #include <string.h>
 
@@ -53,144 +58,162 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         for (int x = 0; x < W; x++)            // vertical: column by column, (y, x) - (y + 1, x)
             for (int y = 0; y < H - 1; y++, e++) order_e[pos[ew[e]]++] = ((y * W + x) << 1) | 1;
     }
-    // Kruskal: union-find with path halving and union by size (the accepted set is independent
-    // of how the components are merged)
-    std::vector<int>&uf = t.s_uf, &sz = t.s_sz, &nconn = t.s_nconn, &conn = t.s_conn;
-    std::vector<uint8_t>& connw = t.s_connw;
+    // Kruskal with Rem's union-find (interleaved finds with splicing, a root is its own parent
+    // and parents only grow towards the roots' larger index); the accepted set is independent of
+    // how the components are merged.  A pixel's accepted edges, in acceptance order (the
+    // reference's neighbour lists): adj = count | direction j << (3 + 2 j) | weight j << (32 + 8 j).
+    std::vector<int>& uf = t.s_uf;
+    std::vector<uint64_t>& adj = t.s_adj;
     uf.resize(n);
-    sz.assign(n, 1);
-    nconn.assign(n, 0);
-    conn.resize((size_t)n * 4);
-    connw.resize((size_t)n * 4);
-    for (int i = 0; i < n; i++) uf[i] = i;
-    auto find = [&](int x) {
-        while (uf[x] != x) {
-            uf[x] = uf[uf[x]];
-            x = uf[x];
+    adj.assign(n, 0);
+    int* P = uf.data();
+    for (int i = 0; i < n; i++) P[i] = i;
+    // true if x and y were in different components (which are then merged)
+    auto unite = [P](int x, int y) {
+        while (P[x] != P[y]) {
+            if (P[x] < P[y]) {
+                if (x == P[x]) {
+                    P[x] = P[y];
+                    return true;
+                }
+                const int z = P[x];
+                P[x] = P[y];
+                x = z;
+            } else {
+                if (y == P[y]) {
+                    P[y] = P[x];
+                    return true;
+                }
+                const int z = P[y];
+                P[y] = P[x];
+                y = z;
+            }
         }
-        return x;
+        return false;
+    };
+    auto link = [&](int p, uint64_t dir, uint64_t w) {
+        const uint64_t a = adj[p], k = a & 7u;
+        adj[p] = (a + 1u) | dir << (3 + 2 * k) | w << (32 + 8 * k);
     };
     int accepted = 0;
     for (int w = 0; w < 256 && accepted < n - 1; w++)   // weight buckets in order
     for (int j = bstart[w]; j < bstart[w + 1] && accepted < n - 1; j++) {
         const int pe = order_e[j];
-        const int u = pe >> 1, v = u + ((pe & 1) ? W : 1);
-        int ru = find(u), rv = find(v);
-        if (ru == rv) continue;
-        if (sz[ru] < sz[rv]) std::swap(ru, rv);
-        uf[rv] = ru;
-        sz[ru] += sz[rv];
-        conn[(size_t)u * 4 + nconn[u]] = v;
-        connw[(size_t)u * 4 + nconn[u]++] = (uint8_t)w;
-        conn[(size_t)v * 4 + nconn[v]] = u;
-        connw[(size_t)v * 4 + nconn[v]++] = (uint8_t)w;
+        const uint32_t vert = (uint32_t)pe & 1u;
+        const int u = pe >> 1, v = u + (vert ? W : 1);
+        if (!unite(u, v)) continue;
+        const uint32_t dc = W > 1 ? 2u * vert : 0u;   // (one column: +W is +1)
+        link(u, dc, (uint32_t)w);        // u -> v: +1 or +W
+        link(v, dc + 1u, (uint32_t)w);   // v -> u: -1 or -W
         accepted++;
     }
     if (accepted != n - 1) return false;
-    // breadth-first orientation from pixel 0 (build_tree)
-    t.parent.assign(n, -1);
-    t.weight.assign(n, 0);
-    t.nchild.assign(n, 0);
-    t.child.assign((size_t)n * 4, -1);
-    std::vector<int>& bfs = t.order;
-    bfs.resize(n);
-    t.parent[0] = 0;
-    bfs[0] = 0;
-    int head = 0, len = 1;
-    while (head < len) {
-        const int p = bfs[head++];
-        for (int i = 0; i < nconn[p]; i++) {
-            const int q = conn[(size_t)p * 4 + i];
-            if (t.parent[q] != -1) continue;
-            t.parent[q] = p;
-            t.weight[q] = connw[(size_t)p * 4 + i];
-            t.child[(size_t)p * 4 + t.nchild[p]++] = q;
-            bfs[len++] = q;
+    // breadth-first walk from pixel 0 (build_tree): every neighbour but the parent is a child, in
+    // list order; the nodes are numbered in the order the walk reaches them.  pdir = the
+    // direction from a node to its parent (4 for the root), the entry skipped in its list.
+    t.pix.resize(n);
+    t.par.resize(n);
+    t.fc.resize(n);
+    t.nch.resize(n);
+    t.wgt.resize(n);
+    t.cdir.resize(n);
+    std::vector<uint8_t>& pdir = t.s_pdir;
+    pdir.resize(n);
+    t.pix[0] = 0;
+    t.par[0] = 0;
+    t.wgt[0] = 0;
+    pdir[0] = 4;
+    const int delta[4] = {1, -1, W, -W};
+    int len = 1;
+    for (int i = 0; i < len; i++) {
+        const int p = t.pix[i];
+        const uint64_t a = adj[p];
+        const uint32_t cnt = (uint32_t)a & 7u, skip = pdir[i];
+        t.fc[i] = len;
+        uint32_t nc = 0, cd = 0;
+        for (uint32_t j = 0; j < cnt; j++) {
+            const uint32_t c = (uint32_t)(a >> (3 + 2 * j)) & 3u;
+            if (c == skip) continue;
+            t.pix[len] = p + delta[c];
+            t.par[len] = i;
+            t.wgt[len] = (uint8_t)(a >> (32 + 8 * j));
+            pdir[len] = (uint8_t)(c ^ 1u);
+            cd |= c << (2 * nc++);
+            len++;
         }
+        t.nch[i] = (uint8_t)nc;
+        t.cdir[i] = (uint8_t)cd;
     }
     if (len != n) return false;
-    // Subtree sizes and heavy children in one reverse breadth-first pass (a node's children come
-    // after it, so their sizes are final when it is reached): the heavy child is the first of
-    // the largest children.
+    // One reverse pass (a node's children follow it, so their values are final when it is
+    // reached): subtree sizes; the heavy child = the first of the largest children; hlen = nodes
+    // from the node down its path; ul = 1 + the largest ul of a light child anywhere on the path
+    // below the node (0 for none), at a path's top the path's up level.
     std::vector<int>& size = t.s_size;
+    std::vector<int>& hlen = t.s_hlen;
+    std::vector<int>& ul = t.s_ul;
     size.assign(n, 1);
+    hlen.resize(n);
+    ul.resize(n);
     t.heavy.resize(n);
     for (int i = n - 1; i >= 0; i--) {
-        const int x = bfs[i];
+        const int f = t.fc[i], nc = t.nch[i];
         int best = -1, bs = 0;
-        for (int j = 0; j < t.nchild[x]; j++) {
-            const int cs = size[t.child[(size_t)x * 4 + j]];
+        for (int j = 0; j < nc; j++) {
+            const int cs = size[f + j];
             if (cs > bs) {
                 bs = cs;
                 best = j;
             }
         }
-        t.heavy[x] = (int8_t)best;
-        if (i > 0) size[t.parent[x]] += size[x];
+        int u = 0;
+        for (int j = 0; j < nc; j++) u = std::max(u, j == best ? ul[f + j] : ul[f + j] + 1);
+        t.heavy[i] = (int8_t)best;
+        hlen[i] = best >= 0 ? hlen[f + best] + 1 : 1;
+        ul[i] = u;
+        if (i > 0) size[t.par[i]] += size[i];
     }
-    // Heavy paths, numbered in breadth-first order of their tops (forward pass): a node continues
-    // its parent's path when it is the parent's heavy child; pos = its depth below the path's top.
-    // Down level = 1 + that of the path its top hangs off (0 for the root's path).
+    // Heavy paths, numbered in breadth-first order of their tops, in one forward pass: a node
+    // continues its parent's path when it is the parent's heavy child.  A path's records are
+    // stored bottom -> top from its start, so a node's slot is start + hlen - 1.  Down level = 1 +
+    // that of the path its top hangs off (0 for the root's path).
     std::vector<int>& chain_of = t.s_chain_of;
-    std::vector<int>& pos = t.s_path;
     chain_of.resize(n);
-    pos.resize(n);
+    t.slot.resize(n);
+    t.chain_start.clear();
     t.chain_len.clear();
+    t.up_level.clear();
     t.down_level.clear();
+    int next = 0;
     for (int i = 0; i < n; i++) {
-        const int x = bfs[i];
-        const int p = t.parent[x];
-        if (i > 0 && t.heavy[p] >= 0 && t.child[(size_t)p * 4 + t.heavy[p]] == x) {
-            const int c = chain_of[p];
-            chain_of[x] = c;
-            pos[x] = pos[p] + 1;
-            t.chain_len[c]++;
+        const int p = t.par[i];
+        int c;
+        if (i > 0 && t.heavy[p] >= 0 && t.fc[p] + t.heavy[p] == i) {
+            c = chain_of[p];
         } else {
-            const int c = (int)t.chain_len.size();
-            chain_of[x] = c;
-            pos[x] = 0;
-            t.chain_len.push_back(1);
+            c = (int)t.chain_len.size();
+            t.chain_start.push_back(next);
+            t.chain_len.push_back(hlen[i]);
+            t.up_level.push_back(ul[i]);
             t.down_level.push_back(i == 0 ? 0 : t.down_level[chain_of[p]] + 1);
+            next += hlen[i];
         }
-    }
-    const int nch = (int)t.chain_len.size();
-    t.chain_start.resize(nch);
-    for (int c = 0, o = 0; c < nch; c++) {
-        t.chain_start[c] = o;
-        o += t.chain_len[c];
-    }
-    // Nodes stored bottom -> top, and up levels (1 + the largest up level of a path hanging off
-    // the path, 0 for none) in one reverse pass: the paths hanging off a node lie below it, so
-    // their levels are final when it is reached.
-    t.chain_nodes.resize(n);
-    t.up_level.assign(nch, 0);
-    for (int i = n - 1; i >= 0; i--) {
-        const int x = bfs[i];
-        const int c = chain_of[x];
-        t.chain_nodes[t.chain_start[c] + t.chain_len[c] - 1 - pos[x]] = x;
-        for (int j = 0; j < t.nchild[x]; j++)
-            if (j != t.heavy[x]) t.up_level[c] = std::max(t.up_level[c], t.up_level[chain_of[t.child[(size_t)x * 4 + j]]] + 1);
+        chain_of[i] = c;
+        t.slot[i] = t.chain_start[c] + hlen[i] - 1;
     }
     return true;
 }
 
-void nl_pack_records(const NlTree& t, int W, int base, int32_t* rec) {
-    for (int k = 0; k < t.n; k++) {
-        const int x = t.chain_nodes[k];
-        const int nc = t.nchild[x];
-        int meta = nc | (t.heavy[x] + 1) << 3 | t.weight[x] << 16;
+void nl_pack_records(const NlTree& t, int /*W*/, int base, int32_t* rec) {
+    for (int i = 0; i < t.n; i++) {
+        const int nc = t.nch[i], f = t.fc[i];
         uint32_t wp = 0;
-        for (int j = 0; j < nc; j++) {
-            const int q = t.child[(size_t)x * 4 + j], dq = q - x;
-            const int code = dq == 1 ? 0 : dq == -1 ? 1 : dq == W ? 2 : 3;   // +1, -1, +W, -W
-            meta |= code << (6 + 2 * j);
-            wp |= (uint32_t)t.weight[q] << (8 * j);
-        }
-        int32_t* r = rec + (size_t)k * 4;
-        r[0] = x + base;
-        r[1] = meta;
+        for (int j = 0; j < nc; j++) wp |= (uint32_t)t.wgt[f + j] << (8 * j);
+        int32_t* r = rec + (size_t)t.slot[i] * 4;
+        r[0] = t.pix[i] + base;
+        r[1] = nc | (t.heavy[i] + 1) << 3 | t.cdir[i] << 6 | t.wgt[i] << 16;
         r[2] = (int32_t)wp;
-        r[3] = t.parent[x] + base;
+        r[3] = t.pix[t.par[i]] + base;
     }
 }
 
@@ -199,24 +222,22 @@ void nl_weight_sums(NlTree& t, const double* table, float* wsum) {
     std::vector<double>& v = t.s_v;
     v.resize(n);
     for (int i = n - 1; i >= 0; i--) {     // up: children before parents
-        const int x = t.order[i];
         double s = 1.0;
-        for (int j = 0; j < t.nchild[x]; j++) {
-            const int c = t.child[(size_t)x * 4 + j];
-            const double m = v[c] * table[t.weight[c]];
+        for (int j = 0; j < t.nch[i]; j++) {
+            const int c = t.fc[i] + j;
+            const double m = v[c] * table[t.wgt[c]];
             s = s + m;
         }
-        v[x] = s;
+        v[i] = s;
     }
     for (int i = 1; i < n; i++) {          // down: parents before children (the root keeps its sum)
-        const int x = t.order[i];
-        const double w = table[t.weight[x]];
-        const double m = w * v[x];
-        const double q = v[t.parent[x]] - m;
+        const double w = table[t.wgt[i]];
+        const double m = w * v[i];
+        const double q = v[t.par[i]] - m;
         const double r = w * q;
-        v[x] = r + v[x];
+        v[i] = r + v[i];
     }
-    for (int x = 0; x < n; x++) wsum[x] = (float)v[x];
+    for (int i = 0; i < n; i++) wsum[t.pix[i]] = (float)v[i];
 }
 
 }  // namespace sm

@@ -6,20 +6,26 @@
 
 namespace sm {
 
+// The tree is kept in breadth-first numbering: node i is the i-th pixel the walk from pixel 0
+// reaches, so a node's parent precedes it and its children are consecutive (fc[i] ..
+// fc[i] + nch[i] - 1, in discovery order); every pass over the tree is then a linear sweep.
 struct NlTree {
     int n = 0;
-    std::vector<int> parent;        // [n], parent[0] = 0 (root = pixel 0)
-    std::vector<uint8_t> weight;    // [n] edge weight to the parent (0 for the root)
-    std::vector<uint8_t> nchild;    // [n]
-    std::vector<int> child;         // [n][4] in breadth-first discovery order, -1 unused
+    std::vector<int> pix;           // [n] pixel of node i (pix[0] = 0, the root)
+    std::vector<int> par;           // [n] parent node (par[0] = 0)
+    std::vector<int> fc;            // [n] first child node
+    std::vector<uint8_t> nch;       // [n] number of children
+    std::vector<uint8_t> wgt;       // [n] weight of the edge to the parent (0 for the root)
+    std::vector<uint8_t> cdir;      // [n] the children's directions, 2 bits each in child order
+                                    //     (0: +1, 1: -1, 2: +W, 3: -W, as q - pixel)
     std::vector<int8_t> heavy;      // [n] index j of the child continuing the node's path, -1 at leaves
-    std::vector<int> chain_nodes;   // paths concatenated, each bottom -> top
+    std::vector<int> slot;          // [n] record slot of node i (paths concatenated, each bottom -> top)
     std::vector<int> chain_start, chain_len;
     std::vector<int> up_level, down_level;   // rounds of the filter's two passes
-    std::vector<int> order;         // breadth-first order from the root
     // scratch kept with the tree so that repeated builds reuse their memory (no page faults)
-    std::vector<int> s_order_e, s_uf, s_sz, s_nconn, s_conn, s_size, s_chain_of, s_path;
-    std::vector<uint8_t> s_connw;
+    std::vector<int> s_order_e, s_uf, s_size, s_hlen, s_ul, s_chain_of;
+    std::vector<uint64_t> s_adj;
+    std::vector<uint8_t> s_pdir;
     std::vector<double> s_v;
 };
 
@@ -28,7 +34,7 @@ struct NlTree {
 bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t);
 
 // The tree's nodes as the filter kernels' records (NlArgs::rec), in path order: rec[4 k ..] =
-// {node + base, meta, child weights, parent + base} for the k-th entry of t.chain_nodes.
+// {pixel + base, meta, child weights, parent pixel + base} for the node whose slot is k.
 void nl_pack_records(const NlTree& t, int W, int base, int32_t* rec);
 
 // The filtered ones (the NL() weight sums, cpp:4899-4910) as floats: the tree filter of a constant

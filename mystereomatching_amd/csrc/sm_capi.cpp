@@ -74,11 +74,17 @@ struct sm_ctx {
     uint8_t* nl_ew = nullptr;   // [cap][ne]
     int* nl_ints = nullptr;     // chain_start, chain_len, order_up, order_down: [cap][npix] each
     int* nl_rec = nullptr;      // path-node records (4 ints) [cap][npix], zero padding on both sides
+    int* nl_par = nullptr;      // spanning-tree union-find parents [cap][npix] (sm_nl_mst.hip)
+    unsigned long long* nl_best = nullptr;  // lightest edge key offered to each component [cap][npix]
+    uint8_t* nl_mst = nullptr;              // spanning-tree work space (sm::nl_mst_scratch_bytes)
+    unsigned long long* nl_adj = nullptr;   // tree neighbour lists [cap][npix] (downloaded)
     double nl_table_h[256];     // the weight table (host copy)
-    void* nl_host = nullptr;    // pinned staging: edge weights, records, path tables, weight sums
+    std::vector<int> nl_tabs_h; // path tables on the host: [4][cap * npix] (page-locked, nl_reg)
+    std::vector<void*> nl_reg;  // host buffers page-locked with hipHostRegister (unregistered in free_all)
     std::vector<sm::NlTree> nl_trees;   // per pair, kept so that rebuilding reuses their memory
     std::unique_ptr<sm::HostPool> pool; // host workers of the NL tree builds (created on first use)
-    size_t nl_host_bytes = 0;
+    hipStream_t nl_st = nullptr;        // NL front (median, edge weights, spanning trees, list download)
+    hipEvent_t nl_ev_up = nullptr;      // the last uploads from the host tree buffers (on c->st)
     double* nl_table = nullptr; // [256]
     double* nl_val = nullptr;   // [cap][nvol]
     float* nl_wsum = nullptr;   // [cap][npix]
@@ -256,11 +262,21 @@ void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
                     c->gf_s, c->gf_planes, c->gf_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
-                    c->nl_table, c->nl_val, c->nl_wsum};
+                    c->nl_table, c->nl_val, c->nl_wsum, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj};
     for (void* q : ptrs)
         if (q) hipFree(q);
-    if (c->nl_host) hipHostFree(c->nl_host);
-    c->nl_host = nullptr;
+    if (c->nl_st) {
+        hipStreamSynchronize(c->nl_st);
+        hipStreamDestroy(c->nl_st);
+        c->nl_st = nullptr;
+    }
+    if (c->nl_ev_up) {
+        hipEventSynchronize(c->nl_ev_up);
+        hipEventDestroy(c->nl_ev_up);
+        c->nl_ev_up = nullptr;
+    }
+    for (void* q : c->nl_reg) hipHostUnregister(q);
+    c->nl_reg.clear();
     for (auto& r : c->recs) {
         if (r.start) hipEventDestroy(r.start);
         if (r.stop) hipEventDestroy(r.stop);
@@ -477,10 +493,35 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, np = c->npix;
     const int H = c->p.rows, W = c->p.cols, D = c->p.num_disparities;
     const size_t ne = (size_t)H * (W - 1) + (size_t)(H - 1) * W;
-    sm_status s = timed(c, "nl_edges", (double)n * np * 4, [&] {
-        sm::launch_nl_edges(B.bgr, 2 * np * 3, c->nl_med + off * np * 3, c->nl_ew + off * ne, H, W, n, c->st);
-    });
-    if (s) return s;
+    // The front (median, edge weights, spanning trees and the download of their lists) runs on
+    // its own stream: it reads only the colour images, which change only through upload() (which
+    // synchronises), so it need not wait for the work still queued on c->st -- with inputs
+    // resident across calls, the host builds this call's trees while the GPU finishes the
+    // previous call's filter and optimisation.
+    if (!c->nl_st) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->nl_st, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->nl_ev_up, hipEventDisableTiming));
+    }
+    sm_status s;
+    {
+        struct Swap {   // the front's launches (and their profiling events) go to nl_st
+            sm_ctx* c;
+            hipStream_t keep;
+            ~Swap() { c->st = keep; }
+        } sw{c, c->st};
+        c->st = c->nl_st;
+        s = timed(c, "nl_edges", (double)n * np * 4, [&] {
+            sm::launch_nl_edges(B.bgr, 2 * np * 3, c->nl_med + off * np * 3, c->nl_ew + off * ne, H, W, n, c->st);
+        });
+        if (s) return s;
+        // the spanning trees' neighbour lists (Boruvka on the GPU, sm_nl_mst.hip); bytes = the edge
+        // weights read once
+        s = timed(c, "nl_mst", (double)n * ne, [&] {
+            sm::launch_nl_mst(c->nl_ew + off * ne, H, W, n, c->nl_par + off * np, c->nl_best + off * np,
+                              c->nl_mst, c->nl_adj + off * np, c->st);
+        });
+        if (s) return s;
+    }
     // SM_NL_TRACE=1: host phase times on stderr (diagnostics); "outside" = since the last call's end
     static const bool trace = getenv("SM_NL_TRACE") != nullptr;
     static thread_local auto t_prev_end = std::chrono::steady_clock::now();
@@ -492,31 +533,62 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
         t_last = now;
     };
     phase("outside");
-    // pinned staging (sm_alloc): [records n np x 4][chain_start, chain_len, order_up, order_down:
-    // cap np each][weight sums n np][edge weights n ne]; the uploads are asynchronous on the stream,
-    // and every previous use of the staging has completed by the synchronisation below
-    int32_t* rec = (int32_t*)c->nl_host;
-    const size_t slot = (size_t)c->cap * np;
-    int32_t* tabs = rec + slot * 4;
-    float* wsum = (float*)(tabs + slot * 4);
-    uint8_t* ew = (uint8_t*)(wsum + slot);
-    HIP_TRY(c, hipMemcpyAsync(ew, c->nl_ew + off * ne, (size_t)n * ne, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(c, hipStreamSynchronize(c->st));
-    phase("edges");
+    // Host buffers: per pair (NlTree scratch) the neighbour lists, records and weight sums, and
+    // the path tables of the context, all ordinary memory first touched by the pool's workers and
+    // page-locked once (hipHostRegister), so the copies are asynchronous DMA and the host passes
+    // read and write cached memory (random accesses to hipHostMalloc'ed staging measured several
+    // times slower).  Every earlier copy from them has completed by the event wait below.
     if ((int)c->nl_trees.size() < n) c->nl_trees.resize(n);
     std::vector<sm::NlTree>& trees = c->nl_trees;
-    // host threads over the pairs (disjoint slices of the staging): phase 1 builds each pair's
-    // tree, its records and its weight sums; phase 2 writes the concatenated path tables (paths
-    // of pair b: records from b * npix) and the paths of every round, ordered by round, then
-    // pair, then path (a counting sort whose offsets are summed between the phases)
     if (!c->pool) c->pool.reset(new sm::HostPool(std::max(1, std::min(c->cap, (int)std::thread::hardware_concurrency()))));
     auto parallel = [&](const std::function<void(int)>& body) { c->pool->run(n, body); };
+    const size_t slot = (size_t)c->cap * np;
+    auto registered = [&](void* q, size_t bytes) -> bool {
+        if (std::find(c->nl_reg.begin(), c->nl_reg.end(), q) != c->nl_reg.end()) return true;
+        if (hipHostRegister(q, bytes, hipHostRegisterDefault) != hipSuccess) return false;
+        c->nl_reg.push_back(q);
+        return true;
+    };
+    if (trees[n - 1].s_wsum.size() != np) {
+        parallel([&](int b) {
+            trees[b].s_adj.resize(np);
+            trees[b].s_rec.resize(np * 4);
+            trees[b].s_wsum.resize(np);
+        });
+    }
+    if (c->nl_tabs_h.size() != 4 * slot) c->nl_tabs_h.resize(4 * slot);
+    bool reg_ok = registered(c->nl_tabs_h.data(), 4 * slot * 4);
+    for (int b = 0; b < n && reg_ok; b++)
+        reg_ok = registered(trees[b].s_adj.data(), np * 8) && registered(trees[b].s_rec.data(), np * 16) &&
+                 registered(trees[b].s_wsum.data(), np * 4);
+    if (!reg_ok) return fail(c, SM_ENOMEM, "NL: hipHostRegister of the host tree buffers failed");
+    for (int b = 0; b < n; b++)
+        HIP_TRY(c, hipMemcpyAsync(trees[b].s_adj.data(), c->nl_adj + (off + b) * np, np * 8, hipMemcpyDeviceToHost, c->nl_st));
+    HIP_TRY(c, hipStreamSynchronize(c->nl_st));
+    HIP_TRY(c, hipEventSynchronize(c->nl_ev_up));   // the previous call's uploads from the buffers below
+    phase("lists");
+    // host threads over the pairs: phase 1 builds each pair's tree, its records and its weight
+    // sums; phase 2 writes the concatenated path tables (paths of pair b: records from b * npix)
+    // and the paths of every round, ordered by round, then pair, then path (a counting sort whose
+    // offsets are summed between the phases)
     std::vector<char> ok(n, 0);
+    std::vector<int> mx((size_t)n * 2, 0);
     parallel([&](int b) {
-        ok[b] = sm::nl_build_tree(H, W, ew + (size_t)b * ne, trees[b]);
+        sm::NlTree& t = trees[b];
+        ok[b] = sm::nl_tree_from_lists(H, W, t.s_adj.data(), t, c->nl_table_h, b * (int)np, t.s_rec.data(), t.s_wsum.data());
         if (!ok[b]) return;
-        sm::nl_pack_records(trees[b], W, b * (int)np, rec + (size_t)b * np * 4);
-        sm::nl_weight_sums(trees[b], c->nl_table_h, wsum + (size_t)b * np);
+        // the pair's paths per round (histograms indexed by level)
+        t.s_cu.assign(1, 0);
+        t.s_cd.assign(1, 0);
+        for (size_t k = 0; k < t.up_level.size(); k++) {
+            const int u = t.up_level[k], d = t.down_level[k];
+            if (u >= (int)t.s_cu.size()) t.s_cu.resize(u + 1, 0);
+            if (d >= (int)t.s_cd.size()) t.s_cd.resize(d + 1, 0);
+            t.s_cu[u]++;
+            t.s_cd[d]++;
+        }
+        mx[2 * b] = (int)t.s_cu.size() - 1;
+        mx[2 * b + 1] = (int)t.s_cd.size() - 1;
     });
     for (int b = 0; b < n; b++)
         if (!ok[b]) return fail(c, SM_EINVAL, "NL: spanning tree construction failed");
@@ -524,24 +596,19 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     int max_up = 0, max_dn = 0;
     std::vector<int> coff(n + 1, 0);
     for (int b = 0; b < n; b++) {
-        const sm::NlTree& t = trees[b];
-        for (size_t k = 0; k < t.up_level.size(); k++) {
-            max_up = std::max(max_up, t.up_level[k]);
-            max_dn = std::max(max_dn, t.down_level[k]);
-        }
-        coff[b + 1] = coff[b] + (int)t.chain_len.size();
+        max_up = std::max(max_up, mx[2 * b]);
+        max_dn = std::max(max_dn, mx[2 * b + 1]);
+        coff[b + 1] = coff[b] + (int)trees[b].chain_len.size();
     }
     const int nchain = coff[n];
     // per round: [pair][round] counts -> round offsets (up_off) and each pair's first slot in a round
     const int nu = max_up + 1, nd = max_dn + 1;
     std::vector<int> cu((size_t)n * nu, 0), cd((size_t)n * nd, 0);
-    parallel([&](int b) {
+    for (int b = 0; b < n; b++) {
         const sm::NlTree& t = trees[b];
-        for (size_t k = 0; k < t.up_level.size(); k++) {
-            cu[(size_t)b * nu + t.up_level[k]]++;
-            cd[(size_t)b * nd + t.down_level[k]]++;
-        }
-    });
+        std::copy(t.s_cu.begin(), t.s_cu.end(), cu.begin() + (size_t)b * nu);
+        std::copy(t.s_cd.begin(), t.s_cd.end(), cd.begin() + (size_t)b * nd);
+    }
     std::vector<int> up_off(nu + 1, 0), dn_off(nd + 1, 0);
     auto offsets = [n](std::vector<int>& cnt, std::vector<int>& off, int nr) {
         int o = 0;
@@ -557,8 +624,8 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     };
     offsets(cu, up_off, nu);
     offsets(cd, dn_off, nd);
-    // device tables: ints [4][cap * npix]: chain_start, chain_len, order_up, order_down, written
-    // straight into the staging
+    // device tables: ints [4][cap * npix]: chain_start, chain_len, order_up, order_down
+    int* tabs = c->nl_tabs_h.data();
     int* cs = tabs;
     int* cl = tabs + slot;
     int* ord_up = tabs + 2 * slot;
@@ -581,8 +648,11 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     int* rec_d = c->nl_rec + sm::NL_REC_PAD * 4;
     for (int k = 0; k < 4; k++)   // the tables' used heads only
         HIP_TRY(c, hipMemcpyAsync(I + k * slot, tabs + k * slot, (size_t)nchain * 4, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, hipMemcpyAsync(rec_d, rec, (size_t)n * np * 16, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->nl_wsum, wsum, (size_t)n * np * 4, hipMemcpyHostToDevice, c->st));
+    for (int b = 0; b < n; b++) {
+        HIP_TRY(c, hipMemcpyAsync(rec_d + (size_t)b * np * 4, trees[b].s_rec.data(), np * 16, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(c, hipMemcpyAsync(c->nl_wsum + (size_t)b * np, trees[b].s_wsum.data(), np * 4, hipMemcpyHostToDevice, c->st));
+    }
+    HIP_TRY(c, hipEventRecord(c->nl_ev_up, c->st));
     phase("upload");
     sm::NlArgs a{};
     a.chain_start = I;
@@ -877,11 +947,10 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->nl_table, 256))) return s;
         if ((s = dalloc(c, &c->nl_val, cap * c->nvol))) return s;
         if ((s = dalloc(c, &c->nl_wsum, cap * c->npix))) return s;
-        c->nl_host_bytes = cap * c->npix * (16 + 16 + 4) + cap * ne;
-        if (hipHostMalloc(&c->nl_host, c->nl_host_bytes, hipHostMallocDefault) != hipSuccess) {
-            c->nl_host = nullptr;
-            return fail(c, SM_ENOMEM, "pinned NL staging");
-        }
+        if ((s = dalloc(c, &c->nl_par, cap * c->npix))) return s;
+        if ((s = dalloc(c, &c->nl_best, cap * c->npix))) return s;
+        if ((s = dalloc(c, &c->nl_mst, sm::nl_mst_scratch_bytes(p->rows, p->cols, cap)))) return s;
+        if ((s = dalloc(c, &c->nl_adj, cap * c->npix))) return s;
         double* table = c->nl_table_h;
         const double sg = p->nl_sigma < 0.01 ? 0.01 : p->nl_sigma;   // update_table (qx_tree_filter.cpp:23-24)
         for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));

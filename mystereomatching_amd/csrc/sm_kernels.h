@@ -111,6 +111,12 @@ struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids =
 constexpr int NL_REC_PAD = 64;  // zero records after the last path (blocked reads past a path's end)
 void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8_t* ew, int H, int W, int n, hipStream_t st);
 void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_t st);
+// minimum spanning trees of n pairs' edge weights (sm_nl_mst.hip): par / best [n H W] and
+// scratch [nl_mst_scratch_bytes] work space; adj [n H W] the neighbour words of
+// nl_tree_from_lists (sm_nl_tree.h)
+size_t nl_mst_scratch_bytes(int H, int W, int n);
+void launch_nl_mst(const uint8_t* ew, int H, int W, int n, int* par, unsigned long long* best, uint8_t* scratch,
+                   unsigned long long* adj, hipStream_t st);
 
 struct SoArgs {                 // scan-line optimisation "so" (sm_so.hip)
     float* vm;                  // [n][H][W][D] costs (accumulated in place when keep_final)

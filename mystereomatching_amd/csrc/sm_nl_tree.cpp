@@ -35,12 +35,9 @@
 
 namespace sm {
 
-// Builds the tree of one pair (pixel ids 0 .. H W - 1) into t; returns false if the graph is
-// not connected (cannot happen for a 4-neighbour grid with H W > 1).
-bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
+bool nl_build_lists(int H, int W, const uint8_t* ew, NlTree& t) {
     const int n = H * W;
     const int neh = H * (W - 1), ne = neh + (H - 1) * W;
-    t.n = n;
     // stable counting sort of the edges by weight; an edge is stored as its first endpoint u
     // and its direction (u << 1 | vertical), generated in edge-index order without divisions
     std::vector<int>& order_e = t.s_order_e;
@@ -107,7 +104,25 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         link(v, dc + 1u, (uint32_t)w);   // v -> u: -1 or -W
         accepted++;
     }
-    if (accepted != n - 1) return false;
+    return accepted == n - 1;
+}
+
+bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
+    return nl_build_lists(H, W, ew, t) && nl_tree_from_lists(H, W, t.s_adj.data(), t);
+}
+
+bool nl_tree_from_lists(int H, int W, const uint64_t* adj, NlTree& t, const double* table, int base, int32_t* rec,
+                        float* wsum) {
+    const int n = H * W;
+    const bool fused = table && rec && wsum;
+    t.n = n;
+    // a tree has 2 (n - 1) list entries; the sequential pass also brings the lists (fresh from a
+    // device copy) into the cache before the walk reads them in breadth-first order
+    {
+        uint64_t deg = 0;
+        for (int i = 0; i < n; i++) deg += adj[i] & 7u;
+        if (deg != 2 * (uint64_t)(n - 1)) return false;
+    }
     // breadth-first walk from pixel 0 (build_tree): every neighbour but the parent is a child, in
     // list order; the nodes are numbered in the order the walk reaches them.  pdir = the
     // direction from a node to its parent (4 for the root), the entry skipped in its list.
@@ -134,6 +149,7 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         for (uint32_t j = 0; j < cnt; j++) {
             const uint32_t c = (uint32_t)(a >> (3 + 2 * j)) & 3u;
             if (c == skip) continue;
+            if (len == n) return false;   // not a tree (lists from elsewhere are not trusted)
             t.pix[len] = p + delta[c];
             t.par[len] = i;
             t.wgt[len] = (uint8_t)(a >> (32 + 8 * j));
@@ -148,8 +164,11 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
     // One reverse pass (a node's children follow it, so their values are final when it is
     // reached): subtree sizes; the heavy child = the first of the largest children; hlen = nodes
     // from the node down its path; ul = 1 + the largest ul of a light child anywhere on the path
-    // below the node (0 for none), at a path's top the path's up level.
+    // below the node (0 for none), at a path's top the path's up level.  Fused: the up pass of
+    // the weight sums (nl_weight_sums).
     std::vector<int>& size = t.s_size;
+    std::vector<double>& v = t.s_v;
+    if (fused) v.resize(n);
     std::vector<int>& hlen = t.s_hlen;
     std::vector<int>& ul = t.s_ul;
     size.assign(n, 1);
@@ -172,11 +191,20 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
         hlen[i] = best >= 0 ? hlen[f + best] + 1 : 1;
         ul[i] = u;
         if (i > 0) size[t.par[i]] += size[i];
+        if (fused) {
+            double sv = 1.0;
+            for (int j = 0; j < nc; j++) {
+                const double m = v[f + j] * table[t.wgt[f + j]];
+                sv = sv + m;
+            }
+            v[i] = sv;
+        }
     }
     // Heavy paths, numbered in breadth-first order of their tops, in one forward pass: a node
     // continues its parent's path when it is the parent's heavy child.  A path's records are
     // stored bottom -> top from its start, so a node's slot is start + hlen - 1.  Down level = 1 +
-    // that of the path its top hangs off (0 for the root's path).
+    // that of the path its top hangs off (0 for the root's path).  Fused: the down pass of the
+    // weight sums and the records (nl_pack_records).
     std::vector<int>& chain_of = t.s_chain_of;
     chain_of.resize(n);
     t.slot.resize(n);
@@ -199,7 +227,26 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
             next += hlen[i];
         }
         chain_of[i] = c;
-        t.slot[i] = t.chain_start[c] + hlen[i] - 1;
+        const int sl = t.chain_start[c] + hlen[i] - 1;
+        t.slot[i] = sl;
+        if (fused) {
+            if (i > 0) {
+                const double w = table[t.wgt[i]];
+                const double m = w * v[i];
+                const double q = v[p] - m;
+                const double r = w * q;
+                v[i] = r + v[i];
+            }
+            wsum[t.pix[i]] = (float)v[i];
+            const int nc = t.nch[i], f = t.fc[i];
+            uint32_t wp = 0;
+            for (int j = 0; j < nc; j++) wp |= (uint32_t)t.wgt[f + j] << (8 * j);
+            int32_t* rr = rec + (size_t)sl * 4;
+            rr[0] = t.pix[i] + base;
+            rr[1] = nc | (t.heavy[i] + 1) << 3 | t.cdir[i] << 6 | t.wgt[i] << 16;
+            rr[2] = (int32_t)wp;
+            rr[3] = t.pix[p] + base;
+        }
     }
     return true;
 }

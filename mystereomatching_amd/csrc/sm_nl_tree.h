@@ -25,12 +25,29 @@ struct NlTree {
     // scratch kept with the tree so that repeated builds reuse their memory (no page faults)
     std::vector<int> s_order_e, s_uf, s_size, s_hlen, s_ul, s_chain_of;
     std::vector<uint64_t> s_adj;
+    std::vector<int32_t> s_rec;     // (sm_capi.cpp: the pair's neighbour lists, records and weight
+    std::vector<float> s_wsum;      //  sums, page-locked for the copies; paths per round)
+    std::vector<int> s_cu, s_cd;
     std::vector<uint8_t> s_pdir;
     std::vector<double> s_v;
 };
 
+// Neighbour lists of the pair's minimum spanning tree, one 64-bit word per pixel (the tree
+// edges in Kruskal's acceptance order): count | direction j << (3 + 2 j) | weight j << (32 + 8 j),
+// directions 0: +1, 1: -1, 2: +W, 3: -W (one column: 0 / 1).  The product path builds them on
+// the GPU (sm_nl_mst.hip); nl_build_lists is the host's sequential Kruskal (tools, checks).
 // ew: the pair's edge weights, H (W - 1) horizontal edges row by row, then (H - 1) W vertical
-// edges column by column (qx_mst_compute_edges_4neighbor).
+// edges column by column (qx_mst_compute_edges_4neighbor).  Lists land in t.s_adj.
+bool nl_build_lists(int H, int W, const uint8_t* ew, NlTree& t);
+
+// The breadth-first tree from pixel 0 over the lists, its heavy paths, rounds and record slots;
+// false if the lists do not form a spanning tree.  With table, rec and wsum given, the records
+// (as nl_pack_records with this base) and the weight sums (as nl_weight_sums) are written by the
+// same two passes.
+bool nl_tree_from_lists(int H, int W, const uint64_t* adj, NlTree& t, const double* table = nullptr, int base = 0,
+                        int32_t* rec = nullptr, float* wsum = nullptr);
+
+// nl_build_lists + nl_tree_from_lists
 bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t);
 
 // The tree's nodes as the filter kernels' records (NlArgs::rec), in path order: rec[4 k ..] =

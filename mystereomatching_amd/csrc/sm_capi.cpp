@@ -465,7 +465,7 @@ sm_status run_scale(sm_ctx* c, int n, int view, float w, const Bufs& B) {
 // dispOptimize (cpp:1046-1136) for one view: vm[0] with the left image's penalty flags
 // (leftFirst = true) -> DP[0]; vm[1] with the right image's (leftFirst = false) -> DP[1].
 // guideFilter(0, vm) on one view (cpp:4492-4516), MY_GUIDE form: sm_gf.hip
-sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B) {
+sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B, bool solve_all, float w) {
     const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, cap = c->cap, nv = c->nvol;
     sm::GfArgs a{};
     a.vm = view == 0 ? B.vm0 : B.vm1;
@@ -482,6 +482,8 @@ sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B) {
     a.W = c->p.cols;
     a.D = c->p.num_disparities;
     a.eps = c->p.gf_eps;
+    a.solve_all = solve_all;
+    a.scale = w;
     // four volume sweeps, each reading and writing four channels (V0: reads one)
     const double bytes = (double)n * nv * (4 + 16 + 32 + 32 + 16 + 4);
     return timed(c, view == 0 ? "gf" : "gf_r", bytes, [&] { sm::launch_gf(a, n, c->st); });
@@ -489,7 +491,7 @@ sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B) {
 
 // NL() on vm[0] (cpp:4892-4917): edge weights on the GPU, the tree on the host, the tree filter
 // on the GPU (sm_nl.hip, sm_nl_tree.cpp)
-sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
+sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, np = c->npix;
     const int H = c->p.rows, W = c->p.cols, D = c->p.num_disparities;
     const size_t ne = (size_t)H * (W - 1) + (size_t)(H - 1) * W;
@@ -665,6 +667,8 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     a.vm = B.vm0;
     a.wsum = c->nl_wsum;
     a.W = W;
+    a.solve_all = solve_all;
+    a.scale = w;
     // the cost volume (the weight sums came from the host): up rounds, then down rounds; per
     // voxel: cost in, up sum out; up sum in, final out, float out (+ the light children's sums,
     // about one per node)
@@ -678,12 +682,16 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B) {
     return s;
 }
 
+#ifndef SM_FUSE_SOLVE_ALL
+#define SM_FUSE_SOLVE_ALL 1   // sm_run: SolveAll's scaling in the GF / NL output stores (tuning switch)
+#endif
+
 // aggregation other than CBCA: GF on every view (num = Do_refine ? 2 : 1, cpp:4499), NL on vm[0]
-sm_status run_other_agg(sm_ctx* c, int n, const Bufs& B) {
+sm_status run_other_agg(sm_ctx* c, int n, const Bufs& B, bool solve_all = false, float w = 1.f) {
     sm_status s = SM_OK;
     if (c->p.aggregation == SM_AGG_GF)
-        for (int v = 0; v < n_views(c->p) && !s; v++) s = run_gf(c, n, v, B);
-    if (c->p.aggregation == SM_AGG_NL) s = run_nl(c, n, B);
+        for (int v = 0; v < n_views(c->p) && !s; v++) s = run_gf(c, n, v, B, solve_all, w);
+    if (c->p.aggregation == SM_AGG_NL) s = run_nl(c, n, B, solve_all, w);
     return s;
 }
 
@@ -1274,12 +1282,12 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
         if ((s_out = run_prep(c, m2, B))) break;
         if ((s_out = run_cost(c, m2, 0, B))) break;
         if (right_view(c->p) && (s_out = run_cost(c, m2, 1, B))) break;
-        if ((s_out = run_other_agg(c, m2, B))) break;
+        if ((s_out = run_other_agg(c, m2, B, SM_FUSE_SOLVE_ALL, w))) break;   // SolveAll fused into GF / NL
         for (int v = 0; v < n_views(c->p) && !s_out; v++) {
             if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0)
                 s_out = run_cbca(c, m2, v, true, w, B);   // SolveAll fused into the last pass
-            else
-                s_out = run_scale(c, m2, v, w, B);
+            else if (!SM_FUSE_SOLVE_ALL || !(c->p.aggregation == SM_AGG_GF || (c->p.aggregation == SM_AGG_NL && v == 0)))
+                s_out = run_scale(c, m2, v, w, B);      // (GF and NL's vm[0]: fused above)
         }
         if (s_out) break;
         if (ns > 1 && (e = hipEventRecord(c->xev[1 + k % 8], c->st)) != hipSuccess) {

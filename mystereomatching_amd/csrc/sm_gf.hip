@@ -280,6 +280,11 @@ __global__ __launch_bounds__(64) void k_gf_sweep(const GfArgs a) {
                     const float m = ma * (float)q[c];
                     out += m;
                 }
+                if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
+                    float sum = 0.f;
+                    sum += a.scale * out;
+                    out = sum;
+                }
                 if (live) a.vm[vo] = out;
             }
         }

@@ -91,6 +91,8 @@ struct GfArgs {
     GfPix* pix;                 // [n][H][W]
     int H, W, D;
     float eps;
+    int solve_all;              // 1: the output is SolveAll's `0 + w * q` (cpp:2189-2201), w = scale
+    float scale;
 };
 void launch_gf(const GfArgs& a, int n, hipStream_t st);
 
@@ -105,6 +107,8 @@ struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids =
     const double* table;        // exp(-i / (255 sigma)), i = 0..255
     double* val;                // [nodes][D] up sums, then final values (in place)
     float* vm;                  // [nodes][D] costs in, normalised aggregated costs out
+    int solve_all;              // 1: vm out is SolveAll's `0 + w * v` (cpp:2189-2201), w = scale
+    float scale;
     const float* wsum;          // [nodes] the filtered ones (host, nl_weight_sums)
     int W;
 };

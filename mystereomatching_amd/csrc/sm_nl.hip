@@ -262,7 +262,13 @@ __device__ __forceinline__ void nl_down_compute(const NlDownBlock<K>& B, const N
         }
         a.val[(size_t)r.x * P + d] = fin;
         carry = fin;
-        a.vm[(size_t)r.x * P + d] = (float)fin / B.ws[k];
+        float out = (float)fin / B.ws[k];
+        if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
+            float sum = 0.f;
+            sum += a.scale * out;
+            out = sum;
+        }
+        a.vm[(size_t)r.x * P + d] = out;
     }
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Builds tuning variants of libsm_hip.so that differ only in one source file's compile-time
-# switches (default sm_cbca.hip; SRC=sm_kernels or SRC=sm_sgm for the others), for same-box A/B
+# switches (default sm_cbca.hip; SRC=sm_kernels, SRC=sm_sgm, SRC=sm_capi (.cpp), ... for the others), for same-box A/B
 # runs on one GPU box (select with SM_HIP_LIB=<path>, tools/sweep_variants.sh).
 # usage: [SRC=sm_cbca] tools/build_variants.sh NAME "-DSWITCH=value ..." [NAME2 "DEFS2" ...]
 set -e
@@ -9,13 +9,14 @@ cd "$(dirname "$0")/../mystereomatching_amd/csrc"
 make -s
 mkdir -p ../../tools/variants build/var
 rm -f build/var/*.o
+EXT=hip; [ -f $SRC.cpp ] && EXT=cpp
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden -Wno-unused-result -Wno-unused-value"
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
-  /opt/rocm/bin/hipcc $FLAGS $defs -c $SRC.hip -o build/var/${SRC}__$name.o &
+  /opt/rocm/bin/hipcc $FLAGS $defs -c $SRC.$EXT -o build/var/${SRC}__$name.o &
 done
 wait
-OBJS="build/sm_kernels.o build/sm_cbca.o build/sm_sgm.o build/sm_refine.o build/sm_pyramid.o build/sm_so.o build/sm_gf.o build/sm_nl.o build/sm_nl_tree.o build/sm_capi.o"
+OBJS="build/sm_kernels.o build/sm_cbca.o build/sm_sgm.o build/sm_refine.o build/sm_pyramid.o build/sm_so.o build/sm_gf.o build/sm_nl.o build/sm_nl_mst.o build/sm_nl_tree.o build/sm_capi.o"
 for o in build/var/${SRC}__*.o; do
   name=${o#build/var/${SRC}__}; name=${name%.o}
   objs=${OBJS/build\/$SRC.o/$o}

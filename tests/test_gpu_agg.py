@@ -3,7 +3,8 @@
 "GF": guideFilter (stereoMatching.cpp:4492-4516) in its MY_GUIDE form, guideFilterCore_matlab
 (cpp:4975-5104) with the reference's BoxFilter / CumSum (cpp:5107-5202), r = 9, eps = 1e-4;
 its costs can be negative, so SGM runs its float-minimum variant.  "NL": NL() (cpp:4892-4917),
-the MST tree filter of NL/ (Kruskal tree built on the host, filter on the GPU).
+the MST tree filter of NL/ (spanning trees by Boruvka rounds on the GPU -- the same tree as the
+reference's Kruskal -- walked on host threads, filter on the GPU).
 PARITY UNPINNED (the oracle restates the reference text; tests/test_oracle_agg.py cross-checks
 it against an independent numpy restatement).
 """
@@ -64,17 +65,20 @@ def test_batch_maps_match_oracle(oracle, agg, H, W, md, paths, cost):
         np.testing.assert_array_equal(got[i], want)
 
 
-def test_gf_with_refine_both_views(oracle):
-    """Do_refine: guideFilter runs on both views (num = 2, cpp:4499) with each view's colours."""
+@pytest.mark.parametrize("agg", ["GF", "NL"])
+def test_with_refine_both_views(oracle, agg):
+    """Do_refine: guideFilter runs on both views (num = 2, cpp:4499) with each view's colours; NL
+    aggregates vm[0] only, so in sm_run SolveAll is fused into its output for view 0 and a separate
+    pass for view 1."""
     H, W, md = 40, 56, 23
     pair = S.make_pair(H, W, md + 1, 520)
-    sb = StereoBatch(md, H, W, 1, device=0, aggregation=2, do_refine=1)
+    sb = StereoBatch(md, H, W, 1, device=0, aggregation=AGG[agg], do_refine=1)
     try:
         sb.upload(*(pair[k][None] for k in KEYS))
         got = sb.run(0.3)[0]
     finally:
         sb.close()
-    want = oracle.run(pair, oracle.config(H, W, md, aggregation=2, do_refine=1))["disp"]
+    want = oracle.run(pair, oracle.config(H, W, md, aggregation=AGG[agg], do_refine=1))["disp"]
     np.testing.assert_array_equal(got, want)
 
 
@@ -127,3 +131,29 @@ def test_sub_batches_and_streams(oracle, agg, sub_batch, num_streams):
     for i in range(n):
         np.testing.assert_array_equal(first[i], oracle.run({k: batch[k][i] for k in KEYS}, cfg)["disp"])
     np.testing.assert_array_equal(second, first)
+
+
+def test_nl_pipelined_calls_and_new_inputs(oracle):
+    """NL's front (median, edge weights, spanning trees) runs on its own stream and the host walks
+    a call's trees while the GPU still runs the previous call: runs queued back to back without
+    downloads, then new images uploaded and run again, must give the oracle's maps for the images
+    each run saw."""
+    H, W, md, n = 31, 43, 15, 4
+    a = S.make_batch(n, H, W, md + 1, first_index=560)
+    b = S.make_batch(n, H, W, md + 1, first_index=570)
+    sb = StereoBatch(md, H, W, n, device=0, aggregation=AGG["NL"])
+    try:
+        sb.upload(*(a[k] for k in KEYS))
+        for _ in range(3):
+            sb.run(0.3, download=False)
+        got_a = sb.download()
+        sb.upload(*(b[k] for k in KEYS))
+        for _ in range(2):
+            sb.run(0.3, download=False)
+        got_b = sb.download()
+    finally:
+        sb.close()
+    cfg = oracle.config(H, W, md, aggregation=AGG["NL"])
+    for i in range(n):
+        np.testing.assert_array_equal(got_a[i], oracle.run({k: a[k][i] for k in KEYS}, cfg)["disp"])
+        np.testing.assert_array_equal(got_b[i], oracle.run({k: b[k][i] for k in KEYS}, cfg)["disp"])

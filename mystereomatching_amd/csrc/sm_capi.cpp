@@ -489,8 +489,8 @@ sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B, bool solve_all, floa
     return timed(c, view == 0 ? "gf" : "gf_r", bytes, [&] { sm::launch_gf(a, n, c->st); });
 }
 
-// NL() on vm[0] (cpp:4892-4917): edge weights on the GPU, the tree on the host, the tree filter
-// on the GPU (sm_nl.hip, sm_nl_tree.cpp)
+// NL() on vm[0] (cpp:4892-4917): edge weights and spanning trees on the GPU, the tree walk on the
+// host, the tree filter on the GPU (sm_nl.hip, sm_nl_mst.hip, sm_nl_tree.cpp)
 sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, np = c->npix;
     const int H = c->p.rows, W = c->p.cols, D = c->p.num_disparities;

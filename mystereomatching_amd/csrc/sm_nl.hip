@@ -3,7 +3,8 @@
 //
 //   edges      ctmf 3x3 median of each channel with clamped borders (NL/ctmf.c, called with r = 1
 //              by qx_mst_kruskals_image::mst), weight = max channel |difference| of 4-neighbours
-//   tree       host (sm_nl_tree.cpp): Kruskal + breadth-first orientation + heavy paths
+//   tree       GPU spanning trees (sm_nl_mst.hip), host breadth-first orientation + heavy paths
+//              (sm_nl_tree.cpp)
 //   filter     qx_tree_filter::filter (NL/qx_tree_filter.cpp:61-117) in double, w = exp(-c / 25.5):
 //                up(x)  = C(x) + sum_j up(child_j) * w(child_j)           children in list order
 //                fin(x) = w(x) * (fin(parent) - w(x) * up(x)) + up(x),    fin(root) = up(root)

@@ -1,15 +1,16 @@
 // sm_nl_tree.cpp — host side of aggregation "NL" (NL(), stereoMatching.cpp:4892-4917 ->
-// NLCCA::aggreCV, NL/NLCCA.cpp:27-96): the minimum spanning tree of the left colour image and its
-// breadth-first orientation (NL/qx_mst_kruskals_image.cpp:167-277), cut into heavy paths for the
-// GPU tree filter (sm_nl.hip).
+// NLCCA::aggreCV, NL/NLCCA.cpp:27-96): the breadth-first orientation of the left colour image's
+// minimum spanning tree (NL/qx_mst_kruskals_image.cpp:167-277), cut into heavy paths for the GPU
+// tree filter (sm_nl.hip).
 //
-// The tree is the reference's, edge for edge: the GPU's edge weights (max channel difference of
-// the 3x3-median-filtered image, horizontal edges row by row then vertical edges column by column)
-// are sorted stably by weight (a counting sort, qx_sort_increase_using_histogram), Kruskal accepts
-// an edge when its endpoints are in different components, and every accepted edge is appended to
-// both endpoints' neighbour lists; the breadth-first walk from pixel 0 then makes every neighbour
-// but the parent a child, in list order.  Kruskal's acceptance and the neighbour-list order depend
-// only on the edge order, not on the union-find details.
+// The tree is the reference's, edge for edge: over the edge weights (max channel difference of
+// the 3x3-median-filtered image, horizontal edges row by row then vertical edges column by
+// column), Kruskal visits the edges sorted stably by weight (a counting sort,
+// qx_sort_increase_using_histogram), accepts an edge when its endpoints are in different
+// components and appends it to both endpoints' neighbour lists; the breadth-first walk from pixel
+// 0 then makes every neighbour but the parent a child, in list order.  The product path gets the
+// neighbour lists from the GPU (sm_nl_mst.hip: Boruvka, the same tree and list order);
+// nl_build_lists is the sequential Kruskal, kept for the host tools and checks.
 //
 // Heavy paths: every node continues the path of its largest child (the first of equal sizes), so
 // any root path crosses at most log2(n) path boundaries.  The up pass of the filter runs the paths
@@ -17,13 +18,13 @@
 // pass in rounds of depth in the path tree; each round is one launch in which a wave walks a whole
 // path sequentially, the child on its own path arriving in a register and the others from memory.
 // The per-node arithmetic and its order are the reference's (sm_nl.hip), so the rounds only
-// schedule work.  This graph construction is O(n) host work per pair (pairs run on parallel host
-// threads); the O(n D) filtering is on the GPU.
+// schedule work.  The walk is O(n) host work per pair (pairs run on parallel host threads); the
+// O(n D) filtering is on the GPU.
 //
-// Layout: Kruskal records each pixel's accepted edges as 2-bit directions + weight bytes (8 bytes
-// a pixel), the walk renumbers the nodes in breadth-first order, and every later pass (sizes,
-// paths, levels, records, weight sums) is a linear sweep over that numbering: a node's children
-// are consecutive and follow it, its parent precedes it.
+// Layout: the lists are one 64-bit word per pixel (2-bit directions + weight bytes), the walk
+// renumbers the nodes in breadth-first order, and every later pass (sizes, paths, levels, records,
+// weight sums) is a linear sweep over that numbering: a node's children are consecutive and
+// follow it, its parent precedes it.
 #include <stdint.h>
 #include <string.h>
 

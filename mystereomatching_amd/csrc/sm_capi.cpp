@@ -77,7 +77,7 @@ struct sm_ctx {
     int* nl_par = nullptr;      // spanning-tree union-find parents [cap][npix] (sm_nl_mst.hip)
     unsigned long long* nl_best = nullptr;  // lightest edge key offered to each component [cap][npix]
     uint8_t* nl_mst = nullptr;              // spanning-tree work space (sm::nl_mst_scratch_bytes)
-    unsigned long long* nl_adj = nullptr;   // tree neighbour lists [cap][npix] (downloaded)
+    uint32_t* nl_adj = nullptr;             // tree neighbour lists [cap][npix] (downloaded)
     double nl_table_h[256];     // the weight table (host copy)
     std::vector<int> nl_tabs_h; // path tables on the host: [4][cap * npix] (page-locked, nl_reg)
     std::vector<void*> nl_reg;  // host buffers page-locked with hipHostRegister (unregistered in free_all)
@@ -561,11 +561,11 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     if (c->nl_tabs_h.size() != 4 * slot) c->nl_tabs_h.resize(4 * slot);
     bool reg_ok = registered(c->nl_tabs_h.data(), 4 * slot * 4);
     for (int b = 0; b < n && reg_ok; b++)
-        reg_ok = registered(trees[b].s_adj.data(), np * 8) && registered(trees[b].s_rec.data(), np * 16) &&
+        reg_ok = registered(trees[b].s_adj.data(), np * 4) && registered(trees[b].s_rec.data(), np * 16) &&
                  registered(trees[b].s_wsum.data(), np * 4);
     if (!reg_ok) return fail(c, SM_ENOMEM, "NL: hipHostRegister of the host tree buffers failed");
     for (int b = 0; b < n; b++)
-        HIP_TRY(c, hipMemcpyAsync(trees[b].s_adj.data(), c->nl_adj + (off + b) * np, np * 8, hipMemcpyDeviceToHost, c->nl_st));
+        HIP_TRY(c, hipMemcpyAsync(trees[b].s_adj.data(), c->nl_adj + (off + b) * np, np * 4, hipMemcpyDeviceToHost, c->nl_st));
     HIP_TRY(c, hipStreamSynchronize(c->nl_st));
     HIP_TRY(c, hipEventSynchronize(c->nl_ev_up));   // the previous call's uploads from the buffers below
     phase("lists");

@@ -120,7 +120,7 @@ void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_
 // nl_tree_from_lists (sm_nl_tree.h)
 size_t nl_mst_scratch_bytes(int H, int W, int n);
 void launch_nl_mst(const uint8_t* ew, int H, int W, int n, int* par, unsigned long long* best, uint8_t* scratch,
-                   unsigned long long* adj, hipStream_t st);
+                   uint32_t* adj, hipStream_t st);
 
 struct SoArgs {                 // scan-line optimisation "so" (sm_so.hip)
     float* vm;                  // [n][H][W][D] costs (accumulated in place when keep_final)

@@ -17,8 +17,8 @@
 // Each round at least halves the number of components of every pair, so ceil(log2(H W)) rounds
 // finish; a round in which nothing was united clears the flag the later rounds' kernels test
 // first, so they return at once.  (4) one pass builds the neighbour words the host walk reads
-// (sm_nl_tree.cpp): count | direction j << (3 + 2 j) | weight j << (32 + 8 j), directions 0: +1,
-// 1: -1, 2: +W, 3: -W (one column: the vertical edges use 0 / 1).
+// (sm_nl_tree.h): count | direction j << (3 + 2 j) | right weight << 16 | down weight << 24,
+// directions 0: +1, 1: -1, 2: +W, 3: -W (one column: the vertical edges use 0 / 1).
 // Layout (per batch of nn = n H W pixels, in `scratch`): tree flags of each pixel's right edge
 // [nn] and down edge [nn] (bytes), the pixel's (right | down << 8) weights [nn] (u16, the
 // vertical weights transposed from k_nl_edges' column-major order), then one flag per round.
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void k_mst_flatten(int* par, const int* __rest
     st_par(par + t, x);
 }
 
-__global__ __launch_bounds__(256) void k_mst_lists(const uint8_t* __restrict__ scratch, u64* __restrict__ adj, int H, int W, int n) {
+__global__ __launch_bounds__(256) void k_mst_lists(const uint8_t* __restrict__ scratch, uint32_t* __restrict__ adj, int H, int W, int n) {
     const int np = H * W, nn = np * n;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nn) return;
@@ -184,16 +184,15 @@ __global__ __launch_bounds__(256) void k_mst_lists(const uint8_t* __restrict__ s
     cx(k[0], k[2]);
     cx(k[1], k[3]);
     cx(k[1], k[2]);
-    u64 a = 0;
-    int cnt = 0;
+    uint32_t a = (uint32_t)wp[t] << 16;   // the pixel's right | down weights
+    uint32_t cnt = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         if (k[j] == ~0ull) continue;
-        a |= (k[j] & 3ull) << (3 + 2 * j) | (k[j] >> 32) << (32 + 8 * j);
+        a |= (uint32_t)(k[j] & 3ull) << (3 + 2 * j);
         cnt++;
     }
-    a |= (u64)cnt;
-    adj[t] = a;
+    adj[t] = a | cnt;
 }
 
 }  // namespace
@@ -207,7 +206,7 @@ int nl_mst_rounds(int np) {
 size_t nl_mst_scratch_bytes(int H, int W, int n) { return (size_t)4 * H * W * n + 4 * 64; }
 
 void launch_nl_mst(const uint8_t* ew, int H, int W, int n, int* par, unsigned long long* best, uint8_t* scratch,
-                   unsigned long long* adj, hipStream_t st) {
+                   uint32_t* adj, hipStream_t st) {
     const int np = H * W, nn = np * n;
     const unsigned gn = (unsigned)((nn + 255) / 256);
     const int rounds = nl_mst_rounds(np);

@@ -21,7 +21,8 @@
 // schedule work.  The walk is O(n) host work per pair (pairs run on parallel host threads); the
 // O(n D) filtering is on the GPU.
 //
-// Layout: the lists are one 64-bit word per pixel (2-bit directions + weight bytes), the walk
+// Layout: the lists are one 32-bit word per pixel (2-bit directions + the pixel's right / down
+// edge weights), the walk
 // renumbers the nodes in breadth-first order, and every later pass (sizes, paths, levels, records,
 // weight sums) is a linear sweep over that numbering: a node's children are consecutive and
 // follow it, its parent precedes it.
@@ -59,11 +60,21 @@ bool nl_build_lists(int H, int W, const uint8_t* ew, NlTree& t) {
     // Kruskal with Rem's union-find (interleaved finds with splicing, a root is its own parent
     // and parents only grow towards the roots' larger index); the accepted set is independent of
     // how the components are merged.  A pixel's accepted edges, in acceptance order (the
-    // reference's neighbour lists): adj = count | direction j << (3 + 2 j) | weight j << (32 + 8 j).
+    // reference's neighbour lists), as in sm_nl_tree.h: count | direction j << (3 + 2 j), and the
+    // pixel's own right / down edge weights in bits 16-23 / 24-31.
     std::vector<int>& uf = t.s_uf;
-    std::vector<uint64_t>& adj = t.s_adj;
+    std::vector<uint32_t>& adj = t.s_adj;
     uf.resize(n);
-    adj.assign(n, 0);
+    adj.resize(n);
+    {
+        int p = 0;
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++, p++) {
+                const uint32_t wr = x < W - 1 ? ew[y * (W - 1) + x] : 0u;
+                const uint32_t wd = y < H - 1 ? ew[neh + x * (H - 1) + y] : 0u;
+                adj[p] = wr << 16 | wd << 24;
+            }
+    }
     int* P = uf.data();
     for (int i = 0; i < n; i++) P[i] = i;
     // true if x and y were in different components (which are then merged)
@@ -89,9 +100,9 @@ bool nl_build_lists(int H, int W, const uint8_t* ew, NlTree& t) {
         }
         return false;
     };
-    auto link = [&](int p, uint64_t dir, uint64_t w) {
-        const uint64_t a = adj[p], k = a & 7u;
-        adj[p] = (a + 1u) | dir << (3 + 2 * k) | w << (32 + 8 * k);
+    auto link = [&](int p, uint32_t dir) {
+        const uint32_t a = adj[p], k = a & 7u;
+        adj[p] = (a + 1u) | dir << (3 + 2 * k);
     };
     int accepted = 0;
     for (int w = 0; w < 256 && accepted < n - 1; w++)   // weight buckets in order
@@ -101,8 +112,8 @@ bool nl_build_lists(int H, int W, const uint8_t* ew, NlTree& t) {
         const int u = pe >> 1, v = u + (vert ? W : 1);
         if (!unite(u, v)) continue;
         const uint32_t dc = W > 1 ? 2u * vert : 0u;   // (one column: +W is +1)
-        link(u, dc, (uint32_t)w);        // u -> v: +1 or +W
-        link(v, dc + 1u, (uint32_t)w);   // v -> u: -1 or -W
+        link(u, dc);        // u -> v: +1 or +W
+        link(v, dc + 1u);   // v -> u: -1 or -W
         accepted++;
     }
     return accepted == n - 1;
@@ -112,16 +123,29 @@ bool nl_build_tree(int H, int W, const uint8_t* ew, NlTree& t) {
     return nl_build_lists(H, W, ew, t) && nl_tree_from_lists(H, W, t.s_adj.data(), t);
 }
 
-bool nl_tree_from_lists(int H, int W, const uint64_t* adj, NlTree& t, const double* table, int base, int32_t* rec,
+bool nl_tree_from_lists(int H, int W, const uint32_t* adj, NlTree& t, const double* table, int base, int32_t* rec,
                         float* wsum) {
     const int n = H * W;
     const bool fused = table && rec && wsum;
     t.n = n;
-    // a tree has 2 (n - 1) list entries; the sequential pass also brings the lists (fresh from a
-    // device copy) into the cache before the walk reads them in breadth-first order
+    // A sequential check that every entry names a neighbour inside the image and that there are
+    // 2 (n - 1) entries (a tree); it also brings the lists (fresh from a device copy) into the
+    // cache before the walk reads them in breadth-first order.
     {
         uint64_t deg = 0;
-        for (int i = 0; i < n; i++) deg += adj[i] & 7u;
+        int p = 0;
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++, p++) {
+                const uint32_t a = adj[p], cnt = a & 7u;
+                if (cnt > 4) return false;
+                for (uint32_t j = 0; j < cnt; j++) {
+                    const uint32_t c = (a >> (3 + 2 * j)) & 3u;
+                    const bool in = W > 1 ? (c == 0 ? x < W - 1 : c == 1 ? x > 0 : c == 2 ? y < H - 1 : y > 0)
+                                          : (c == 0 ? y < H - 1 : c == 1 && y > 0);
+                    if (!in) return false;
+                }
+                deg += cnt;
+            }
         if (deg != 2 * (uint64_t)(n - 1)) return false;
     }
     // breadth-first walk from pixel 0 (build_tree): every neighbour but the parent is a child, in
@@ -143,17 +167,21 @@ bool nl_tree_from_lists(int H, int W, const uint64_t* adj, NlTree& t, const doub
     int len = 1;
     for (int i = 0; i < len; i++) {
         const int p = t.pix[i];
-        const uint64_t a = adj[p];
-        const uint32_t cnt = (uint32_t)a & 7u, skip = pdir[i];
+        const uint32_t a = adj[p];
+        const uint32_t cnt = a & 7u, skip = pdir[i];
         t.fc[i] = len;
         uint32_t nc = 0, cd = 0;
         for (uint32_t j = 0; j < cnt; j++) {
-            const uint32_t c = (uint32_t)(a >> (3 + 2 * j)) & 3u;
+            const uint32_t c = (a >> (3 + 2 * j)) & 3u;
             if (c == skip) continue;
             if (len == n) return false;   // not a tree (lists from elsewhere are not trusted)
-            t.pix[len] = p + delta[c];
+            const int q = p + delta[c];
+            // the edge's weight: the right / down field of its left / upper end (one column:
+            // every edge is vertical)
+            const uint32_t src = (c & 1u) ? adj[q] : a;
+            t.pix[len] = q;
             t.par[len] = i;
-            t.wgt[len] = (uint8_t)(a >> (32 + 8 * j));
+            t.wgt[len] = (uint8_t)(((c & 2u) || W == 1) ? src >> 24 : src >> 16);
             pdir[len] = (uint8_t)(c ^ 1u);
             cd |= c << (2 * nc++);
             len++;

@@ -24,7 +24,7 @@ struct NlTree {
     std::vector<int> up_level, down_level;   // rounds of the filter's two passes
     // scratch kept with the tree so that repeated builds reuse their memory (no page faults)
     std::vector<int> s_order_e, s_uf, s_size, s_hlen, s_ul, s_chain_of;
-    std::vector<uint64_t> s_adj;
+    std::vector<uint32_t> s_adj;
     std::vector<int32_t> s_rec;     // (sm_capi.cpp: the pair's neighbour lists, records and weight
     std::vector<float> s_wsum;      //  sums, page-locked for the copies; paths per round)
     std::vector<int> s_cu, s_cd;
@@ -32,9 +32,10 @@ struct NlTree {
     std::vector<double> s_v;
 };
 
-// Neighbour lists of the pair's minimum spanning tree, one 64-bit word per pixel (the tree
-// edges in Kruskal's acceptance order): count | direction j << (3 + 2 j) | weight j << (32 + 8 j),
-// directions 0: +1, 1: -1, 2: +W, 3: -W (one column: 0 / 1).  The product path builds them on
+// Neighbour lists of the pair's minimum spanning tree, one 32-bit word per pixel (the tree
+// edges in Kruskal's acceptance order): count | direction j << (3 + 2 j), directions 0: +1, 1: -1,
+// 2: +W, 3: -W (one column: 0 / 1), and the weights of the pixel's own right and down edges
+// (tree edges or not) in bits 16-23 and 24-31.  The product path builds them on
 // the GPU (sm_nl_mst.hip); nl_build_lists is the host's sequential Kruskal (tools, checks).
 // ew: the pair's edge weights, H (W - 1) horizontal edges row by row, then (H - 1) W vertical
 // edges column by column (qx_mst_compute_edges_4neighbor).  Lists land in t.s_adj.
@@ -44,7 +45,7 @@ bool nl_build_lists(int H, int W, const uint8_t* ew, NlTree& t);
 // false if the lists do not form a spanning tree.  With table, rec and wsum given, the records
 // (as nl_pack_records with this base) and the weight sums (as nl_weight_sums) are written by the
 // same two passes.
-bool nl_tree_from_lists(int H, int W, const uint64_t* adj, NlTree& t, const double* table = nullptr, int base = 0,
+bool nl_tree_from_lists(int H, int W, const uint32_t* adj, NlTree& t, const double* table = nullptr, int base = 0,
                         int32_t* rec = nullptr, float* wsum = nullptr);
 
 // nl_build_lists + nl_tree_from_lists

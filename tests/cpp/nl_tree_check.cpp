@@ -61,7 +61,7 @@ int main() {
         // host lists + walk (fused records / weight sums)
         sm::NlTree t;
         if (!sm::nl_build_lists(H, W, ew.data(), t)) return fail("lists", cs);
-        const std::vector<uint64_t> adj = t.s_adj;
+        const std::vector<uint32_t> adj = t.s_adj;
         std::vector<int32_t> rec((size_t)n * 4), rec2((size_t)n * 4);
         std::vector<float> wsum(n);
         if (!sm::nl_tree_from_lists(H, W, adj.data(), t, table.data(), 5, rec.data(), wsum.data())) return fail("walk", cs);
@@ -86,7 +86,9 @@ int main() {
             uint64_t prev = 0;
             for (int j = 0; j < cnt; j++) {
                 const int d = (int)(adj[p] >> (3 + 2 * j)) & 3;
-                const int ww = (int)(adj[p] >> (32 + 8 * j)) & 255;
+                const int q = W == 1 ? (d == 0 ? p + 1 : p - 1) : (d == 0 ? p + 1 : d == 1 ? p - 1 : d == 2 ? p + W : p - W);
+                const uint32_t src = (d & 1) ? adj[q] : adj[p];
+                const int ww = (int)(((d & 2) || W == 1) ? src >> 24 : (src >> 16) & 255);
                 int idx;
                 if (W == 1) idx = H * (W - 1) + x * (H - 1) + (d == 0 ? y : y - 1);
                 else if (d == 0) idx = y * (W - 1) + x;
@@ -98,12 +100,15 @@ int main() {
                 prev = key;
             }
         }
-        // corrupted lists: one entry too many (degree sum off)
+        // corrupted lists: one entry too many (degree sum off); a neighbour outside the image
         if (n >= 4 && W >= 2 && H >= 2) {
-            std::vector<uint64_t> bad = adj;
-            bad[0] = (bad[0] & ~7ull) | ((bad[0] & 7) + 1);
+            std::vector<uint32_t> bad = adj;
+            bad[0] = (bad[0] & ~7u) | ((bad[0] & 7) + 1);
             sm::NlTree t2;
             if (sm::nl_tree_from_lists(H, W, bad.data(), t2)) return fail("corrupt lists accepted", cs);
+            bad = adj;   // an entry pointing out of the image (pixel 0 has no left neighbour)
+            bad[0] = (bad[0] & ~(3u << 3)) | (1u << 3);
+            if (sm::nl_tree_from_lists(H, W, bad.data(), t2)) return fail("out-of-image entry accepted", cs);
         }
         cases++;
     }

@@ -71,14 +71,20 @@ __global__ __launch_bounds__(256) void k_gf_img_v(const uint8_t* __restrict__ bg
     float* out = planes + ((size_t)b * 10 + k) * H * W + x;
     float ring[GF_RING];
     float S = 0.f;
-    for (int j0 = 0; j0 < H + GF_R; j0 += GF_RING) {
-        // the block's inputs first: one memory latency per block, not per row
-        float vin[GF_RING];
+    // the inputs of a block of rows are loaded while the previous block is summed
+    auto fetch = [&](float (&v)[GF_RING], int j0) {
 #pragma unroll
         for (int s = 0; s < GF_RING; s++) {
             const int j = j0 + s;
-            vin[s] = j < H ? gf_plane(src + (size_t)j * W * 3, k) : 0.f;
+            v[s] = j < H ? gf_plane(src + (size_t)j * W * 3, k) : 0.f;
         }
+    };
+    float vin[GF_RING], nxt[GF_RING];
+    fetch(nxt, 0);
+    for (int j0 = 0; j0 < H + GF_R; j0 += GF_RING) {
+#pragma unroll
+        for (int s = 0; s < GF_RING; s++) vin[s] = nxt[s];
+        if (j0 + GF_RING < H + GF_R) fetch(nxt, j0 + GF_RING);   // (rows past H read 0)
 #pragma unroll
         for (int s = 0; s < GF_RING; s++) {
             const int j = j0 + s;
@@ -93,27 +99,85 @@ __global__ __launch_bounds__(256) void k_gf_img_v(const uint8_t* __restrict__ bg
     }
 }
 
-// one thread per (pair, plane, row): row box in place
-__global__ __launch_bounds__(256) void k_gf_img_h(float* __restrict__ planes, int H, int W, int n) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * 10 * H) return;
-    float* row = planes + (size_t)t * W;   // planes are [b][k][H][W]: thread t owns row t
+// one thread per (pair, plane, row): row box in place.  A wave owns 64 consecutive rows and
+// walks them in blocks of GF_RING columns staged through LDS: the block is loaded and the outputs
+// stored row segment by row segment across the lanes (coalesced), while each lane runs its row's
+// sequential cumulative sum on the LDS copy (a lane per row reading global memory directly makes
+// every load instruction touch 64 rows).  Block j0 reads columns j0 .. j0 + 19 and writes the
+// outputs of columns j0 - 9 .. j0 + 10, all of which it has already read (in place is safe).
+#ifndef SM_GF_IMG_H_LDS
+#define SM_GF_IMG_H_LDS 1
+#endif
+constexpr int GF_HP = GF_RING + 1;   // LDS row pitch (odd: conflict-free column reads)
+__global__ __launch_bounds__(64) void k_gf_img_h(float* __restrict__ planes, int H, int W, int n) {
+    const int rows = n * 10 * H;
+    const int lane = threadIdx.x;
+    const int r0 = blockIdx.x * 64;
+    if (!SM_GF_IMG_H_LDS) {
+        const int t = r0 + lane;
+        if (t >= rows) return;
+        float* row = planes + (size_t)t * W;   // planes are [b][k][H][W]: thread t owns row t
+        float ring[GF_RING];
+        float S = 0.f;
+        for (int j0 = 0; j0 < W + GF_R; j0 += GF_RING) {
+            float vin[GF_RING];
+#pragma unroll
+            for (int s = 0; s < GF_RING; s++) vin[s] = j0 + s < W ? row[j0 + s] : 0.f;
+#pragma unroll
+            for (int s = 0; s < GF_RING; s++) {
+                const int j = j0 + s;
+                if (j < W + GF_R) {
+                    if (j < W) S = (j == 0) ? vin[0] : S + vin[s];   // CumSum(., 2): x = 0 copies
+                    ring[s] = S;
+                    const int i = j - GF_R;
+                    if (i >= 0) row[i] = i >= GF_R + 1 ? S - ring[(s + 1) % GF_RING] : S;
+                }
+            }
+        }
+        return;
+    }
+    __shared__ float tin[64 * GF_HP], tout[64 * GF_HP];
+    // element m of a lane's share of a block: row (m * 64 + lane) / GF_RING, column % GF_RING
+    auto fetch = [&](float (&v)[GF_RING], int j0) {
+#pragma unroll
+        for (int m = 0; m < GF_RING; m++) {
+            const int e = m * 64 + lane, rr = e / GF_RING, cc = e - rr * GF_RING;
+            const int j = j0 + cc;
+            v[m] = (r0 + rr < rows && j < W) ? planes[(size_t)(r0 + rr) * W + j] : 0.f;
+        }
+    };
+    float nxt[GF_RING];
+    fetch(nxt, 0);
     float ring[GF_RING];
     float S = 0.f;
     for (int j0 = 0; j0 < W + GF_R; j0 += GF_RING) {
-        // the block's inputs first (originals: the in-place outputs so far reach only j0 - 10)
-        float vin[GF_RING];
 #pragma unroll
-        for (int s = 0; s < GF_RING; s++) vin[s] = j0 + s < W ? row[j0 + s] : 0.f;
+        for (int m = 0; m < GF_RING; m++) {
+            const int e = m * 64 + lane, rr = e / GF_RING, cc = e - rr * GF_RING;
+            tin[rr * GF_HP + cc] = nxt[m];
+        }
+        __syncthreads();
+        // the next block's loads fly while this block is summed (its columns are >= j0 + 20,
+        // past every output this block stores)
+        if (j0 + GF_RING < W + GF_R) fetch(nxt, j0 + GF_RING);   // (columns past W read 0)
 #pragma unroll
         for (int s = 0; s < GF_RING; s++) {
             const int j = j0 + s;
             if (j < W + GF_R) {
-                if (j < W) S = (j == 0) ? vin[0] : S + vin[s];   // CumSum(., 2): x = 0 copies
+                const float v = tin[lane * GF_HP + s];
+                if (j < W) S = (j == 0) ? v : S + v;   // CumSum(., 2): x = 0 copies
                 ring[s] = S;
                 const int i = j - GF_R;
-                if (i >= 0) row[i] = i >= GF_R + 1 ? S - ring[(s + 1) % GF_RING] : S;
+                tout[lane * GF_HP + s] = i >= GF_R + 1 ? S - ring[(s + 1) % GF_RING] : S;
             }
+        }
+        __syncthreads();
+        // store: tout[row][s] is the output of column j0 + s - GF_R
+#pragma unroll
+        for (int m = 0; m < GF_RING; m++) {
+            const int e = m * 64 + lane, rr = e / GF_RING, cc = e - rr * GF_RING;
+            const int i = j0 + cc - GF_R;
+            if (r0 + rr < rows && i >= 0 && i < W) planes[(size_t)(r0 + rr) * W + i] = tout[rr * GF_HP + cc];
         }
     }
 }
@@ -298,7 +362,7 @@ void launch_gf(const GfArgs& a, int n, hipStream_t st) {
         const int th = n * 10 * a.W;
         hipLaunchKernelGGL(k_gf_img_v, dim3((th + 255) / 256), dim3(256), 0, st, a.bgr, a.planes, a.H, a.W, n, a.bgr_pair_stride);
         const int tr = n * 10 * a.H;
-        hipLaunchKernelGGL(k_gf_img_h, dim3((tr + 255) / 256), dim3(256), 0, st, a.planes, a.H, a.W, n);
+        hipLaunchKernelGGL(k_gf_img_h, dim3((tr + 63) / 64), dim3(64), 0, st, a.planes, a.H, a.W, n);
         const size_t tp = (size_t)n * a.H * a.W;
         hipLaunchKernelGGL(k_gf_pix, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, st, a.planes, a.pix, a.H, a.W, n, a.eps);
     }

@@ -476,6 +476,8 @@ sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B, bool solve_all, floa
     a.s3 = c->gf_s + (2 * cap + off) * nv;
     a.bgr = B.bgr + (size_t)view * c->npix * 3;   // I_c[view] (cpp:4502)
     a.bgr_pair_stride = 2 * c->npix * 3;
+    a.px = B.px + (size_t)view * c->npix;        // packed words of the same image (run_prep)
+    a.px_pair_stride = 2 * c->npix;
     a.planes = c->gf_planes + off * 10 * c->npix;
     a.pix = c->gf_pix + off * c->npix;
     a.H = c->p.rows;

@@ -45,8 +45,8 @@ constexpr int GF_RING = 2 * GF_R + 2;  // S(j) .. S(j - 2r - 1)
 // ---------------------------------------------------------------------------------------------
 // Image planes: 0 = ones, 1..3 = B, G, R, 4..9 = BB, BG, BR, GG, GR, RR (var_I order, cpp:5005-5016)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float gf_plane(const uint8_t* px, int k) {
-    const float b = (float)px[0], g = (float)px[1], r = (float)px[2];
+__device__ __forceinline__ float gf_plane_w(uint32_t w, int k) {   // w = B | G << 8 | R << 16
+    const float b = (float)(w & 0xffu), g = (float)((w >> 8) & 0xffu), r = (float)((w >> 16) & 0xffu);
     switch (k) {
         case 0: return 1.0f;
         case 1: return b;
@@ -62,12 +62,13 @@ __device__ __forceinline__ float gf_plane(const uint8_t* px, int k) {
 }
 
 // one thread per (pair, plane, column): column box of the plane into planes[b][k][H][W]
-__global__ __launch_bounds__(256) void k_gf_img_v(const uint8_t* __restrict__ bgr, float* __restrict__ planes, int H, int W,
-                                                  int n, size_t bgr_pair_stride) {
+// (the colours come from the packed BGR words k_pack_bgr made in the prep: one dword per row)
+__global__ __launch_bounds__(256) void k_gf_img_v(const uint32_t* __restrict__ pxw, float* __restrict__ planes, int H, int W,
+                                                  int n, size_t px_pair_stride) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n * 10 * W) return;
     const int x = t % W, k = (t / W) % 10, b = t / (W * 10);
-    const uint8_t* src = bgr + (size_t)b * bgr_pair_stride + (size_t)x * 3;
+    const uint32_t* src = pxw + (size_t)b * px_pair_stride + x;
     float* out = planes + ((size_t)b * 10 + k) * H * W + x;
     float ring[GF_RING];
     float S = 0.f;
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void k_gf_img_v(const uint8_t* __restrict__ bg
 #pragma unroll
         for (int s = 0; s < GF_RING; s++) {
             const int j = j0 + s;
-            v[s] = j < H ? gf_plane(src + (size_t)j * W * 3, k) : 0.f;
+            v[s] = j < H ? gf_plane_w(src[(size_t)j * W], k) : 0.f;
         }
     };
     float vin[GF_RING], nxt[GF_RING];
@@ -360,7 +361,7 @@ __global__ __launch_bounds__(64) void k_gf_sweep(const GfArgs a) {
 void launch_gf(const GfArgs& a, int n, hipStream_t st) {
     {
         const int th = n * 10 * a.W;
-        hipLaunchKernelGGL(k_gf_img_v, dim3((th + 255) / 256), dim3(256), 0, st, a.bgr, a.planes, a.H, a.W, n, a.bgr_pair_stride);
+        hipLaunchKernelGGL(k_gf_img_v, dim3((th + 255) / 256), dim3(256), 0, st, a.px, a.planes, a.H, a.W, n, a.px_pair_stride);
         const int tr = n * 10 * a.H;
         hipLaunchKernelGGL(k_gf_img_h, dim3((tr + 63) / 64), dim3(64), 0, st, a.planes, a.H, a.W, n);
         const size_t tp = (size_t)n * a.H * a.W;

@@ -87,6 +87,8 @@ struct GfArgs {
     float *s0, *s1, *s2, *s3;   // four scratch volumes [n][H][W][D]
     const uint8_t* bgr;         // the view's colour image of pair 0 ([n][2][H][W][3] + view offset)
     size_t bgr_pair_stride;     // bytes between pairs
+    const uint32_t* px;         // the same image as packed B | G << 8 | R << 16 words (prep's k_pack_bgr)
+    size_t px_pair_stride;      // words between pairs
     float* planes;              // [n][10][H][W] scratch
     GfPix* pix;                 // [n][H][W]
     int H, W, D;

@@ -109,7 +109,10 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #define SM_CB_V_READLANE 1
 #endif
 #ifndef SM_CB_PROBE_NOVG
-#define SM_CB_PROBE_NOVG 0   // timing probe only (wrong results): V sweeps skip the other image's arm gather
+#define SM_CB_PROBE_NOVG 0   // timing probes only (wrong results): V sweeps skip the other image's arm gather (1) or gather row 0 every time (2)
+#endif
+#ifndef SM_CB_VG_AUX
+#define SM_CB_VG_AUX 0       // cache policy bits of the V sweeps' arm gathers (tuning)
 #endif
 __host__ __device__ constexpr int cbca_win_ring(int T) { return 63 + T; }
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
@@ -145,6 +148,23 @@ __host__ __device__ constexpr int cbca_kw(bool horiz, int mode) {
 }
 // staged words per set and row: KW own + KW + 63 other
 __host__ __device__ constexpr int cbca_spw(int kw) { return 2 * kw + 63; }
+// V sweeps as blocks of WPB INDEPENDENT waves on WPB adjacent columns of one chunk
+// (SM_CB_WPB_*_V): every wave runs the one-line sweep with its own rings and its own gathers — no
+// staging and no per-tile barrier — but the waves of a block share one CU, so a row's
+// other-image gathers of neighbouring columns (spans overlapping in all but one word per column)
+// are served by that CU's L1 instead of each going to L2.  One block per CU (WPB rings fill its
+// LDS), the same waves per CU as one-wave blocks.  Measured (full resolution, interleaved
+// same-process A/B, profiles/r2l/ab_vsweeps.txt): v_norm 6.71 -> 9.56 ms at WPB = 5, v_scan
+// 5.06 -> 5.86 ms at WPB = 6 — slower; off.
+#ifndef SM_CB_WPB_SCAN_V
+#define SM_CB_WPB_SCAN_V 1
+#endif
+#ifndef SM_CB_WPB_NORM_V
+#define SM_CB_WPB_NORM_V 1
+#endif
+__host__ __device__ constexpr int cbca_wpb(bool horiz, int mode) {
+    return (horiz || SM_CB_VGROUP) ? 1 : (mode == CB_SCAN ? SM_CB_WPB_SCAN_V : (mode == CB_NORM ? SM_CB_WPB_NORM_V : 1));
+}
 
 template <bool HORIZ, int MODE, int KW = 1>
 struct CbCfg {
@@ -177,6 +197,7 @@ __host__ __device__ inline int cbca_ring_words(int lag, bool horiz, int mode, in
 }
 __host__ __device__ inline int cbca_win_words(bool horiz, int mode) {
     if (!SM_CB_LDS_WIN) return 0;
+    if (!horiz && SM_CB_V_READLANE) return 0;   // V sweeps: own words by v_readlane, gathers in registers
     const int T = cbca_tile(horiz, mode);
     const int nsets = mode == CB_SCAN ? 1 : (mode == CB_NORM ? 2 : 3);
     return nsets * (T + (horiz ? (SM_CB_WIN_RING ? 2 * cbca_win_ring(T) : 64 + T - 1) : 0));
@@ -325,9 +346,12 @@ struct CbLine {
                 const int q = RV ? base + lane + c64 + 63 : base + lane - c64;
                 t.a1v[s] = buf_ld_u32(A1r[s], (lane < T && (unsigned)q < (unsigned)len) ? (uint32_t)q * 4u : 0x80000000u, 0);
             } else {
-                const __amdgpu_buffer_rsrc_t ra1 = bounded_rsrc(A1v[s] + (long)base * (long)(pstride * 4), aend);
+                // (SM_CB_PROBE_NOVG == 2, timing only: every gather re-reads row 0 of the plane)
+                const __amdgpu_buffer_rsrc_t ra1 = bounded_rsrc(A1v[s] + (SM_CB_PROBE_NOVG == 2 ? 0L : (long)base * (long)(pstride * 4)), aend);
 #pragma unroll
-                for (int k = 0; k < T; k++) t.a1[s][k] = SM_CB_PROBE_NOVG ? 0x00110011u : buf_ld_u32(ra1, ao[k], 0);
+                for (int k = 0; k < T; k++)
+                    t.a1[s][k] = SM_CB_PROBE_NOVG == 1 ? 0x00110011u
+                                                       : __builtin_amdgcn_raw_buffer_load_b32(ra1, (int)(SM_CB_PROBE_NOVG == 2 ? ao[0] : ao[k]), 0, SM_CB_VG_AUX);
             }
         }
     }
@@ -546,15 +570,16 @@ struct CbLine {
 #define SM_CB_CHUNK_MAJOR_V 1
 #endif
 
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, int WPB>
 __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
     CbLine<HORIZ, MODE, FULL, SCALE, RV, KW> L;
     constexpr int T = CbCfg<HORIZ, MODE, KW>::T;
     constexpr int NSETS = CbCfg<HORIZ, MODE, KW>::NSETS;
-    L.lane = KW > 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+    L.lane = (KW > 1 || WPB > 1) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
     L.wv = KW > 1 ? (int)(threadIdx.x >> 6) : 0;
+    const int wb = WPB > 1 ? (int)(threadIdx.x >> 6) : 0;      // independent wave of a WPB block
     const int nchunks = (a.D + 63) >> 6;
-    const int ngroups = ((HORIZ ? a.H : a.W) + KW - 1) / KW;   // KW = 1: one line per block
+    const int ngroups = ((HORIZ ? a.H : a.W) + KW * WPB - 1) / (KW * WPB);   // KW = WPB = 1: one line per block
     const int per_pair = ngroups * nchunks;
     const int b = blk / per_pair;
     const int lc = blk - b * per_pair;
@@ -564,7 +589,10 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     const bool cmaj = !HORIZ && SM_CB_CHUNK_MAJOR_V;
     const int grp = cmaj ? lc % ngroups : lc / nchunks;
     const int chunk = cmaj ? lc / ngroups : lc - grp * nchunks;
-    L.line = grp * KW + L.wv;
+    L.line = grp * KW * WPB + L.wv + wb;
+    // a WPB block's spare waves (past the last column) only zero their rings and pass the barrier
+    const bool spare = WPB > 1 && L.line >= (HORIZ ? a.H : a.W);
+    if (spare) L.line = (HORIZ ? a.H : a.W) - 1;
     L.active = true;
     if (KW > 1 && L.line >= (HORIZ ? a.H : a.W)) {   // spare wave: runs column W - 1, stores nothing
         L.active = false;
@@ -621,11 +649,13 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         }
     }
     const int ring_words = cbca_ring_words(a.lag, HORIZ, MODE, KW);
-    float* const mine = KW > 1 ? smem + (size_t)L.wv * ring_words : smem;   // this wave's rings
+    // this wave's rings (WPB blocks: each wave's rings + window words)
+    float* const mine = KW > 1 ? smem + (size_t)L.wv * ring_words
+                               : (WPB > 1 ? smem + (size_t)wb * cbca_smem_words(a.lag, HORIZ, MODE) : smem);
     L.r1 = mine;
     L.r2 = mine + (size_t)L.ring * 64;
     L.ra = (uint16_t*)(mine + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
-    L.wown = (uint32_t*)(smem + ring_words);
+    L.wown = (uint32_t*)((KW > 1 ? smem : mine) + ring_words);
     L.wspan = L.wown + NSETS * T;
     L.scale = a.scale;
     {   // zero the rings: reads of positions before the line start then yield S = 0, area = 0
@@ -661,6 +691,7 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         }
     }
     __syncthreads();  // orders the float ring stores before the u16 ring reads (and across waves)
+    if (spare) return;   // WPB blocks have no later barrier
     L.S1 = L.S2 = 0.f;
     L.Acc = 0;
     L.ws = 0;
@@ -723,41 +754,41 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     }
 }
 
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, bool PERSIST>
-__global__ __launch_bounds__(64 * KW) void k_cbca(const CbcaArgs a, const int nlines) {
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, bool PERSIST, int WPB>
+__global__ __launch_bounds__(64 * KW * WPB) void k_cbca(const CbcaArgs a, const int nlines) {
     extern __shared__ float smem[];
     const int slot = xcd_swizzle(blockIdx.x, gridDim.x);   // neighbouring lines on one XCD
     if (!PERSIST) {
-        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW>(a, slot, smem);
+        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW, WPB>(a, slot, smem);
         return;
     }
     for (int blk = slot; blk < nlines; blk += gridDim.x) {   // every block exits after its last line
-        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW>(a, blk, smem);
+        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW, WPB>(a, blk, smem);
         __syncthreads();   // the next line's ring zeroing follows this line's last ring reads
     }
 }
 
-template <bool HORIZ, int MODE, bool SCALE, int KW>
+template <bool HORIZ, int MODE, bool SCALE, int KW, int WPB = 1>
 static void launch_kw(const CbcaArgs& a, int n, hipStream_t st) {
     const int nchunks = (a.D + 63) / 64;
-    const int groups = ((HORIZ ? a.H : a.W) + KW - 1) / KW;
+    const int groups = ((HORIZ ? a.H : a.W) + KW * WPB - 1) / (KW * WPB);
     const int nlines = groups * nchunks * n;
-    const size_t shm = 4 * (size_t)(KW > 1 ? cbca_smem_words_vg(a.lag, MODE, KW) : cbca_smem_words(a.lag, HORIZ, MODE));
+    const size_t shm = 4 * (size_t)(KW > 1 ? cbca_smem_words_vg(a.lag, MODE, KW) : WPB * cbca_smem_words(a.lag, HORIZ, MODE));
     const bool full = a.D % 64 == 0;
-    constexpr bool PERSIST = !HORIZ && KW == 1 && SM_CB_PERSIST_V;
+    constexpr bool PERSIST = !HORIZ && KW == 1 && WPB == 1 && SM_CB_PERSIST_V;
     int nblk = nlines;
     if (PERSIST) {
         // resident blocks: LDS-bound (160 KiB per CU), at most 8 waves per CU
         const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / std::max<size_t>(shm, 1))));
         nblk = std::min(nlines, per_cu * a.num_cu);
     }
-    dim3 grid(nblk);
+    dim3 grid(nblk), block(64 * KW * WPB);
     if (a.view == 0) {
-        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, false, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
-        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, false, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
+        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, false, KW, PERSIST, WPB>), grid, block, shm, st, a, nlines);
+        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, false, KW, PERSIST, WPB>), grid, block, shm, st, a, nlines);
     } else {
-        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, true, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
-        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, true, KW, PERSIST>), grid, dim3(64 * KW), shm, st, a, nlines);
+        if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, true, KW, PERSIST, WPB>), grid, block, shm, st, a, nlines);
+        else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, true, KW, PERSIST, WPB>), grid, block, shm, st, a, nlines);
     }
 }
 
@@ -767,6 +798,11 @@ static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
     if constexpr (KW > 1) {
         // the group's rings and staging must fit one CU's 160 KiB of LDS (lag <= 34 does)
         if (4 * (size_t)cbca_smem_words_vg(a.lag, MODE, KW) <= 160 * 1024) return launch_kw<HORIZ, MODE, SCALE, KW>(a, n, st);
+    }
+    constexpr int WPB = cbca_wpb(HORIZ, MODE);
+    if constexpr (WPB > 1) {
+        // WPB waves' rings must fit one CU's 160 KiB of LDS (else one wave per block)
+        if (4 * (size_t)WPB * cbca_smem_words(a.lag, HORIZ, MODE) <= 160 * 1024) return launch_kw<HORIZ, MODE, SCALE, 1, WPB>(a, n, st);
     }
     launch_kw<HORIZ, MODE, SCALE, 1>(a, n, st);
 }

@@ -109,7 +109,10 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #define SM_CB_V_READLANE 1
 #endif
 #ifndef SM_CB_PROBE_NOVG
-#define SM_CB_PROBE_NOVG 0   // timing probes only (wrong results): V sweeps skip the other image's arm gather (1) or gather row 0 every time (2)
+// Timing probes only (wrong results; DESIGN §5 "What the V gathers cost"): V sweeps skip the other
+// image's arm gathers (1), gather row 0 every time (2), gather columns 0..63 of the right rows (3),
+// gather 16 distinct words (4), skip v_norm's second-set gather (5), 5 with padded rings (6).
+#define SM_CB_PROBE_NOVG 0
 #endif
 #ifndef SM_CB_VG_AUX
 #define SM_CB_VG_AUX 0       // cache policy bits of the V sweeps' arm gathers (tuning)
@@ -193,7 +196,8 @@ __host__ __device__ inline int cbca_ring_words(int lag, bool horiz, int mode, in
     const int ring = cbca_ring(lag, horiz, mode, kw);
     const int floats = mode == CB_NORM_SCAN ? 2 : 1;
     const int u16s = mode == CB_SCAN ? 0 : 1;
-    return ring * 64 * floats + ring * 32 * u16s;
+    // (SM_CB_PROBE_NOVG == 6: timing probe, a further 2 bytes per slot and lane in normalising sweeps)
+    return ring * 64 * floats + ring * 32 * u16s + (SM_CB_PROBE_NOVG == 6 && mode == CB_NORM ? ring * 32 : 0);
 }
 __host__ __device__ inline int cbca_win_words(bool horiz, int mode) {
     if (!SM_CB_LDS_WIN) return 0;
@@ -351,7 +355,9 @@ struct CbLine {
 #pragma unroll
                 for (int k = 0; k < T; k++)
                     t.a1[s][k] = SM_CB_PROBE_NOVG == 1 ? 0x00110011u
-                                                       : __builtin_amdgcn_raw_buffer_load_b32(ra1, (int)(SM_CB_PROBE_NOVG == 2 ? ao[0] : ao[k]), 0, SM_CB_VG_AUX);
+                               : ((SM_CB_PROBE_NOVG == 5 || SM_CB_PROBE_NOVG == 6) && s == 1)
+                                   ? t.a1[0][k] ^ 0x00010001u   // probe: the second set's gather skipped
+                                   : __builtin_amdgcn_raw_buffer_load_b32(ra1, (int)(SM_CB_PROBE_NOVG == 2 ? ao[0] : ao[k]), 0, SM_CB_VG_AUX);
             }
         }
     }
@@ -630,8 +636,15 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         // other image's column: u - d (left view) or u + d (right view); lanes whose column lies
         // outside the image get an out-of-range offset, so their gathers return the reference's
         // zeroed intersection (cpp:2794-2845) without a mask per position
-        const bool out = RV ? L.line + dl >= a.W : L.line - dl < 0;
-        const uint32_t col = (uint32_t)(RV ? L.line + dl : L.line - dl) * 4u;
+        bool out = RV ? L.line + dl >= a.W : L.line - dl < 0;
+        uint32_t col = (uint32_t)(RV ? L.line + dl : L.line - dl) * 4u;
+        if (SM_CB_PROBE_NOVG == 3) {   // timing probe: every wave gathers columns 0..63 of the right rows
+            out = false;
+            col = (uint32_t)L.lane * 4u;
+        } else if (SM_CB_PROBE_NOVG == 4) {   // timing probe: 16 distinct words per gather (lane & 15)
+            out = L.line - (chunk * 64 + (L.lane & 15)) < 0;
+            col = (uint32_t)(L.line - (chunk * 64 + (L.lane & 15))) * 4u;
+        }
 #pragma unroll
         for (int k = 0; k < (HORIZ ? 1 : T); k++) L.ao[k] = out ? 0x80000000u : col + (uint32_t)(k * a.W * 4);
     }

@@ -57,10 +57,12 @@ class DistributedBatchRunner:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
-        # RCCL moves device tensors; gloo host tensors
+        backend = dist.get_backend(group) if dist.is_initialized() else None
+        # RCCL moves device tensors, gloo host tensors; a single process with a GPU keeps the
+        # blocks on the device too (one host-to-device copy in, one device-to-host copy out)
+        on_gpu = backend == "nccl" or (backend is None and torch.cuda.is_available())
         self.device = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
-                                                         if backend == "nccl" else torch.device("cpu"))
+                                                         if on_gpu else torch.device("cpu"))
 
     def _bcast_header(self, header: Optional[list]) -> list:
         t = torch.zeros(6, dtype=torch.float64, device=self.device)
@@ -95,7 +97,7 @@ class DistributedBatchRunner:
             if self.world > 1:
                 dist.scatter(recv, chunks, src=0, group=self.group)
             else:
-                recv.copy_(chunks[0])
+                recv = chunks[0]   # one rank: the block is rank 0's own copy
             block[k] = recv
         lo, hi, _ = shard_bounds(n, self.world, self.rank)
         mine = hi - lo
@@ -108,11 +110,10 @@ class DistributedBatchRunner:
             out[:mine] = res if isinstance(res, torch.Tensor) else torch.from_numpy(res).to(self.device)
         # gather the disparity maps to rank 0 (moved as bytes: gloo has no int16 collectives)
         raw = out.view(torch.uint8)
-        if self.world > 1:
-            gl = [torch.empty_like(raw) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(raw, gl, dst=0, group=self.group)
-        else:
-            gl = [raw]
+        if self.world == 1:
+            return out[:n].cpu().numpy()
+        gl = [torch.empty_like(raw) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(raw, gl, dst=0, group=self.group)
         if self.rank != 0:
             return None
         return torch.cat(gl).view(torch.int16)[:n].cpu().numpy()

@@ -44,7 +44,13 @@ def test_runner_single_rank_hip(oracle):
     try:
         runner = DistributedBatchRunner(fn, device=torch.device("cuda", 0))
         got = runner.run(batch, max_disp=md, reg_lambda=0.3)
-        np.testing.assert_array_equal(got, _oracle_maps(oracle, batch, H, W, md))
+        want = _oracle_maps(oracle, batch, H, W, md)
+        np.testing.assert_array_equal(got, want)
+        # one process without torch.distributed: the runner keeps the blocks on the GPU by default
+        default = DistributedBatchRunner(fn)
+        assert default.device.type == "cuda"
+        for _ in range(2):
+            np.testing.assert_array_equal(default.run(batch, max_disp=md, reg_lambda=0.3), want)
     finally:
         fn.close()
 

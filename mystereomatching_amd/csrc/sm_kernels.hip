@@ -572,6 +572,9 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 #ifndef SM_COST_UNROLL
 #define SM_COST_UNROLL 1
 #endif
+#ifndef SM_COST_ND
+#define SM_COST_ND 1   // D = 128 / 192 / 256: element loop unrolled at compile time (k_cost<..., ND>)
+#endif
 // Pixels of a row segment per block (at most; launch_cost splits a row into equal segments of
 // at most this many): D <= 64 amortises the P + D - 1 moving-pixel staging over up to 240 pixels
 // (Teddy x16, same-process A/B: 128 -> 0.195-0.203 ms, 160 -> 0.186, 192 -> 0.187-0.191, 225 (two
@@ -608,7 +611,9 @@ __host__ __device__ constexpr int cost_rec_u4() { return CW <= 2 ? 1 : 2; }
 // fl(t - e) == t (see above).  Saves the range test, three selects and a min per element.
 constexpr int LUT_T_N = 260;   // >= 128 census bits + icd (<= 128) + 1
 
-template <int METHOD, bool LAM1, int CW, bool ONE, bool OORZ>
+// ND > 0: D == 64 * ND, the element loop fully unrolled (LDS and store offsets become immediates;
+// no loop counter, compare or pointer increments: 35 -> ~29 VALU per element at D = 256)
+template <int METHOD, bool LAM1, int CW, bool ONE, bool OORZ, int ND = 0>
 __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     extern __shared__ __align__(16) unsigned char cs_raw[];
     constexpr int RW = cost_rec_u4<CW>();
@@ -733,8 +738,10 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
             wb = fwb[pl];
         }
         if (ADM) fc = fbgr[pl];
-        auto elem = [&](int d, int q) {                // q = u - sgn * d, the moving position
-            const int mi = q - mbase;                  // staged record (zeros when out of range)
+        // element at staged record mi (moving position q = mbase + mi = u - sgn * d, zeros when out
+        // of range), stored at byte voff + soff of the pixel's row (voff = d * 4 - soff's part)
+        auto elem = [&](int mi, uint32_t voff, uint32_t soff) {
+            const int q = mi + mbase;
             if constexpr (NOSEL) {
                 const uint4 r0 = recA(mi);
                 uint32_t pc, gxm, gym;
@@ -763,7 +770,7 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 const float t = luta[pc];                       // fl(2 - expf(-min(pc, icd) / lamCen))
                 const float ex = expf_glibc_core(fmaxf(xg, -100.0f), etab);
                 const float res = t - ex;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, d * 4, pl * D * 4,
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, voff, soff,
                                                       SM_COST_STORE_AUX);
                 return;
             }
@@ -821,17 +828,27 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 }
             }
 #if SM_COST_PROBE == 2
-            res = (float)d;                              // timing probe: stores only
+            res = (float)mi;                             // timing probe: stores only
 #endif
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, d * 4, pl * D * 4,
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, voff, soff,
                                                   SM_COST_STORE_AUX);
         };
-        if (ONE) {
-            elem(lane, u - sgn * lane);
+        if constexpr (ONE) {
+            elem(u - sgn * lane - mbase, lane * 4, pl * D * 4);
+        } else if constexpr (ND > 0) {
+            // element k takes disparity d = lane + 64 kk with kk = k (left view) or ND - 1 - k (right
+            // view), so that its record index is mil + 64 (ND - 1 - k) in both views: the LDS reads
+            // take non-negative immediate offsets from one per-lane base, the stores a uniform soffset
+            const int mil = (sgn > 0 ? u - lane - 64 * (ND - 1) : u + lane) - mbase;
+#pragma unroll
+            for (int k = 0; k < ND; k++) {
+                const int kk = sgn > 0 ? k : ND - 1 - k;
+                elem(mil + 64 * (ND - 1 - k), lane * 4, (uint32_t)(pl * D * 4 + kk * 256));
+            }
         } else {
             const int qstep = sgn * 64;
             int q = u - sgn * lane;
-            for (int d = lane; d < D; d += 64, q -= qstep) elem(d, q);
+            for (int d = lane; d < D; d += 64, q -= qstep) elem(q - mbase, d * 4, pl * D * 4);
         }
     }
 }
@@ -912,6 +929,14 @@ template <int METHOD, bool LAM1, int CW, bool OORZ>
 static void launch_cost_z(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
     if (a.D <= 64)
         hipLaunchKernelGGL((k_cost<METHOD, LAM1, CW, true, OORZ>), grid, block, shm, st, a);
+#if SM_COST_ND
+    else if (a.D == 256)
+        hipLaunchKernelGGL((k_cost<METHOD, LAM1, CW, false, OORZ, 4>), grid, block, shm, st, a);
+    else if (a.D == 192)
+        hipLaunchKernelGGL((k_cost<METHOD, LAM1, CW, false, OORZ, 3>), grid, block, shm, st, a);
+    else if (a.D == 128)
+        hipLaunchKernelGGL((k_cost<METHOD, LAM1, CW, false, OORZ, 2>), grid, block, shm, st, a);
+#endif
     else
         hipLaunchKernelGGL((k_cost<METHOD, LAM1, CW, false, OORZ>), grid, block, shm, st, a);
 }

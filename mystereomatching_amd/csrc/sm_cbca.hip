@@ -114,6 +114,9 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 // gather 16 distinct words (4), skip v_norm's second-set gather (5), 5 with padded rings (6).
 #define SM_CB_PROBE_NOVG 0
 #endif
+#ifndef SM_CB_ACC_DOT2
+#define SM_CB_ACC_DOT2 1     // area prefix step as v_dot2_u32_u16 (see tile())
+#endif
 #ifndef SM_CB_VG_AUX
 #define SM_CB_VG_AUX 0       // cache policy bits of the V sweeps' arm gathers (tuning)
 #endif
@@ -469,7 +472,13 @@ struct CbLine {
             pi[k] = isect(t, 0, k);
             if (MODE != CB_SCAN) {
                 const uint32_t pp = isect(t, 1, k);
+#if SM_CB_ACC_DOT2
+                // only Acc mod 2^16 is ever read (u16 ring): Acc + pp + 1 adds lo + 1 (and hi << 16),
+                // the dot adds lo + hi exactly; one udot2 + one add instead of shift, add, add3
+                Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
+#else
                 Acc = Acc + (pp & 0xffffu) + (pp >> 16) + 1u;
+#endif
                 wa[k * 64] = (uint16_t)Acc;
             }
             if (MODE == CB_NORM_SCAN) pi2[k] = isect(t, 2, k);

@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--no-parity", action="store_true", help="skip the pair-0 fixture comparison (timing probes)")
+    ap.add_argument("--no-d2h", action="store_true",
+                    help="leave the maps in HBM at the end of a step (default: every timed step ends with the "
+                         "int16 maps in pinned host memory, SURVEY §8d's `disp_out` ready)")
     ap.add_argument("--sub-batch", type=int, default=0, help="sm_params.sub_batch: run the pairs in groups of k")
     ap.add_argument("--streams", type=int, default=1, help="sm_params.num_streams: groups alternate over s streams")
     ap.add_argument("--fuse-norm-scan", action="store_true",
@@ -178,8 +181,17 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
+    # A step ends with the maps on the host (t up to "disp_out ready"): the int16 maps
+    # of the batch are copied into page-locked host memory and the copy is waited for.
+    host_maps = torch.empty((B, H, W), dtype=torch.int16, pin_memory=True).numpy() if not args.no_d2h else None
+
+    def step():
         sb.run(0.3, download=False)
+        if host_maps is not None:
+            sb.download(host_maps)
+
+    for _ in range(args.warmup):
+        step()
     sb.synchronize()
 
     barrier()
@@ -187,7 +199,7 @@ def main():
     sb.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sb.run(0.3, download=False)
+        step()
     sb.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -306,7 +318,9 @@ def main():
             "data": "synthetic (seeded piecewise-planar pairs, mystereomatching_amd/synthetic.py)",
             "config": {"workload": desc, "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": B * world,
                        "sgm_paths": paths, "aggregation": args.agg, "optimization": args.opt, "refine": bool(args.refine),
-                       "parallelism": f"dp{world} (independent pairs, no data-path collective)"},
+                       "parallelism": f"dp{world} (independent pairs, no data-path collective)",
+                       "timed_region": "inputs resident in HBM -> maps in HBM (D2H excluded, --no-d2h)" if args.no_d2h
+                       else "inputs resident in HBM -> int16 maps in pinned host memory (D2H included)"},
             "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "kernels": kern_out,
             "ms_per_step_instrumented": None if ms_prof is None else round(ms_prof, 4),

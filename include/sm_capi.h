@@ -60,9 +60,15 @@ typedef enum sm_cost_method {
 typedef enum sm_aggregation {
     SM_AGG_NONE = 0,
     SM_AGG_CBCA = 1,         /* "CBCA" (main:16; cpp:1002-1003) — default */
-    SM_AGG_GF = 2,           /* "GF"  guideFilter, MY_GUIDE form (cpp:4492-4516, 4975-5104); sgm / WTA only */
+    SM_AGG_GF = 2,           /* "GF"  guideFilter (cpp:4492-4516), form chosen by gf_mode; sgm / WTA only */
     SM_AGG_NL = 3,           /* "NL"  non-local MST tree filter (cpp:4892-4917, NL/NLCCA.cpp:27-96) */
 } sm_aggregation;
+
+/* guideFilter's two builds (stereoMatching.h:38 `//#define MY_GUIDE`): */
+typedef enum sm_gf_mode {
+    SM_GF_XIMGPROC = 0,      /* cv::ximgproc::guidedFilter(I, vm, vm, 9, 1e-4) (cpp:4513) — the shipped build */
+    SM_GF_MY_GUIDE = 1,      /* guideFilterCore_matlab (cpp:4509, 4975-5104) — the MY_GUIDE build */
+} sm_gf_mode;
 
 typedef enum sm_optimization {
     SM_OPT_WTA = 0,          /* "" : WTA only (cpp:1104-1128) */
@@ -73,6 +79,7 @@ typedef enum sm_optimization {
 /* The subset of StereoMatching::Parameters (h:85-351) that the hot path reads, plus the
  * static selectors.  Field defaults come from sm_params_default (= the reference ctor). */
 typedef struct sm_params {
+    uint32_t struct_size;        /* = sizeof(sm_params), set by sm_params_default; sm_create refuses others */
     int32_t rows, cols;          /* h_, w_ */
     int32_t num_disparities;     /* numDisparities = maxDisp + 1 (h:209) */
     int32_t cost_method;         /* sm_cost_method */
@@ -115,7 +122,8 @@ typedef struct sm_params {
                                   * group k + 1 starting once group k's CBCA is done */
     int32_t fuse_norm_scan;      /* 1: CBCA normalising sweep fused with the next scan (measured slower) */
     /* alternative aggregators */
-    float gf_eps;                /* guideFilterCore_matlab eps = 0.0001 (cpp:4509; radius fixed at 9) */
+    float gf_eps;                /* gf_eps[0] = 0.0001 (h:298; radius gf_r[0] = 9, h:297) */
+    int32_t gf_mode;             /* sm_gf_mode: SM_GF_XIMGPROC (default, the shipped build) or SM_GF_MY_GUIDE */
     double nl_sigma;             /* NLCCA sigma = 0.1 (NL/NLCCA.cpp:33): weights exp(-c / (255 sigma)) */
 } sm_params;
 

@@ -219,13 +219,13 @@ class StereoMatching {
         I_mask[0] = nonocc_mask;   // cpp:2073-2075
         I_mask[1] = all_mask;
         I_mask[2] = disc_mask;
-        init(I1_c, I2_c, I1_g, I2_g, hip_device);
+        init_or_release(I1_c, I2_c, I1_g, I2_g, hip_device);
     }
     // without ground truth (no calErr)
     StereoMatching(const Mat& I1_c, const Mat& I2_c, const Mat& I1_g, const Mat& I2_g, const Parameters& param,
                    int hip_device = 0)
         : param_(param), h_(I1_c.rows), w_(I1_c.cols), d_(param.numDisparities) {
-        init(I1_c, I2_c, I1_g, I2_g, hip_device);
+        init_or_release(I1_c, I2_c, I1_g, I2_g, hip_device);
     }
     ~StereoMatching() { sm_destroy(ctx_); }
     StereoMatching(const StereoMatching&) = delete;
@@ -306,6 +306,17 @@ class StereoMatching {
     std::ostringstream csv_;
     std::vector<std::string> times_;
 
+    // a throwing constructor never runs the destructor: release the context (and its device
+    // buffers) here before the exception leaves
+    void init_or_release(const Mat& I1_c, const Mat& I2_c, const Mat& I1_g, const Mat& I2_g, int hip_device) {
+        try {
+            init(I1_c, I2_c, I1_g, I2_g, hip_device);
+        } catch (...) {
+            sm_destroy(ctx_);
+            ctx_ = nullptr;
+            throw;
+        }
+    }
     void init(const Mat& I1_c, const Mat& I2_c, const Mat& I1_g, const Mat& I2_g, int hip_device) {
         const Parameters& param = param_;
         if (I1_c.channels() != 3 || I2_c.channels() != 3 || I1_g.channels() != 1 || I2_g.channels() != 1 ||

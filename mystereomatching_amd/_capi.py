@@ -21,6 +21,7 @@ class sm_params(C.Structure):
     """Mirror of struct sm_params (include/sm_capi.h); field order must match."""
 
     _fields_ = [
+        ("struct_size", C.c_uint32),
         ("rows", C.c_int32), ("cols", C.c_int32), ("num_disparities", C.c_int32),
         ("cost_method", C.c_int32), ("aggregation", C.c_int32), ("optimization", C.c_int32),
         ("census_rv", C.c_int32), ("census_ru", C.c_int32), ("census_ring", C.c_int32),
@@ -39,7 +40,7 @@ class sm_params(C.Structure):
         ("region_vote_nums", C.c_int32), ("rv_ratio", C.c_float), ("rv_s", C.c_int32),
         ("do_proper_ipol", C.c_int32), ("disp_occ", C.c_int32), ("do_last_median_blur", C.c_int32),
         ("sub_batch", C.c_int32), ("num_streams", C.c_int32), ("fuse_norm_scan", C.c_int32),
-        ("gf_eps", C.c_float), ("nl_sigma", C.c_double),
+        ("gf_eps", C.c_float), ("gf_mode", C.c_int32), ("nl_sigma", C.c_double),
     ]
 
 

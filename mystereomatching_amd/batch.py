@@ -47,6 +47,8 @@ def hip_compute_fn(max_disp: int, rows: int, cols: int, capacity: int, device: i
         return sb.download()
 
     run.close = sb.close  # type: ignore[attr-defined]
+    # the runner may hand this function device tensors on its own GPU (no host round trip)
+    run.device = torch.device("cuda", device)  # type: ignore[attr-defined]
     return run
 
 
@@ -55,20 +57,32 @@ class DistributedBatchRunner:
                  group=None):
         self.compute_fn = compute_fn
         self.group = group
+        # with a process group the collectives run even at world size 1 (RCCL on the device
+        # tensors, as on 8 ranks); without one the block is rank 0's own copy
+        self.collective = dist.is_initialized()
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         backend = dist.get_backend(group) if dist.is_initialized() else None
-        # RCCL moves device tensors, gloo host tensors; a single process with a GPU keeps the
-        # blocks on the device too (one host-to-device copy in, one device-to-host copy out)
-        on_gpu = backend == "nccl" or (backend is None and torch.cuda.is_available())
-        self.device = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
-                                                         if on_gpu else torch.device("cpu"))
+        # Blocks live on a GPU only for a compute function that takes device tensors (it says so
+        # with a `device` attribute, as hip_compute_fn does) and then on that function's device:
+        # RCCL needs device tensors, and a single process keeps the blocks on its GPU (one
+        # host-to-device copy in, one device-to-host copy out).  Any other function (numpy-based,
+        # e.g. a CPU reference) gets host arrays, as it does over gloo.
+        fn_dev = getattr(compute_fn, "device", None)
+        if device is not None:
+            self.device = device
+        elif fn_dev is not None and (backend == "nccl" or backend is None):
+            self.device = torch.device(fn_dev)
+        elif backend == "nccl":
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            self.device = torch.device("cpu")
 
     def _bcast_header(self, header: Optional[list]) -> list:
         t = torch.zeros(6, dtype=torch.float64, device=self.device)
         if self.rank == 0:
             t[:] = torch.tensor(header, dtype=torch.float64)
-        if self.world > 1:
+        if self.collective:
             dist.broadcast(t, 0, group=self.group)
         return t.tolist()
 
@@ -94,7 +108,7 @@ class DistributedBatchRunner:
                 if pad:
                     src = torch.cat([src, torch.zeros((pad,) + src.shape[1:], dtype=torch.uint8)])
                 chunks = [c.contiguous().to(self.device) for c in src.split(per)]
-            if self.world > 1:
+            if self.collective:
                 dist.scatter(recv, chunks, src=0, group=self.group)
             else:
                 recv = chunks[0]   # one rank: the block is rank 0's own copy
@@ -104,13 +118,13 @@ class DistributedBatchRunner:
         out = torch.zeros((per, H, W), dtype=torch.int16, device=self.device)
         if mine > 0:
             mine_block = {k: v[:mine] for k, v in block.items()}
-            if self.device.type == "cpu":
-                mine_block = {k: v.numpy() for k, v in mine_block.items()}
+            if self.device.type == "cpu" or getattr(self.compute_fn, "device", None) is None:
+                mine_block = {k: v.cpu().numpy() for k, v in mine_block.items()}
             res = self.compute_fn(mine_block, reg_lambda)
             out[:mine] = res if isinstance(res, torch.Tensor) else torch.from_numpy(res).to(self.device)
         # gather the disparity maps to rank 0 (moved as bytes: gloo has no int16 collectives)
         raw = out.view(torch.uint8)
-        if self.world == 1:
+        if not self.collective:
             return out[:n].cpu().numpy()
         gl = [torch.empty_like(raw) for _ in range(self.world)] if self.rank == 0 else None
         dist.gather(raw, gl, dst=0, group=self.group)

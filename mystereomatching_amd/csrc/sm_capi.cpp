@@ -91,6 +91,7 @@ struct sm_ctx {
     int n_loaded = 0;
     int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized, 5 refined
     float lut_a[1024], lut_b[1024];
+    float* luts = nullptr;      // device copy of lut_a | lut_b (per context: contexts on one device may differ)
     float ad_oor_exp = 0;
     bool fuse_norm_scan = false;
     int num_cu = 256;           // compute units of the device
@@ -196,11 +197,13 @@ sm_status validate(const sm_params& p, std::string& why) {
         // reads outside the image below 2 r + 1); the "so" optimiser's minima assume costs >= 0
         if (p.rows < 19 || p.cols < 19) return bad("aggregation GF needs rows, cols >= 19 (box radius 9)");
         if (p.optimization == SM_OPT_SO) return bad("aggregation GF (costs may be negative) supports optimization sgm or WTA");
+        if (!(p.gf_eps > 0)) return bad("gf_eps must be > 0");
+        if (p.gf_mode != SM_GF_MY_GUIDE) return bad("gf_mode: only 1 (MY_GUIDE) is built so far");
     }
-    if (!(p.gf_eps > 0)) return bad("gf_eps must be > 0");
-    if (!(p.nl_sigma > 0)) return bad("nl_sigma must be > 0");
     if (p.aggregation == SM_AGG_NL) {
-        if (p.rows <= 2 && p.cols <= 2) return bad("aggregation NL needs more than 2 x 2 pixels (qx_mst: no edges)");
+        if (!(p.nl_sigma > 0)) return bad("nl_sigma must be > 0");
+        // ctmf's 3x3 median asserts width >= 3 and height >= 3 (NL/ctmf.c:211-212)
+        if (p.rows < 3 || p.cols < 3) return bad("aggregation NL needs rows, cols >= 3 (ctmf median)");
     }
     if (p.optimization < 0 || p.optimization > 2) return bad("unknown optimization");
     if (p.census_rv < 0 || p.census_ru < 0 || census_len(p) > 128) return bad("census code longer than 128 bits");
@@ -262,7 +265,7 @@ void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
                     c->gf_s, c->gf_planes, c->gf_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
-                    c->nl_table, c->nl_val, c->nl_wsum, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj};
+                    c->nl_table, c->nl_val, c->nl_wsum, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->luts};
     for (void* q : ptrs)
         if (q) hipFree(q);
     if (c->nl_st) {
@@ -401,6 +404,7 @@ sm_status run_cost(sm_ctx* c, int n, int view, const Bufs& B) {
     a.lam2 = p.lam_g;
     a.ad_trunc = p.ad_trunc_ad;
     a.ad_oor_exp = c->ad_oor_exp;
+    a.lut = c->luts;
     const int m = p.cost_method == SM_COST_CENSUS_GRAD ? sm::SM_M_CENSUS_GRAD
                   : p.cost_method == SM_COST_CENSUS    ? sm::SM_M_CENSUS
                   : p.cost_method == SM_COST_AD_CENSUS ? sm::SM_M_AD_CENSUS
@@ -545,7 +549,7 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     if ((int)c->nl_trees.size() < n) c->nl_trees.resize(n);
     std::vector<sm::NlTree>& trees = c->nl_trees;
     if (!c->pool) c->pool.reset(new sm::HostPool(std::max(1, std::min(c->cap, (int)std::thread::hardware_concurrency()))));
-    auto parallel = [&](const std::function<void(int)>& body) { c->pool->run(n, body); };
+    auto parallel = [&](const std::function<void(int)>& body) { return c->pool->run(n, body); };
     const size_t slot = (size_t)c->cap * np;
     auto registered = [&](void* q, size_t bytes) -> bool {
         if (std::find(c->nl_reg.begin(), c->nl_reg.end(), q) != c->nl_reg.end()) return true;
@@ -554,11 +558,12 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
         return true;
     };
     if (trees[n - 1].s_wsum.size() != np) {
-        parallel([&](int b) {
-            trees[b].s_adj.resize(np);
-            trees[b].s_rec.resize(np * 4);
-            trees[b].s_wsum.resize(np);
-        });
+        if (!parallel([&](int b) {
+                trees[b].s_adj.resize(np);
+                trees[b].s_rec.resize(np * 4);
+                trees[b].s_wsum.resize(np);
+            }))
+            return fail(c, SM_ENOMEM, "NL: host tree buffers could not be allocated");
     }
     if (c->nl_tabs_h.size() != 4 * slot) c->nl_tabs_h.resize(4 * slot);
     bool reg_ok = registered(c->nl_tabs_h.data(), 4 * slot * 4);
@@ -577,7 +582,7 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     // offsets are summed between the phases)
     std::vector<char> ok(n, 0);
     std::vector<int> mx((size_t)n * 2, 0);
-    parallel([&](int b) {
+    const bool built = parallel([&](int b) {
         sm::NlTree& t = trees[b];
         ok[b] = sm::nl_tree_from_lists(H, W, t.s_adj.data(), t, c->nl_table_h, b * (int)np, t.s_rec.data(), t.s_wsum.data());
         if (!ok[b]) return;
@@ -594,6 +599,7 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
         mx[2 * b] = (int)t.s_cu.size() - 1;
         mx[2 * b + 1] = (int)t.s_cd.size() - 1;
     });
+    if (!built) return fail(c, SM_ENOMEM, "NL: host tree construction ran out of memory");
     for (int b = 0; b < n; b++)
         if (!ok[b]) return fail(c, SM_EINVAL, "NL: spanning tree construction failed");
     phase("trees");
@@ -634,7 +640,7 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     int* cl = tabs + slot;
     int* ord_up = tabs + 2 * slot;
     int* ord_dn = tabs + 3 * slot;
-    parallel([&](int b) {
+    const bool tabled = parallel([&](int b) {
         const sm::NlTree& t = trees[b];
         const int r0 = b * (int)np, c0 = coff[b];
         int* pu = &cu[(size_t)b * nu];
@@ -647,6 +653,7 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
             ord_dn[pd[t.down_level[k]]++] = g;
         }
     });
+    if (!tabled) return fail(c, SM_ENOMEM, "NL: path tables could not be written");
     phase("records");
     int* I = c->nl_ints;
     int* rec_d = c->nl_rec + sm::NL_REC_PAD * 4;
@@ -831,6 +838,7 @@ extern "C" {
 void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t cols) {
     if (!p) return;
     memset(p, 0, sizeof(*p));
+    p->struct_size = (uint32_t)sizeof(sm_params);
     p->rows = rows;
     p->cols = cols;
     p->num_disparities = max_disp + 1;  // h:209
@@ -874,7 +882,8 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->sub_batch = 0;
     p->num_streams = 1;
     p->fuse_norm_scan = 0;
-    p->gf_eps = 0.0001f;        // guideFilterCore_matlab(I, p, 9, 0.0001) (cpp:4509)
+    p->gf_eps = 0.0001f;        // gf_eps[0] = 1e-4 (h:298; guidedFilter / guideFilterCore_matlab, cpp:4509-4513)
+    p->gf_mode = SM_GF_MY_GUIDE;  // (interim: the ximgproc form is not built yet)
     p->nl_sigma = 0.1;          // NLCCA::aggreCV (NL/NLCCA.cpp:33)
 }
 
@@ -895,6 +904,11 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     sm_ctx* c = new (std::nothrow) sm_ctx();
     if (!c) return SM_ENOMEM;
     *out = c;  // returned even on failure so sm_last_error works; caller must sm_destroy
+    // a struct from another version of sm_capi.h (or not filled by sm_params_default) is refused
+    // before any field past struct_size is read
+    if (p->struct_size != (uint32_t)sizeof(sm_params))
+        return fail(c, SM_EINVAL, "sm_params.struct_size != sizeof(sm_params): initialise the struct with sm_params_default "
+                                  "from this library's sm_capi.h");
     c->p = *p;
     c->device = hip_device;
     if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess || c->num_cu < 1)
@@ -981,7 +995,9 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
             c->xev.push_back(e);
         }
     }
-    HIP_TRY(c, sm::upload_luts(c->lut_a, c->lut_b, c->st));
+    if ((s = dalloc(c, &c->luts, 2048))) return s;
+    HIP_TRY(c, hipMemcpyAsync(c->luts, c->lut_a, sizeof(c->lut_a), hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->luts + 1024, c->lut_b, sizeof(c->lut_b), hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     return SM_OK;
 }

@@ -24,16 +24,20 @@ public:
         for (auto& x : th_) x.join();
     }
     int size() const { return nth_; }
-    // runs f(0 .. n-1) on the workers and returns when every item is done
-    void run(int n, const std::function<void(int)>& f) {
+    // runs f(0 .. n-1) on the workers and returns when every item is done; false if any item
+    // threw (e.g. std::bad_alloc from a resize): the exception stays on its worker, which goes on
+    // with its next item, and the caller reports a status instead of the process terminating
+    bool run(int n, const std::function<void(int)>& f) {
         std::unique_lock<std::mutex> g(m_);
         job_ = &f;
         n_ = n;
         pending_ = nth_;
+        failed_ = false;
         gen_++;
         cv_.notify_all();
         done_.wait(g, [this] { return pending_ == 0; });
         job_ = nullptr;
+        return !failed_;
     }
 
 private:
@@ -50,9 +54,17 @@ private:
                 f = job_;
                 n = n_;
             }
-            for (int b = t; b < n; b += nth_) (*f)(b);
+            bool bad = false;
+            for (int b = t; b < n; b += nth_) {
+                try {
+                    (*f)(b);
+                } catch (...) {
+                    bad = true;
+                }
+            }
             {
                 std::lock_guard<std::mutex> g(m_);
+                failed_ = failed_ || bad;
                 if (--pending_ == 0) done_.notify_one();
             }
         }
@@ -65,6 +77,7 @@ private:
     int n_ = 0, pending_ = 0;
     long gen_ = 0;
     bool stop_ = false;
+    bool failed_ = false;
 };
 
 }  // namespace sm

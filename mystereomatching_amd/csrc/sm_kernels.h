@@ -45,6 +45,8 @@ struct CostArgs {
     float lam2;                 // lamG
     float ad_trunc;             // "AD" method truncation
     float ad_oor_exp;           // ADCensus: expf(-(trunc)/lamAD) for out-of-range pairs
+    const float* lut;           // the context's exponent tables [2][1024]: expf(-x / lam) of the
+                                // census (or AD-census census) term, then the ADCensus AD term
 };
 
 struct CbcaArgs {
@@ -140,7 +142,6 @@ struct PyrArgs {                // SolveAll over PY_LVL pyramid levels (sm_pyram
     int levels, n;
 };
 
-hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st);
 void launch_cost(const CostArgs& a, int method, int n, hipStream_t st);
 void launch_prep(const PrepArgs& a, int n, hipStream_t st);
 size_t prep_smem_bytes(int rv, int ru, int L_out);

@@ -22,8 +22,6 @@
 namespace sm {
 
 __constant__ uint64_t c_exp_tab[32] = SM_EXPF_TABLE;
-__constant__ float c_lut_a[1024];   // expf(-x/lam) for integer-valued costs (census / AD)
-__constant__ float c_lut_b[1024];
 
 __device__ inline float dev_expf(float x) { return expf_glibc(x, c_exp_tab); }
 
@@ -658,11 +656,11 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     const int icd = (int)cd;                        // (int)fminf(pc, cd) == min(pc, (int)cd) for integer pc >= 0
     if (GRAD && tid < 32) etab[tid] = c_exp_tab[tid];
     if (NOSEL)   // luta's region (LUT_A_N + LUT_B_N floats) holds the clamped 2 - e0 table
-        for (int i = tid; i < LUT_T_N; i += 256) luta[i] = 2.0f - c_lut_a[min(i, icd)];
+        for (int i = tid; i < LUT_T_N; i += 256) luta[i] = 2.0f - a.lut[min(i, icd)];
     else if (CEN)
-        for (int i = tid; i < LUT_A_N; i += 256) luta[i] = c_lut_a[i];
+        for (int i = tid; i < LUT_A_N; i += 256) luta[i] = a.lut[i];
     if (METHOD == SM_M_AD_CENSUS)
-        for (int i = tid; i < LUT_B_N; i += 256) lutb[i] = c_lut_b[i];
+        for (int i = tid; i < LUT_B_N; i += 256) lutb[i] = a.lut[1024 + i];
     for (int i = tid; i < np; i += 256) {
         const int u = u0 + i;
         if (CEN) fcode[i] = a.code[frow + u];
@@ -919,12 +917,6 @@ __global__ void k_expf_range(uint32_t first, uint32_t n, float* __restrict__ out
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
-hipError_t upload_luts(const float* lut_a, const float* lut_b, hipStream_t st) {
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut_a), lut_a, sizeof(float) * 1024, 0, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return e;
-    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut_b), lut_b, sizeof(float) * 1024, 0, hipMemcpyHostToDevice, st);
-}
-
 template <int METHOD, bool LAM1, int CW, bool OORZ>
 static void launch_cost_z(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
     if (a.D <= 64)

@@ -594,15 +594,13 @@ static void launch_k(const SgmArgs& a, int mode, int n, hipStream_t st) {
 
 // Lanes-per-line layout for straight paths with D <= SM_SGM_VEC_MIN_D.  Measured on MI355X
 // (Teddy x16): faster for the vertical paths and the last (WTA) path, slower for the middle
-// horizontal one, whose K = 1 sweep already streams whole rows.  SM_SGM_ROWS = bit mask over
-// path indices (tuning).  Larger D runs every direction one line per wave with dwordx4 lanes
+// horizontal one, whose K = 1 sweep already streams whole rows.  Larger D runs every direction
+// one line per wave with dwordx4 lanes
 // (k_sgm VEC): the four-lines-per-wave layout leaves too few waves in flight there
 // (tools/ubench_sgm.hip, KITTI D = 192: 3.5 TB/s with 4 lines per wave vs 5.0 TB/s with one).
 static int rows_kv(const SgmArgs& a, int mode) {
-    static const int mask = [] { const char* e = getenv("SM_SGM_ROWS"); return e ? (int)strtol(e, nullptr, 0) : -1; }();
     if ((a.rv != 0 && a.ru != 0) || a.D % 4 != 0 || a.D > SM_SGM_VEC_MIN_D) return 0;
-    const bool use = mask >= 0 ? ((mask >> a.dir) & 1) : (a.ru == 0 || (mode & SGM_LAST));
-    if (!use) return 0;
+    if (!(a.ru == 0 || (mode & SGM_LAST))) return 0;
     const int K = (a.D + 15) / 16;
     return (K + 3) / 4;
 }

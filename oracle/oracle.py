@@ -34,7 +34,7 @@ class Config(C.Structure):
         ("do_refine", C.c_int), ("lr_max_diff", C.c_float), ("do_region_vote", C.c_int),
         ("region_vote_nums", C.c_int), ("rv_ratio", C.c_float), ("rv_s", C.c_int),
         ("do_proper_ipol", C.c_int), ("disp_occ", C.c_int), ("do_last_median", C.c_int),
-        ("gf_r", C.c_int), ("gf_eps", C.c_float), ("nl_sigma", C.c_double),
+        ("gf_r", C.c_int), ("gf_eps", C.c_float), ("nl_sigma", C.c_double), ("gf_mode", C.c_int),
     ]
 
 
@@ -86,6 +86,9 @@ def load():
         lib.smo_bad_ratio.restype = C.c_float
         lib.smo_expf_range.argtypes = [C.c_uint32, C.c_uint32, P]
         lib.smo_box_filter.argtypes = [C.c_int, C.c_int, C.c_int, P, P, P]
+        lib.smo_box_filter_cv.argtypes = [C.c_int, C.c_int, C.c_int, P, P, P]
+        lib.smo_reflect.argtypes = [C.c_int, C.c_int]
+        lib.smo_reflect.restype = C.c_int
         lib.smo_guided_filter.argtypes = [C.POINTER(Config), P, P]
         lib.smo_guided_filter.restype = C.c_int
         lib.smo_nl_median3.argtypes = [C.c_int, C.c_int, P, P]
@@ -269,8 +272,18 @@ def box_filter(img: np.ndarray, r: int) -> np.ndarray:
     return out
 
 
+def box_filter_cv(img: np.ndarray, r: int) -> np.ndarray:
+    """OpenCV boxFilter (normalised, BORDER_REFLECT, double running sums) of a float32 H x W image."""
+    a = np.ascontiguousarray(img, np.float32)
+    H, W = a.shape
+    out, rs = np.empty_like(a), np.empty((H, W), np.float64)
+    load().smo_box_filter_cv(H, W, r, _p(a), _p(out), _p(rs))
+    return out
+
+
 def guided_filter(vm: np.ndarray, bgr: np.ndarray, cfg: Config) -> np.ndarray:
-    """guideFilterCore_matlab over every slice of an H x W x D volume (MY_GUIDE form of GF)."""
+    """guideFilter on every slice of an H x W x D volume: cfg.gf_mode 0 = ximgproc::guidedFilter
+    (the shipped build), 1 = guideFilterCore_matlab (the MY_GUIDE build)."""
     out = np.ascontiguousarray(vm, np.float32).copy()
     if load().smo_guided_filter(C.byref(cfg), _p(out), _p(np.ascontiguousarray(bgr, np.uint8))) != 0:
         raise ValueError("guided filter needs H, W >= 2 r + 1")

@@ -70,8 +70,9 @@ void smo_default_config(smo_config* c, int maxdisp, int H, int W) {
     c->do_proper_ipol = 1;       /* Do_properIpol (h:76) */
     c->disp_occ = -2 * 16;       /* DISP_OCC (h:216) */
     c->do_last_median = 1;       /* Do_lastMedianBlur (h:80) */
-    c->gf_r = 9;                 /* guideFilterCore_matlab(I[i], guideVm[i][d], 9, 0.0001) (cpp:4509) */
+    c->gf_r = 9;                 /* gf_r[0] = 9, gf_eps[0] = 0.0001 (h:297-298) */
     c->gf_eps = 0.0001f;
+    c->gf_mode = 0;              /* `//#define MY_GUIDE` (h:38): the shipped build calls ximgproc::guidedFilter */
     c->nl_sigma = 0.1;           /* NLCCA::aggreCV (NL/NLCCA.cpp:33) */
 }
 

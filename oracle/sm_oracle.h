@@ -59,16 +59,24 @@ typedef struct smo_config {
     int disp_occ;                /* DISP_OCC = -2 * 16 (h:216) */
     int do_last_median;          /* Do_lastMedianBlur = 1 (h:80) */
     /* alternative aggregators (sm_oracle_agg.c): aggregation 2 = "GF", 3 = "NL" */
-    int gf_r;                    /* guideFilterCore_matlab(I, p, 9, 0.0001) (cpp:4509) */
-    float gf_eps;
+    int gf_r;                    /* gf_r[0] = 9 (h:297) */
+    float gf_eps;                /* gf_eps[0] = 0.0001 (h:298) */
     double nl_sigma;             /* NLCCA::aggreCV sigma = 0.1 (NL/NLCCA.cpp:33) */
+    int gf_mode;                 /* 0: ximgproc::guidedFilter (cpp:4513, the shipped build), 1: MY_GUIDE (cpp:4509) */
 } smo_config;
 
 void smo_default_config(smo_config* c, int maxdisp, int H, int W);
 
 /* sm_oracle_agg.c */
 void smo_box_filter(int H, int W, int r, const float* src, float* dst, float* tmp);
-int smo_guided_filter(const smo_config* c, float* vm, const uint8_t* bgr);
+int smo_guided_filter(const smo_config* c, float* vm, const uint8_t* bgr);   /* dispatches on gf_mode */
+int smo_guided_filter_my(const smo_config* c, float* vm, const uint8_t* bgr);
+int smo_guided_filter_cv(const smo_config* c, float* vm, const uint8_t* bgr);
+/* OpenCV boxFilter(src, dst, CV_32F, (2r+1)^2, normalize, BORDER_REFLECT) of a float image (ximgproc's
+ * meanFilter): RowSum<float, double> then ColumnSum<double, float>.  rs: H*W doubles of scratch. */
+void smo_box_filter_cv(int H, int W, int r, const float* src, float* dst, double* rs);
+/* OpenCV borderInterpolate(BORDER_REFLECT). */
+int smo_reflect(int p, int len);
 void smo_nl_median3(int H, int W, const uint8_t* src, uint8_t* dst);
 int smo_nl_tree(int H, int W, const uint8_t* bgr, int* order, int* parent, uint8_t* weight, int* nchild, int* child);
 void smo_nl_table(double sigma, double* table);

@@ -2,13 +2,25 @@
  * sm_oracle_agg.c — CPU restatement of the reference's alternative aggregators.
  * TEST INFRASTRUCTURE ONLY (see sm_oracle.h); PARITY UNPINNED.
  *
- *  "GF"  guideFilter (stereoMatching.cpp:4492-4516) in its MY_GUIDE form: per disparity slice
- *        guideFilterCore_matlab (cpp:4975-5104), the colour guided filter of He et al. with the
- *        reference's own O(1) BoxFilter / CumSum (cpp:5107-5202), r = 9, eps = 0.0001.  The
- *        shipped build instead calls opencv_contrib's ximgproc::guidedFilter (cpp:4513), which
- *        is absent here; its borders (OpenCV boxFilter, BORDER_REFLECT_101, normalised) differ
- *        from the MY_GUIDE form's cumulative-sum borders, so only the MY_GUIDE form can be
- *        restated from the reference's own text.
+ *  "GF"  guideFilter (stereoMatching.cpp:4492-4516), r = gf_r[0] = 9, eps = gf_eps[0] = 1e-4
+ *        (h:297-298), guide = the view's BGR image as float (gf_channel_isColor, h:301), in two forms:
+ *        gf_mode 0 — the shipped build (`//#define MY_GUIDE`, h:38): opencv_contrib's
+ *          cv::ximgproc::guidedFilter(I, vm, vm, 9, 1e-4) (cpp:4513).  opencv_contrib is a
+ *          third-party dependency absent from /root/reference (version unpinned: the reference has
+ *          no build files).  Restated from its published algorithm (He et al., "Guided Image
+ *          Filtering", colour guide) in the structure of ximgproc's GuidedFilterImpl
+ *          (modules/ximgproc/src/guided_filter.cpp): every mean is meanFilter =
+ *          boxFilter(CV_32F, (2r+1)^2, normalize, BORDER_REFLECT), i.e. OpenCV's generic
+ *          RowSum<float, double> running row sums then ColumnSum<double, float> running column sums
+ *          scaled by 1 / (2r+1)^2; the guide covariance Sigma + eps (float, eps added to the
+ *          diagonal) is inverted per pixel by cofactors / det in float; per source channel
+ *          alpha = Sigma^-1 cov(I, p) and beta = mean_p - alpha . mean_I with separate float products
+ *          and sums (the scalar add_mul / sub_mul row helpers), q = mean_beta + mean_alpha . I.
+ *          Assumptions that nothing here can pin (PARITY UNPINNED): the non-IPP, non-SIMD code path
+ *          (IPP's box filter and FMA-based add_mul of SIMD builds round differently), the
+ *          double casts inside RowSum's running update (OpenCV 4.x), the cofactor order.
+ *        gf_mode 1 — the MY_GUIDE build: per disparity slice guideFilterCore_matlab (cpp:4975-5104),
+ *          the same filter with the reference's own O(1) BoxFilter / CumSum (cpp:5107-5202).
  *  "NL"  NL() (cpp:4892-4917) -> NLCCA::aggreCV (NL/NLCCA.cpp:27-96): Qingxiong Yang's non-local
  *        aggregation on a minimum spanning tree of the left colour image (NL/qx_mst_kruskals_image
  *        .cpp: 3x3 ctmf median, 4-neighbour edges weighted by the max channel difference, counting
@@ -60,7 +72,7 @@ void smo_box_filter(int H, int W, int r, const float* src, float* dst, float* tm
 
 /* guideFilterCore_matlab(I, p, r, eps) (cpp:4975-5104) for every slice d of vm (in place),
  * I = the view's colour image as float, channels in BGR order (split of I_c, cpp:4977-4978). */
-int smo_guided_filter(const smo_config* c, float* vm, const uint8_t* bgr) {
+int smo_guided_filter_my(const smo_config* c, float* vm, const uint8_t* bgr) {
     const int H = c->H, W = c->W, D = c->D, r = c->gf_r;
     const float eps = c->gf_eps;
     if (H < 2 * r + 1 || W < 2 * r + 1) return -1;
@@ -164,6 +176,155 @@ int smo_guided_filter(const smo_config* c, float* vm, const uint8_t* bgr) {
     free(buf);
     free(cof);
     return 0;
+}
+
+/* OpenCV borderInterpolate(p, len, BORDER_REFLECT): fedcba|abcdefgh|hgfedcb */
+int smo_reflect(int p, int len) {
+    if (len == 1) return 0;
+    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p - 1 : 2 * len - 1 - p;
+    return p;
+}
+
+/* ximgproc's meanFilter: boxFilter(src, dst, CV_32F, Size(k, k), Point(-1, -1), true,
+ * BORDER_REFLECT), k = 2 r + 1, on a 1-channel float image.  OpenCV's FilterEngine runs
+ * RowSum<float, double> on every border-extended row (running sum: s = sum of the first k,
+ * then s += (double)S[i + k] - (double)S[i]), then ColumnSum<double, float> down the rows (SUM =
+ * sum of the first k - 1 row sums; per output row s0 = SUM + Sp, out = (float)(s0 * scale),
+ * SUM = s0 - Sm), scale = 1.0 / (k * k). */
+void smo_box_filter_cv(int H, int W, int r, const float* src, float* dst, double* rs) {
+    const int k = 2 * r + 1;
+    const double scale = 1. / (k * k);
+    for (int y = 0; y < H; y++) {
+        const float* S = src + (size_t)y * W;
+        double* D = rs + (size_t)y * W;
+        double s = 0;
+        for (int i = 0; i < k; i++) s += (double)S[smo_reflect(i - r, W)];
+        D[0] = s;
+        for (int i = 0; i < W - 1; i++) {
+            s += (double)S[smo_reflect(i + k - r, W)] - (double)S[smo_reflect(i - r, W)];
+            D[i + 1] = s;
+        }
+    }
+    for (int x = 0; x < W; x++) {
+        double SUM = 0;
+        for (int i = 0; i < k - 1; i++) SUM += rs[(size_t)smo_reflect(i - r, H) * W + x];
+        for (int y = 0; y < H; y++) {
+            const double s0 = SUM + rs[(size_t)smo_reflect(y + r, H) * W + x];
+            dst[(size_t)y * W + x] = (float)(s0 * scale);
+            SUM = s0 - rs[(size_t)smo_reflect(y - r, H) * W + x];
+        }
+    }
+}
+
+/* cv::ximgproc::guidedFilter(I, vm, vm, r, eps) (cpp:4513) for every channel d of vm (in place),
+ * I = the view's colour image as float, channels B, G, R.  See the file header for the source of
+ * each step. */
+int smo_guided_filter_cv(const smo_config* c, float* vm, const uint8_t* bgr) {
+    const int H = c->H, W = c->W, D = c->D, r = c->gf_r;
+    const float eps = c->gf_eps;
+    if (H < 1 || W < 1 || r < 0) return -1;
+    const size_t n = (size_t)H * W;
+    float* buf = (float*)malloc(n * 4 * 32);
+    double* rs = (double*)malloc(n * 8);
+    if (!buf || !rs) {
+        free(buf);
+        free(rs);
+        return -1;
+    }
+    float* I[3] = {buf, buf + n, buf + 2 * n};
+    float* mI[3] = {buf + 3 * n, buf + 4 * n, buf + 5 * n};
+    float* inv[6] = {buf + 6 * n, buf + 7 * n, buf + 8 * n, buf + 9 * n, buf + 10 * n, buf + 11 * n};  /* 00 01 02 11 12 22 */
+    float* t = buf + 12 * n;
+    float* p = buf + 13 * n;
+    float* mP = buf + 14 * n;
+    float* cov[3] = {buf + 15 * n, buf + 16 * n, buf + 17 * n};
+    float* al[3] = {buf + 18 * n, buf + 19 * n, buf + 20 * n};
+    float* be = buf + 21 * n;
+    float* sg[6] = {buf + 22 * n, buf + 23 * n, buf + 24 * n, buf + 25 * n, buf + 26 * n, buf + 27 * n};
+    for (size_t i = 0; i < n; i++)
+        for (int ch = 0; ch < 3; ch++) I[ch][i] = (float)bgr[i * 3 + ch];   /* convertTo(CV_32F) */
+    /* init: guideCnMean = meanFilter(guideCn); covars(i, j) = meanFilter(I_i I_j) - m_i m_j,
+     * + eps on the diagonal; covarsInv = cofactors / det */
+    for (int ch = 0; ch < 3; ch++) smo_box_filter_cv(H, W, r, I[ch], mI[ch], rs);
+    int vi = 0;
+    for (int c0 = 0; c0 < 3; c0++)
+        for (int c1 = c0; c1 < 3; c1++, vi++) {
+            for (size_t i = 0; i < n; i++) t[i] = I[c0][i] * I[c1][i];
+            smo_box_filter_cv(H, W, r, t, sg[vi], rs);
+            for (size_t i = 0; i < n; i++) {
+                const float m = mI[c0][i] * mI[c1][i];
+                sg[vi][i] = sg[vi][i] - m;
+                if (c0 == c1) sg[vi][i] = sg[vi][i] + eps;
+            }
+        }
+    for (size_t i = 0; i < n; i++) {
+        const float a00 = sg[0][i], a01 = sg[1][i], a02 = sg[2][i], a11 = sg[3][i], a12 = sg[4][i], a22 = sg[5][i];
+        float b00 = a11 * a22, b01 = a02 * a12, b02 = a01 * a12, b11 = a00 * a22, b12 = a01 * a02, b22 = a00 * a11;
+        float m;
+        m = a12 * a12; b00 = b00 - m;
+        m = a01 * a22; b01 = b01 - m;
+        m = a02 * a11; b02 = b02 - m;
+        m = a02 * a02; b11 = b11 - m;
+        m = a00 * a12; b12 = b12 - m;
+        m = a01 * a01; b22 = b22 - m;
+        float det = a00 * b00;
+        m = a01 * b01; det = det + m;
+        m = a02 * b02; det = det + m;
+        inv[0][i] = b00 / det;
+        inv[1][i] = b01 / det;
+        inv[2][i] = b02 / det;
+        inv[3][i] = b11 / det;
+        inv[4][i] = b12 / det;
+        inv[5][i] = b22 / det;
+    }
+    static const int IX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+    for (int d = 0; d < D; d++) {
+        for (size_t i = 0; i < n; i++) p[i] = vm[i * D + d];
+        smo_box_filter_cv(H, W, r, p, mP, rs);                               /* srcCnMean */
+        for (int ch = 0; ch < 3; ch++) {                                     /* computeCovGuideAndSrc */
+            for (size_t i = 0; i < n; i++) t[i] = p[i] * I[ch][i];
+            smo_box_filter_cv(H, W, r, t, cov[ch], rs);
+            for (size_t i = 0; i < n; i++) {
+                const float m = mP[i] * mI[ch][i];
+                cov[ch][i] = cov[ch][i] - m;
+            }
+        }
+        for (size_t i = 0; i < n; i++) {
+            for (int gi = 0; gi < 3; gi++) {                                 /* alpha = Sigma^-1 cov */
+                float y = inv[IX[gi][0]][i] * cov[0][i];
+                for (int k = 1; k < 3; k++) {
+                    const float m = inv[IX[gi][k]][i] * cov[k][i];
+                    y = y + m;
+                }
+                al[gi][i] = y;
+            }
+            float b = mP[i];                                                 /* beta = mean_p - alpha . mean_I */
+            for (int gi = 0; gi < 3; gi++) {
+                const float m = al[gi][i] * mI[gi][i];
+                b = b - m;
+            }
+            be[i] = b;
+        }
+        smo_box_filter_cv(H, W, r, be, t, rs);                              /* mean beta -> t */
+        for (int gi = 0; gi < 3; gi++) {
+            smo_box_filter_cv(H, W, r, al[gi], cov[gi], rs);                /* mean alpha -> cov */
+        }
+        for (size_t i = 0; i < n; i++) {                                     /* q = mean_beta + mean_alpha . I */
+            float q = t[i];
+            for (int gi = 0; gi < 3; gi++) {
+                const float m = cov[gi][i] * I[gi][i];
+                q = q + m;
+            }
+            vm[i * D + d] = q;
+        }
+    }
+    free(buf);
+    free(rs);
+    return 0;
+}
+
+int smo_guided_filter(const smo_config* c, float* vm, const uint8_t* bgr) {
+    return c->gf_mode == 1 ? smo_guided_filter_my(c, vm, bgr) : smo_guided_filter_cv(c, vm, bgr);
 }
 
 /* ---------------------------------------------------------------------------------------------

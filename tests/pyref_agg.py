@@ -1,5 +1,6 @@
-"""Independent numpy restatement of the GF (MY_GUIDE) and NL aggregators, written from the
-reference text, used to cross-check oracle/sm_oracle_agg.c on small inputs (test infrastructure).
+"""Independent numpy restatement of the GF (MY_GUIDE and ximgproc forms) and NL aggregators, written
+from the reference text (ximgproc: from the published algorithm, see oracle/sm_oracle_agg.c), used to
+cross-check oracle/sm_oracle_agg.c on small inputs (test infrastructure).
 
 GF:  guideFilterCore_matlab (stereoMatching.cpp:4975-5104) with BoxFilter / CumSum
      (cpp:5107-5202), vectorised over the disparity axis in float32 / float64 as written.
@@ -69,6 +70,83 @@ def guided_filter(vm: np.ndarray, bgr: np.ndarray, r: int = 9, eps: float = 1e-4
     q = box_filter(b, r) / NN
     for c in range(3):
         q = q + (box_filter(a[c], r) / NN) * I[c][..., None]
+    return q.astype(F)
+
+
+def _reflect(p: int, n: int) -> int:
+    """OpenCV borderInterpolate(BORDER_REFLECT)."""
+    if n == 1:
+        return 0
+    while p < 0 or p >= n:
+        p = -p - 1 if p < 0 else 2 * n - 1 - p
+    return p
+
+
+def box_filter_cv(a: np.ndarray, r: int) -> np.ndarray:
+    """OpenCV boxFilter(CV_32F, (2r+1)^2, normalize, BORDER_REFLECT) over axes 0 (rows) and 1 (cols),
+    float64 running sums: RowSum (first window, then += S[i+k] - S[i]) and ColumnSum (k-1 rows, then
+    s0 = SUM + Sp, out = float32(s0 * scale), SUM = s0 - Sm)."""
+    a = a.astype(F)
+    H, W = a.shape[:2]
+    k = 2 * r + 1
+    ext = a[:, [_reflect(j - r, W) for j in range(W + 2 * r)]].astype(np.float64)
+    rs = np.empty(a.shape, np.float64)
+    s = np.zeros(a.shape[:1] + a.shape[2:], np.float64)
+    for i in range(k):
+        s = s + ext[:, i]
+    rs[:, 0] = s
+    for i in range(W - 1):
+        s = s + (ext[:, i + k] - ext[:, i])
+        rs[:, i + 1] = s
+    scale = 1.0 / (k * k)
+    out = np.empty(a.shape, F)
+    SUM = np.zeros(a.shape[1:], np.float64)
+    for i in range(k - 1):
+        SUM = SUM + rs[_reflect(i - r, H)]
+    for y in range(H):
+        s0 = SUM + rs[_reflect(y + r, H)]
+        out[y] = (s0 * scale).astype(F)
+        SUM = s0 - rs[_reflect(y - r, H)]
+    return out
+
+
+def guided_filter_cv(vm: np.ndarray, bgr: np.ndarray, r: int = 9, eps: float = 1e-4) -> np.ndarray:
+    """cv::ximgproc::guidedFilter(I = BGR as float, p = every channel of vm, r, eps) in the structure
+    of GuidedFilterImpl (float32 products and sums, the box filter above), written independently of
+    oracle/sm_oracle_agg.c from the same description (its header)."""
+    H, W, D = vm.shape
+    eps = F(eps)
+    I = [bgr[..., c].astype(F) for c in range(3)]
+    mI = [box_filter_cv(I[c], r) for c in range(3)]
+    sig = {}
+    for i in range(3):
+        for j in range(i, 3):
+            v = box_filter_cv(I[i] * I[j], r) - mI[i] * mI[j]
+            sig[i, j] = sig[j, i] = (v + eps) if i == j else v
+    a = sig
+    cof = {(0, 0): a[1, 1] * a[2, 2] - a[1, 2] * a[1, 2], (0, 1): a[0, 2] * a[1, 2] - a[0, 1] * a[2, 2],
+           (0, 2): a[0, 1] * a[1, 2] - a[0, 2] * a[1, 1], (1, 1): a[0, 0] * a[2, 2] - a[0, 2] * a[0, 2],
+           (1, 2): a[0, 1] * a[0, 2] - a[0, 0] * a[1, 2], (2, 2): a[0, 0] * a[1, 1] - a[0, 1] * a[0, 1]}
+    det = (a[0, 0] * cof[0, 0] + a[0, 1] * cof[0, 1]) + a[0, 2] * cof[0, 2]
+    inv = {}
+    for (i, j), v in cof.items():
+        inv[i, j] = inv[j, i] = v / det
+    p = vm.astype(F)
+    e = lambda x: x[..., None]   # noqa: E731
+    mP = box_filter_cv(p, r)
+    cov = [box_filter_cv(p * e(I[c]), r) - mP * e(mI[c]) for c in range(3)]
+    al = []
+    for gi in range(3):
+        y = e(inv[gi, 0]) * cov[0]
+        for k in (1, 2):
+            y = y + e(inv[gi, k]) * cov[k]
+        al.append(y)
+    be = mP
+    for gi in range(3):
+        be = be - al[gi] * e(mI[gi])
+    q = box_filter_cv(be, r)
+    for gi in range(3):
+        q = q + box_filter_cv(al[gi], r) * e(I[gi])
     return q.astype(F)
 
 

@@ -59,6 +59,8 @@ def test_params_struct_layout_and_defaults():
     assert np.float32(p.rv_ratio) == np.float32(0.4)
     assert (p.sub_batch, p.num_streams, p.fuse_norm_scan) == (0, 1, 0)
     assert np.float32(p.gf_eps) == np.float32(1e-4) and p.nl_sigma == 0.1
+    assert p.gf_mode == 1
+    assert p.struct_size == C.sizeof(_capi.sm_params)
 
 
 @pytest.mark.parametrize("field,value,msg", [
@@ -68,8 +70,7 @@ def test_params_struct_layout_and_defaults():
     ("lam_g", -1.0, b"lambda"), ("grad_trunc", -5.0, b"truncation"), ("sgm_p2", -1.0, b"penalties"),
     ("sgm_redu_coeff", -4, b"penalties"), ("sgm_p2", -0.0, b"penalties"), ("sgm_p1", -0.0, b"penalties"),
     ("grad_trunc", -0.0, b"truncation"), ("ad_trunc_ad", -0.0, b"truncation"), ("num_streams", 5, b"num_streams"),
-    ("sub_batch", -1, b"sub_batch"), ("aggregation", 4, b"aggregation"), ("gf_eps", 0.0, b"gf_eps"),
-    ("nl_sigma", 0.0, b"nl_sigma"),
+    ("sub_batch", -1, b"sub_batch"), ("aggregation", 4, b"aggregation"), ("struct_size", 4, b"struct_size"),
 ])
 def test_validation_rejects_before_device(field, value, msg):
     lib = _capi.load()
@@ -140,7 +141,10 @@ def test_run_batch_multi_argument_checks():
 
 
 @pytest.mark.parametrize("over,msg", [(dict(aggregation=2, rows=18), b"GF"), (dict(aggregation=2, optimization=2), b"GF"),
-                                      (dict(aggregation=3, rows=2, cols=2), b"NL")])
+                                      (dict(aggregation=3, rows=2, cols=2), b"NL"), (dict(aggregation=3, rows=2), b"NL"),
+                                      (dict(aggregation=3, cols=2), b"NL"), (dict(aggregation=2, gf_eps=0.0), b"gf_eps"),
+                                      (dict(aggregation=2, gf_mode=2), b"gf_mode"),
+                                      (dict(aggregation=3, nl_sigma=0.0), b"nl_sigma")])
 def test_alternative_aggregator_domain(over, msg):
     lib = _capi.load()
     p = _capi.default_params(15, 32, 32)
@@ -151,5 +155,18 @@ def test_alternative_aggregator_domain(over, msg):
     try:
         assert st == _capi.SM_EINVAL
         assert msg in lib.sm_last_error(ctx)
+    finally:
+        lib.sm_destroy(ctx)
+
+
+def test_aggregator_constants_checked_only_for_their_aggregator():
+    """gf_eps / nl_sigma / gf_mode are read only by GF / NL: a CBCA struct with them zeroed passes
+    validation (here, without a GPU, sm_create then fails at the device, not with EINVAL)."""
+    lib = _capi.load()
+    p = _capi.default_params(15, 32, 32, gf_eps=0.0, nl_sigma=0.0, gf_mode=7)
+    ctx = C.c_void_p()
+    st = lib.sm_create(C.byref(ctx), C.byref(p), 0)
+    try:
+        assert st != _capi.SM_EINVAL, lib.sm_last_error(ctx)
     finally:
         lib.sm_destroy(ctx)

@@ -11,13 +11,22 @@ it against an independent numpy restatement).
 import numpy as np
 import pytest
 
-from mystereomatching_amd import SolveAll, StereoBatch, StereoMatching
+from mystereomatching_amd import SolveAll, StereoBatch, StereoMatching, _capi
 from mystereomatching_amd import synthetic as S
 
 pytestmark = pytest.mark.gpu
 
 KEYS = ("lbgr", "rbgr", "lgray", "rgray")
 AGG = {"GF": 2, "NL": 3}
+
+
+def _gf_mode():
+    """The library's default guideFilter form (sm_params_default): the oracle is configured alike."""
+    return _capi.default_params(15, 32, 32).gf_mode
+
+
+def ocfg(oracle, H, W, md, **kw):
+    return oracle.config(H, W, md, gf_mode=_gf_mode(), **kw)
 
 
 def bits(a):
@@ -40,7 +49,7 @@ def _agg_volume(pair, H, W, md, agg, cost="censusGrad"):
 @pytest.mark.parametrize("H,W,md,idx", [(24, 30, 7, 500), (40, 61, 63, 501), (33, 47, 69, 502), (21, 19, 255, 503)])
 def test_aggregated_volume_bits(oracle, agg, H, W, md, idx):
     pair = S.make_pair(H, W, md + 1, idx)
-    cfg = oracle.config(H, W, md)
+    cfg = ocfg(oracle, H, W, md)
     vm = oracle.cost_volume(pair, cfg)
     want = oracle.guided_filter(vm, pair["lbgr"], cfg) if agg == "GF" else oracle.nl_aggregate(vm, pair["lbgr"], cfg)
     got = _agg_volume(pair, H, W, md, agg)
@@ -59,7 +68,7 @@ def test_batch_maps_match_oracle(oracle, agg, H, W, md, paths, cost):
         got = sb.run(0.3)
     finally:
         sb.close()
-    cfg = oracle.config(H, W, md, cost=cost, aggregation=AGG[agg], sgm_paths=paths)
+    cfg = ocfg(oracle, H, W, md, cost=cost, aggregation=AGG[agg], sgm_paths=paths)
     for i in range(n):
         want = oracle.run({k: batch[k][i] for k in KEYS}, cfg)["disp"]
         np.testing.assert_array_equal(got[i], want)
@@ -78,7 +87,7 @@ def test_with_refine_both_views(oracle, agg):
         got = sb.run(0.3)[0]
     finally:
         sb.close()
-    want = oracle.run(pair, oracle.config(H, W, md, aggregation=AGG[agg], do_refine=1))["disp"]
+    want = oracle.run(pair, ocfg(oracle, H, W, md, aggregation=AGG[agg], do_refine=1))["disp"]
     np.testing.assert_array_equal(got, want)
 
 
@@ -94,7 +103,7 @@ def test_reference_ordered_api_nl(oracle):
         got = sm.dispOptimize()
     finally:
         StereoMatching.aggregation = "CBCA"
-    np.testing.assert_array_equal(got, oracle.run(pair, oracle.config(H, W, md, aggregation=3))["disp"])
+    np.testing.assert_array_equal(got, oracle.run(pair, ocfg(oracle, H, W, md, aggregation=3))["disp"])
 
 
 @pytest.mark.parametrize("agg", ["GF", "NL"])
@@ -108,7 +117,7 @@ def test_teddy_size_maps(oracle, agg):
         got = sb.run(0.3)[0]
     finally:
         sb.close()
-    want = oracle.run(pair, oracle.config(H, W, md, aggregation=AGG[agg]))["disp"]
+    want = oracle.run(pair, ocfg(oracle, H, W, md, aggregation=AGG[agg]))["disp"]
     np.testing.assert_array_equal(got, want)
 
 
@@ -127,7 +136,7 @@ def test_sub_batches_and_streams(oracle, agg, sub_batch, num_streams):
         second = sb.run(0.3)
     finally:
         sb.close()
-    cfg = oracle.config(H, W, md, aggregation=AGG[agg])
+    cfg = ocfg(oracle, H, W, md, aggregation=AGG[agg])
     for i in range(n):
         np.testing.assert_array_equal(first[i], oracle.run({k: batch[k][i] for k in KEYS}, cfg)["disp"])
     np.testing.assert_array_equal(second, first)
@@ -153,7 +162,7 @@ def test_nl_pipelined_calls_and_new_inputs(oracle):
         got_b = sb.download()
     finally:
         sb.close()
-    cfg = oracle.config(H, W, md, aggregation=AGG["NL"])
+    cfg = ocfg(oracle, H, W, md, aggregation=AGG["NL"])
     for i in range(n):
         np.testing.assert_array_equal(got_a[i], oracle.run({k: a[k][i] for k in KEYS}, cfg)["disp"])
         np.testing.assert_array_equal(got_b[i], oracle.run({k: b[k][i] for k in KEYS}, cfg)["disp"])

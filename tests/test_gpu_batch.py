@@ -85,3 +85,47 @@ def test_run_batch_multi_contexts(oracle, n, caps):
     finally:
         for sb in sbs:
             sb.close()
+
+
+def test_runner_numpy_fn_gets_host_arrays(oracle):
+    """A compute function without a `device` attribute (numpy-based) gets host arrays even in a
+    process with a GPU; hip_compute_fn's blocks stay on its own device."""
+    H, W, md, n = 20, 28, 11, 3
+    batch = S.make_batch(n, H, W, md + 1, first_index=420)
+    seen = []
+
+    def fn(block, lam):
+        seen.append(type(block["lgray"]))
+        return _oracle_maps(oracle, block, H, W, md)
+
+    got = DistributedBatchRunner(fn).run(batch, max_disp=md, reg_lambda=0.3)
+    assert seen and all(t is np.ndarray for t in seen)
+    np.testing.assert_array_equal(got, _oracle_maps(oracle, batch, H, W, md))
+
+
+def test_runner_rccl_world_one(oracle):
+    """DistributedBatchRunner over an initialised `nccl` (RCCL) process group of size 1: header
+    broadcast, scatter and gather run as RCCL collectives on device tensors, as on the 8-GPU node
+    (configs[4]); the maps must equal the oracle's."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    H, W, md, n = 30, 52, 15, 3
+    batch = S.make_batch(n, H, W, md + 1, first_index=440)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    fn = hip_compute_fn(md, H, W, n, device=0)
+    try:
+        runner = DistributedBatchRunner(fn)
+        assert runner.collective and runner.device.type == "cuda"
+        want = _oracle_maps(oracle, batch, H, W, md)
+        for _ in range(2):
+            np.testing.assert_array_equal(runner.run(batch, max_disp=md, reg_lambda=0.3), want)
+    finally:
+        fn.close()
+        dist.destroy_process_group()

@@ -90,3 +90,19 @@ def test_reference_ordered_api_matches_oracle_fixture(name):
         StereoMatching.costcalculation, StereoMatching.aggregation, StereoMatching.optimization = sel
     want = z["disp"]
     assert np.array_equal(got, want), _diff_msg(got, want)
+
+
+@pytest.mark.parametrize("name", ["large_fullres_d256", "large_hd1080_d256", "large_teddy_refine_d64"])
+def test_fuse_norm_scan_matches_oracle_fixture(name):
+    """sm_params.fuse_norm_scan = 1 (CB_NORM_SCAN sweeps) at configs[3] / configs[4] size and with
+    Do_refine: the maps must equal the same oracle fixtures as the default sweep sequence."""
+    z, ov = _load(os.path.join(HERE, "golden", name + ".npz"))
+    pair, H, W, md = _pair(z)
+    sb = StereoBatch(md, H, W, 1, device=0, fuse_norm_scan=1, **ov)
+    try:
+        sb.upload(*(pair[k][None] for k in KEYS))
+        got = sb.run(0.3)[0]
+    finally:
+        sb.close()
+    want = z["disp"]
+    assert np.array_equal(got, want), _diff_msg(got, want)

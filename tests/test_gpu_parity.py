@@ -302,3 +302,50 @@ def test_state_errors():
         assert lib.sm_solve_all(ctx, 2, 0.3) == _capi.SM_EINVAL
     finally:
         lib.sm_destroy(ctx)
+
+
+@pytest.mark.parametrize("iters,md", [(1, 40), (2, 40), (3, 70), (4, 130), (2, 255)])
+def test_fuse_norm_scan_volume(oracle, iters, md):
+    """sm_params.fuse_norm_scan = 1: iteration k's normalising sweep and iteration k+1's scan run
+    as one CB_NORM_SCAN sweep (two prefix rings).  The aggregated volume (cbca_core,
+    cpp:5585-5666) and the map must equal the oracle's bit for bit for 1-4 iterations (0-3 fused
+    sweeps, both directions) and D up to 256."""
+    H, W = 37, 61
+    pair = S.make_pair(H, W, md + 1, 500 + iters)
+    cfg = oracle.config(H, W, md, cbca_iters=iters)
+    ref = oracle.run(pair, cfg, dumps=True)
+    lib = _capi.load()
+    p = _capi.default_params(md, H, W, cbca_iterations=iters, fuse_norm_scan=1, keep_final_volume=1)
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        a = {k: np.ascontiguousarray(pair[k]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        _capi.check(lib, ctx, lib.sm_set_images(ctx, _capi.ptr(a["lbgr"]), _capi.ptr(a["rbgr"]), W * 3,
+                                                _capi.ptr(a["lgray"]), _capi.ptr(a["rgray"]), W))
+        _capi.check(lib, ctx, lib.sm_cost_calculate(ctx))
+        got = np.empty((H, W, md + 1), np.float32)
+        _capi.check(lib, ctx, lib.sm_get_volume(ctx, 0, _capi.ptr(got)))
+        np.testing.assert_array_equal(bits(got), bits(ref["agg"]))
+        _capi.check(lib, ctx, lib.sm_solve_all(ctx, 1, 0.3))
+        dp = np.empty((H, W), np.int16)
+        _capi.check(lib, ctx, lib.sm_disp_optimize(ctx, _capi.ptr(dp)))
+        np.testing.assert_array_equal(dp, ref["disp"])
+    finally:
+        lib.sm_destroy(ctx)
+
+
+def test_fuse_norm_scan_batch_and_right_view(oracle):
+    """fuse_norm_scan through sm_run: batched pairs with Do_refine (the right view's CBCA runs the
+    RV instantiation of the fused sweep), maps equal to the oracle's refined maps."""
+    H, W, md, n = 45, 70, 31, 3
+    b = S.make_batch(n, H, W, md + 1, first_index=520)
+    sb = StereoBatch(md, H, W, n, fuse_norm_scan=1, do_refine=1)
+    try:
+        sb.upload(b["lbgr"], b["rbgr"], b["lgray"], b["rgray"])
+        disp = sb.run(0.3)
+    finally:
+        sb.close()
+    cfg = oracle.config(H, W, md, do_refine=1)
+    for i in range(n):
+        pair = {k: b[k][i] for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        np.testing.assert_array_equal(disp[i], oracle.run_ex(pair, cfg)["disp"])

@@ -18,10 +18,44 @@ def test_box_filter_matches_pyref(oracle, H, W, r):
     np.testing.assert_array_equal(bits(oracle.box_filter(img, r)), bits(R.box_filter(img, r)))
 
 
+@pytest.mark.parametrize("H,W,r", [(19, 19, 9), (25, 31, 9), (12, 9, 4), (5, 7, 2), (3, 4, 9), (1, 6, 2)])
+def test_box_filter_cv_matches_pyref(oracle, H, W, r):
+    """OpenCV's normalised box filter (BORDER_REFLECT, double running sums), including images smaller
+    than the window (multiple reflections)."""
+    img = np.random.default_rng(H * W + 7).random((H, W)).astype(np.float32) * 100
+    got = oracle.box_filter_cv(img, r)
+    np.testing.assert_array_equal(bits(got), bits(R.box_filter_cv(img, r)))
+    # against a float64 windowed mean over the reflected image: within a few ulp
+    pad = np.pad(img.astype(np.float64), r, mode="symmetric") if min(H, W) >= r else None
+    if pad is not None:
+        k = 2 * r + 1
+        want = np.lib.stride_tricks.sliding_window_view(pad, (k, k)).mean(axis=(2, 3))
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-4)
+
+
+def test_reflect_border(oracle):
+    """borderInterpolate(BORDER_REFLECT): fedcba|abcdefgh|hgfedcb."""
+    got = [oracle.load().smo_reflect(p, 8) for p in range(-6, 14)]
+    assert got == [5, 4, 3, 2, 1, 0, 0, 1, 2, 3, 4, 5, 6, 7, 7, 6, 5, 4, 3, 2]
+
+
+@pytest.mark.parametrize("H,W,md,idx", [(24, 30, 7, 402), (19, 40, 11, 403), (12, 10, 5, 404)])
+def test_guided_filter_ximgproc_matches_pyref(oracle, H, W, md, idx):
+    """gf_mode 0 (the shipped build's ximgproc::guidedFilter) against the numpy twin."""
+    pair = S.make_pair(H, W, md + 1, idx)
+    cfg = oracle.config(H, W, md, gf_mode=0)
+    vm = oracle.cost_volume(pair, cfg)
+    got = oracle.guided_filter(vm, pair["lbgr"], cfg)
+    np.testing.assert_array_equal(bits(got), bits(R.guided_filter_cv(vm, pair["lbgr"])))
+    # an edge-aware local average: constant slices stay (numerically) constant
+    flat = np.full_like(vm, 0.75)
+    assert np.allclose(oracle.guided_filter(flat, pair["lbgr"], cfg), 0.75, atol=2e-2)
+
+
 @pytest.mark.parametrize("H,W,md,idx", [(24, 30, 7, 400), (19, 40, 11, 401)])
 def test_guided_filter_matches_pyref(oracle, H, W, md, idx):
     pair = S.make_pair(H, W, md + 1, idx)
-    cfg = oracle.config(H, W, md)
+    cfg = oracle.config(H, W, md, gf_mode=1)
     vm = oracle.cost_volume(pair, cfg)
     got = oracle.guided_filter(vm, pair["lbgr"], cfg)
     want = R.guided_filter(vm, pair["lbgr"])
@@ -32,7 +66,7 @@ def test_guided_filter_matches_pyref(oracle, H, W, md, idx):
 
 
 def test_guided_filter_rejects_small_images(oracle):
-    cfg = oracle.config(10, 30, 3)
+    cfg = oracle.config(10, 30, 3, gf_mode=1)
     with pytest.raises(ValueError):
         oracle.guided_filter(np.zeros((10, 30, 4), np.float32), np.zeros((10, 30, 3), np.uint8), cfg)
 

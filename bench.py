@@ -170,7 +170,8 @@ def main():
                      aggregation=args.agg, fuse_norm_scan=int(args.fuse_norm_scan), sub_batch=args.sub_batch,
                      num_streams=args.streams)
     if args.agg != "CBCA":
-        desc = desc.replace("CBCA", args.agg, 1)
+        agg_name = {"GF": "GF (ximgproc::guidedFilter, r 9, eps 1e-4)", "NL": "NL (MST tree filter)"}[args.agg]
+        desc = desc.replace("CBCA(2 it)", agg_name, 1).replace("CBCA", agg_name, 1)
     if args.opt == "so":
         desc = desc.replace("SGM 4-path+WTA", "so (scan-line DP)").replace("SGM 8-path+WTA", "so (scan-line DP)")
     if args.refine:

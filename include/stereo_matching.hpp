@@ -183,6 +183,9 @@ class StereoMatching {
     inline static bool Do_regionVote = true;       // h:75
     inline static bool Do_properIpol = true;       // h:76
     inline static bool Do_lastMedianBlur = true;   // h:80
+    // `#define MY_GUIDE` (h:38, commented out in the shipped build) as a switch: false = GF runs
+    // cv::ximgproc::guidedFilter (cpp:4513), true = guideFilterCore_matlab (cpp:4509)
+    inline static bool gf_my_guide = false;
 
     struct Parameters {  // StereoMatching::Parameters (h:85-351), the fields the hot path reads
         int numDisparities, rows, cols;
@@ -363,6 +366,7 @@ class StereoMatching {
         p.do_region_vote = Do_regionVote ? 1 : 0;
         p.do_proper_ipol = Do_properIpol ? 1 : 0;
         p.do_last_median_blur = Do_lastMedianBlur ? 1 : 0;
+        p.gf_mode = gf_my_guide ? SM_GF_MY_GUIDE : SM_GF_XIMGPROC;
         check(sm_create(&ctx_, &p, hip_device), "sm_create");
         check(sm_set_images(ctx_, I1_c.data, I2_c.data, I1_c.step, I1_g.data, I2_g.data, I1_g.step), "sm_set_images");
     }

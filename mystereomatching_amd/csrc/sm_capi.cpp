@@ -69,6 +69,12 @@ struct sm_ctx {
     float* gf_s = nullptr;      // [3 (+1 without acc)][cap][nvol]
     float* gf_planes = nullptr; // [cap][10][npix]
     sm::GfPix* gf_pix = nullptr;// [cap][npix]
+    // aggregation "GF", ximgproc form: row sums (4 double volumes), alpha / beta (4 float volumes),
+    // image-plane row sums [cap][9][npix] doubles and per-pixel terms [cap][9][npix] floats
+    double* gfc_rs = nullptr;
+    float* gfc_ab = nullptr;
+    double* gfc_img = nullptr;
+    float* gfc_pix = nullptr;
     // aggregation "NL": median image, edge weights, the tree (uploaded per call), filter values
     uint8_t* nl_med = nullptr;  // [cap][npix][3]
     uint8_t* nl_ew = nullptr;   // [cap][ne]
@@ -193,12 +199,18 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (p.cost_method < 0 || p.cost_method > 3) return bad("unknown cost_method");
     if (p.aggregation < 0 || p.aggregation > 3) return bad("unknown aggregation");
     if (p.aggregation == SM_AGG_GF) {
-        // BoxFilter's windows need 2 r + 1 = 19 rows and columns (cpp:5156 asserts only >= r, and
-        // reads outside the image below 2 r + 1); the "so" optimiser's minima assume costs >= 0
-        if (p.rows < 19 || p.cols < 19) return bad("aggregation GF needs rows, cols >= 19 (box radius 9)");
+        if (p.gf_mode != SM_GF_XIMGPROC && p.gf_mode != SM_GF_MY_GUIDE)
+            return bad("gf_mode must be 0 (ximgproc::guidedFilter) or 1 (MY_GUIDE)");
+        // MY_GUIDE: BoxFilter's windows need 2 r + 1 = 19 rows and columns (cpp:5156 asserts only
+        // >= r, and reads outside the image below 2 r + 1); ximgproc: the reflected border of a
+        // radius-9 box needs >= 9 (one reflection)
+        if (p.gf_mode == SM_GF_MY_GUIDE && (p.rows < 19 || p.cols < 19))
+            return bad("aggregation GF (MY_GUIDE) needs rows, cols >= 19 (box radius 9)");
+        if (p.gf_mode == SM_GF_XIMGPROC && (p.rows < 9 || p.cols < 9))
+            return bad("aggregation GF (ximgproc) needs rows, cols >= 9 (box radius 9, reflected border)");
+        // the "so" optimiser's minima assume costs >= 0
         if (p.optimization == SM_OPT_SO) return bad("aggregation GF (costs may be negative) supports optimization sgm or WTA");
         if (!(p.gf_eps > 0)) return bad("gf_eps must be > 0");
-        if (p.gf_mode != SM_GF_MY_GUIDE) return bad("gf_mode: only 1 (MY_GUIDE) is built so far");
     }
     if (p.aggregation == SM_AGG_NL) {
         if (!(p.nl_sigma > 0)) return bad("nl_sigma must be > 0");
@@ -264,7 +276,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
-                    c->gf_s, c->gf_planes, c->gf_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
+                    c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
                     c->nl_table, c->nl_val, c->nl_wsum, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->luts};
     for (void* q : ptrs)
         if (q) hipFree(q);
@@ -468,9 +480,31 @@ sm_status run_scale(sm_ctx* c, int n, int view, float w, const Bufs& B) {
 
 // dispOptimize (cpp:1046-1136) for one view: vm[0] with the left image's penalty flags
 // (leftFirst = true) -> DP[0]; vm[1] with the right image's (leftFirst = false) -> DP[1].
-// guideFilter(0, vm) on one view (cpp:4492-4516), MY_GUIDE form: sm_gf.hip
+// guideFilter(0, vm) on one view (cpp:4492-4516): ximgproc form (the shipped build, sm_gf_cv.hip)
+// or the MY_GUIDE form (sm_gf.hip), by sm_params.gf_mode
 sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B, bool solve_all, float w) {
     const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, cap = c->cap, nv = c->nvol;
+    if (c->p.gf_mode == SM_GF_XIMGPROC) {
+        sm::GfCvArgs a{};
+        a.vm = view == 0 ? B.vm0 : B.vm1;
+        a.rs = c->gfc_rs + off * nv;
+        a.ab = c->gfc_ab + off * nv;
+        a.cap = c->cap;
+        a.px = B.px + (size_t)view * c->npix;        // packed words of the view's image (run_prep)
+        a.px_pair_stride = 2 * c->npix;
+        a.img_rs = c->gfc_img + off * 9 * c->npix;
+        a.pix = c->gfc_pix + off * 9 * c->npix;
+        a.H = c->p.rows;
+        a.W = c->p.cols;
+        a.D = c->p.num_disparities;
+        a.eps = c->p.gf_eps;
+        a.solve_all = solve_all;
+        a.scale = w;
+        // R0: read p, write 4 doubles; C0: read 4 doubles, write 4 floats; R1: read 4 floats, write 4
+        // doubles; C1: read 4 doubles, write q (the leaving rows / positions re-read from cache)
+        const double bytes = (double)n * nv * (4 + 32 + 32 + 16 + 16 + 32 + 32 + 4);
+        return timed(c, view == 0 ? "gf" : "gf_r", bytes, [&] { sm::launch_gf_cv(a, n, c->st); });
+    }
     sm::GfArgs a{};
     a.vm = view == 0 ? B.vm0 : B.vm1;
     float* s0 = c->acc ? c->acc : c->gf_s + 3 * cap * nv;
@@ -883,7 +917,7 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->num_streams = 1;
     p->fuse_norm_scan = 0;
     p->gf_eps = 0.0001f;        // gf_eps[0] = 1e-4 (h:298; guidedFilter / guideFilterCore_matlab, cpp:4509-4513)
-    p->gf_mode = SM_GF_MY_GUIDE;  // (interim: the ximgproc form is not built yet)
+    p->gf_mode = SM_GF_XIMGPROC;  // `//#define MY_GUIDE` (h:38): the shipped build calls ximgproc::guidedFilter
     p->nl_sigma = 0.1;          // NLCCA::aggreCV (NL/NLCCA.cpp:33)
 }
 
@@ -956,7 +990,12 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->disp_tmp, cap * c->npix))) return s;
     }
     if ((s = dalloc(c, &c->px, 3 * cap * 2 * c->npix))) return s;
-    if (p->aggregation == SM_AGG_GF) {
+    if (p->aggregation == SM_AGG_GF && p->gf_mode == SM_GF_XIMGPROC) {
+        if ((s = dalloc(c, &c->gfc_rs, 4 * cap * c->nvol))) return s;
+        if ((s = dalloc(c, &c->gfc_ab, 4 * cap * c->nvol))) return s;
+        if ((s = dalloc(c, &c->gfc_img, cap * 9 * c->npix))) return s;
+        if ((s = dalloc(c, &c->gfc_pix, cap * 9 * c->npix))) return s;
+    } else if (p->aggregation == SM_AGG_GF) {
         if ((s = dalloc(c, &c->gf_s, (c->acc ? 3 : 4) * cap * c->nvol))) return s;
         if ((s = dalloc(c, &c->gf_planes, cap * 10 * c->npix))) return s;
         if ((s = dalloc(c, &c->gf_pix, cap * c->npix))) return s;

@@ -100,6 +100,22 @@ struct GfArgs {
 };
 void launch_gf(const GfArgs& a, int n, hipStream_t st);
 
+struct GfCvArgs {               // guided filter, ximgproc form (sm_gf_cv.hip); pair-relative bases
+    float* vm;                  // [n][H][W][D], filtered in place
+    double* rs;                 // row sums: 4 channel planes, plane c at rs + c * cap * nvol
+    float* ab;                  // alpha_0..2, beta: 4 planes, plane c at ab + c * cap * nvol
+    int cap;                    // pairs per channel plane (the context's batch capacity)
+    const uint32_t* px;         // the view's packed B | G << 8 | R << 16 words of pair 0
+    size_t px_pair_stride;      // words between pairs
+    double* img_rs;             // [n][9][H][W] image-plane row sums
+    float* pix;                 // [n][9][H][W] mean_I (3), Sigma^-1 (6)
+    int H, W, D;
+    float eps;
+    int solve_all;              // 1: the output is SolveAll's `0 + w * q` (cpp:2189-2201), w = scale
+    float scale;
+};
+void launch_gf_cv(const GfCvArgs& a, int n, hipStream_t st);
+
 struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids = pair * H W + pixel
     const int4* rec;            // path nodes, each path bottom -> top: {x, meta, child weights, parent}
                                 //   meta = nchild | (heavy + 1) << 3 | child directions << 6 (2 bits

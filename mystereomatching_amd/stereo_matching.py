@@ -36,6 +36,9 @@ class StereoMatching:
     # are read when an object is constructed (set StereoMatching.Do_refine = True before it)
     Do_refine = False
     Do_LRConsis = True
+    # `#define MY_GUIDE` (h:38, commented out in the shipped build): guideFilter's form, False =
+    # cv::ximgproc::guidedFilter (cpp:4513), True = guideFilterCore_matlab (cpp:4509)
+    MY_GUIDE = False
     Do_regionVote = True
     Do_properIpol = True
     Do_lastMedianBlur = True
@@ -76,7 +79,7 @@ class StereoMatching:
 
         def to_c(self, cost: str, aggregation: str, optimization: str, batch: int = 1,
                  compute_right_view: bool = False, keep_final_volume: bool = False,
-                 do_refine: bool = False, switches=(True, True, True)) -> _capi.sm_params:
+                 do_refine: bool = False, switches=(True, True, True), my_guide: bool = False) -> _capi.sm_params:
             if self.censusFunc not in (0, 3):
                 raise ValueError("censusFunc must be 0 (plain census) or 3 (census + ring bits)")
             p = _capi.default_params(self.numDisparities - 1, self.rows, self.cols)
@@ -104,6 +107,7 @@ class StereoMatching:
             p.region_vote_nums = int(self.region_vote_nums)
             p.rv_ratio, p.rv_s = float(self.rv_ratio), int(self.rv_s)
             p.do_region_vote, p.do_proper_ipol, p.do_last_median_blur = (int(x) for x in switches)
+            p.gf_mode = 1 if my_guide else 0
             return p
 
     def __init__(self, I1_c, I2_c, I1_g, I2_g, DT=None, all_mask=None, nonocc_mask=None, disc_mask=None,
@@ -128,7 +132,7 @@ class StereoMatching:
         self._lib = _capi.load()
         if self.Do_refine and not self.Do_LRConsis:
             raise ValueError("Do_refine needs Do_LRConsis (refine() starts with the LR check, cpp:1364)")
-        p = param.to_c(self.costcalculation, self.aggregation, self.optimization,
+        p = param.to_c(self.costcalculation, self.aggregation, self.optimization, my_guide=self.MY_GUIDE,
                        compute_right_view=self.Do_LRConsis and self.Do_refine,
                        keep_final_volume=keep_final_volume, do_refine=self.Do_refine,
                        switches=(self.Do_regionVote, self.Do_properIpol, self.Do_lastMedianBlur))

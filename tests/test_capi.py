@@ -59,7 +59,7 @@ def test_params_struct_layout_and_defaults():
     assert np.float32(p.rv_ratio) == np.float32(0.4)
     assert (p.sub_batch, p.num_streams, p.fuse_norm_scan) == (0, 1, 0)
     assert np.float32(p.gf_eps) == np.float32(1e-4) and p.nl_sigma == 0.1
-    assert p.gf_mode == 1
+    assert p.gf_mode == 0   # SM_GF_XIMGPROC: the shipped build (`//#define MY_GUIDE`, h:38)
     assert p.struct_size == C.sizeof(_capi.sm_params)
 
 
@@ -140,7 +140,8 @@ def test_run_batch_multi_argument_checks():
     assert lib.sm_run_batch_multi(arr, 1, 0, p, p, p, p, 0.3, C.cast(out, C.c_void_p)) == _capi.SM_EINVAL
 
 
-@pytest.mark.parametrize("over,msg", [(dict(aggregation=2, rows=18), b"GF"), (dict(aggregation=2, optimization=2), b"GF"),
+@pytest.mark.parametrize("over,msg", [(dict(aggregation=2, rows=8), b"GF"), (dict(aggregation=2, gf_mode=1, rows=18), b"GF"),
+                                      (dict(aggregation=2, optimization=2), b"GF"),
                                       (dict(aggregation=3, rows=2, cols=2), b"NL"), (dict(aggregation=3, rows=2), b"NL"),
                                       (dict(aggregation=3, cols=2), b"NL"), (dict(aggregation=2, gf_eps=0.0), b"gf_eps"),
                                       (dict(aggregation=2, gf_mode=2), b"gf_mode"),

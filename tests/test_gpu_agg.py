@@ -1,8 +1,9 @@
 """GPU parity of the alternative aggregators against the CPU restatement, bit for bit.
 
-"GF": guideFilter (stereoMatching.cpp:4492-4516) in its MY_GUIDE form, guideFilterCore_matlab
-(cpp:4975-5104) with the reference's BoxFilter / CumSum (cpp:5107-5202), r = 9, eps = 1e-4;
-its costs can be negative, so SGM runs its float-minimum variant.  "NL": NL() (cpp:4892-4917),
+"GF": guideFilter (stereoMatching.cpp:4492-4516), r = 9, eps = 1e-4, in the shipped build's form
+(cv::ximgproc::guidedFilter, cpp:4513, the default) and the MY_GUIDE form (guideFilterCore_matlab,
+cpp:4975-5104, with the reference's BoxFilter / CumSum, cpp:5107-5202); its costs can be negative,
+so SGM runs its float-minimum variant.  "NL": NL() (cpp:4892-4917),
 the MST tree filter of NL/ (spanning trees by Boruvka rounds on the GPU -- the same tree as the
 reference's Kruskal -- walked on host threads, filter on the GPU).
 PARITY UNPINNED (the oracle restates the reference text; tests/test_oracle_agg.py cross-checks
@@ -54,6 +55,36 @@ def test_aggregated_volume_bits(oracle, agg, H, W, md, idx):
     want = oracle.guided_filter(vm, pair["lbgr"], cfg) if agg == "GF" else oracle.nl_aggregate(vm, pair["lbgr"], cfg)
     got = _agg_volume(pair, H, W, md, agg)
     np.testing.assert_array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("H,W,md,idx", [(24, 30, 7, 540), (40, 61, 63, 541), (19, 23, 255, 542), (9, 12, 20, 543),
+                                        (11, 9, 64, 544), (33, 70, 130, 545)])
+def test_gf_modes_volume_bits(oracle, mode, H, W, md, idx):
+    """Both guideFilter builds through the C ABI: gf_mode 0 = ximgproc::guidedFilter (the shipped
+    build, sm_gf_cv.hip; images down to 9 x 9, the reflected border's minimum) and 1 = MY_GUIDE
+    (sm_gf.hip; 19 x 19 minimum), D up to 256 and ragged, left and right views."""
+    import ctypes as C
+    if mode == 1 and min(H, W) < 19:
+        pytest.skip("MY_GUIDE needs 19 x 19")
+    pair = S.make_pair(H, W, md + 1, idx)
+    cfg = oracle.config(H, W, md, gf_mode=mode)
+    lib = _capi.load()
+    p = _capi.default_params(md, H, W, aggregation=2, optimization=0, gf_mode=mode, do_refine=1)
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        a = {k: np.ascontiguousarray(pair[k]) for k in KEYS}
+        _capi.check(lib, ctx, lib.sm_set_images(ctx, _capi.ptr(a["lbgr"]), _capi.ptr(a["rbgr"]), W * 3,
+                                                _capi.ptr(a["lgray"]), _capi.ptr(a["rgray"]), W))
+        _capi.check(lib, ctx, lib.sm_cost_calculate(ctx))
+        for view, img in ((0, "lbgr"), (1, "rbgr")):
+            got = np.empty((H, W, md + 1), np.float32)
+            _capi.check(lib, ctx, lib.sm_get_volume(ctx, view, _capi.ptr(got)))
+            want = oracle.guided_filter(oracle.cost_volume(pair, cfg, view=view), pair[img], cfg)
+            np.testing.assert_array_equal(bits(got), bits(want))
+    finally:
+        lib.sm_destroy(ctx)
 
 
 @pytest.mark.parametrize("agg", ["GF", "NL"])

@@ -124,6 +124,8 @@ typedef struct sm_params {
     /* alternative aggregators */
     float gf_eps;                /* gf_eps[0] = 0.0001 (h:298; radius gf_r[0] = 9, h:297) */
     int32_t gf_mode;             /* sm_gf_mode: SM_GF_XIMGPROC (default, the shipped build) or SM_GF_MY_GUIDE */
+    int32_t sgm_2pass;           /* 1 (default): 4-path SGM with D = 64 / 128 / 256 as two 2-D wavefront passes
+                                  * (L0 + L2, then L1 + L3 + sum + WTA; identical results); 0: four path sweeps */
     double nl_sigma;             /* NLCCA sigma = 0.1 (NL/NLCCA.cpp:33): weights exp(-c / (255 sigma)) */
 } sm_params;
 

@@ -22,9 +22,10 @@
 //
 // smamd::Mat mirrors the part of cv::Mat the driver touches: reference-counted shallow copies
 // (the reference's ctor keeps headers of the caller's images, cpp:2066-2075), rows/cols/step/data,
-// empty(), channels(), ptr<T>(row), convertTo(CV_32F, alpha).  imread reads binary PNM (P5 gray,
-// P6 colour; flags 1 -> BGR, 0 -> gray with libpng's rgb_to_gray weights, the formula OpenCV's
-// PNG decoder uses) since the container has no image codecs.  All compute runs in libsm_hip.so on
+// empty(), channels(), ptr<T>(row), convertTo(CV_32F, alpha).  imread reads PNG (main_.cpp:92-107
+// reads the Middlebury *.png files; decoded here with zlib, link -lz) and binary PNM (P5 gray, P6
+// colour): flags 1 -> 3-channel BGR, 0 -> gray with libpng's rgb_to_gray weights, the formula
+// OpenCV's PNG decoder uses.  All compute runs in libsm_hip.so on
 // the GPU; the library does no file I/O, so openCSV/closeCSV/saveTime keep their records in memory
 // (the reference wrote savePath files and exit()ed on failure, h:1727-1744).  Non-OK statuses
 // become std::runtime_error (the reference threw cv::Exception from CV_Assert).
@@ -34,10 +35,12 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <fstream>
 #include <iostream>
+#include <iterator>
 #include <memory>
 #include <sstream>
 #include <stdexcept>
@@ -45,6 +48,13 @@
 #include <vector>
 
 #include "sm_capi.h"
+
+#if __has_include(<zlib.h>)
+#include <zlib.h>
+#define SMAMD_HAVE_PNG 1
+#else
+#define SMAMD_HAVE_PNG 0
+#endif
 
 namespace smamd {
 
@@ -124,19 +134,140 @@ class Mat {
     std::shared_ptr<std::vector<uint8_t>> buf_;
 };
 
-// cv::imread for binary PNM: P6 (RGB) or P5 (gray), maxval 255.  flags 1: 3-channel BGR; flags 0:
-// gray ((R*9798 + G*19235 + B*3735 + 16384) >> 15, libpng's rgb_to_gray).  Empty Mat on failure
-// (main_.cpp:108 tests empty()).
-inline Mat imread(const std::string& path, int flags = 1) {
-    std::ifstream f(path, std::ios::binary);
+namespace detail {
+
+// Decoded 8-bit pixels: w x h, cin = 1 (gray) or 3 (R, G, B), row-major.
+struct Pixels {
+    int w = 0, h = 0, cin = 0;
+    std::vector<uint8_t> px;
+};
+
+inline bool read_pnm(std::ifstream& f, Pixels& out) {
     std::string magic;
     int w = 0, h = 0, maxv = 0;
     if (!(f >> magic >> w >> h >> maxv) || (magic != "P6" && magic != "P5") || maxv != 255 || w < 1 || h < 1)
-        return Mat();
+        return false;
     f.get();
-    const int cin = magic == "P6" ? 3 : 1;
-    std::vector<uint8_t> px((size_t)w * h * cin);
-    if (!f.read((char*)px.data(), (std::streamsize)px.size())) return Mat();
+    out.w = w, out.h = h, out.cin = magic == "P6" ? 3 : 1;
+    out.px.resize((size_t)w * h * out.cin);
+    return (bool)f.read((char*)out.px.data(), (std::streamsize)out.px.size());
+}
+
+#if SMAMD_HAVE_PNG
+inline uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+// PNG (ISO/IEC 15948) the way OpenCV's PngDecoder delivers it to imread(.., 0 / 1): 8-bit samples
+// (1/2/4-bit gray expanded to 8 bits, 16-bit samples stripped to their high byte as
+// png_set_strip_16 does, palettes expanded to RGB, alpha dropped).  Non-interlaced images only.
+inline bool read_png(const std::vector<uint8_t>& file, Pixels& out) {
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0d, 0x0a, 0x1a, 0x0a};
+    if (file.size() < 8 || std::memcmp(file.data(), sig, 8) != 0) return false;
+    int w = 0, h = 0, depth = 0, ctype = -1, interlace = 0;
+    std::vector<uint8_t> idat, plte;
+    for (size_t pos = 8; pos + 12 <= file.size();) {
+        const uint32_t len = be32(&file[pos]);
+        if (pos + 12 + (size_t)len > file.size()) return false;
+        const uint8_t* type = &file[pos + 4];
+        const uint8_t* data = &file[pos + 8];
+        if (!std::memcmp(type, "IHDR", 4) && len >= 13) {
+            w = (int)be32(data), h = (int)be32(data + 4), depth = data[8], ctype = data[9], interlace = data[12];
+        } else if (!std::memcmp(type, "PLTE", 4)) {
+            plte.assign(data, data + len);
+        } else if (!std::memcmp(type, "IDAT", 4)) {
+            idat.insert(idat.end(), data, data + len);
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            break;
+        }
+        pos += 12 + (size_t)len;
+    }
+    // samples per pixel by colour type: 0 gray, 2 RGB, 3 palette index, 4 gray + alpha, 6 RGBA
+    const int spp = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
+    const bool depth_ok = depth == 8 || depth == 16 || ((ctype == 0 || ctype == 3) && (depth == 1 || depth == 2 || depth == 4));
+    if (w < 1 || h < 1 || spp == 0 || !depth_ok || interlace != 0 || (ctype == 3 && (plte.empty() || depth == 16)))
+        return false;
+    const size_t bpp = std::max<size_t>(1, (size_t)spp * depth / 8);     // filter byte distance
+    const size_t stride = ((size_t)w * spp * depth + 7) / 8;             // bytes per scanline
+    std::vector<uint8_t> raw(h * (stride + 1));
+    uLongf rlen = (uLongf)raw.size();
+    if (uncompress(raw.data(), &rlen, idat.data(), (uLong)idat.size()) != Z_OK || rlen != raw.size()) return false;
+    // undo the per-scanline filters (None, Sub, Up, Average, Paeth)
+    std::vector<uint8_t> img((size_t)h * stride);
+    for (int y = 0; y < h; y++) {
+        const uint8_t ft = raw[(size_t)y * (stride + 1)];
+        const uint8_t* src = &raw[(size_t)y * (stride + 1) + 1];
+        uint8_t* cur = &img[(size_t)y * stride];
+        const uint8_t* up = y > 0 ? &img[(size_t)(y - 1) * stride] : nullptr;
+        for (size_t i = 0; i < stride; i++) {
+            const int a = i >= bpp ? cur[i - bpp] : 0, b = up ? up[i] : 0, c = (up && i >= bpp) ? up[i - bpp] : 0;
+            int x = src[i];
+            switch (ft) {
+                case 0: break;
+                case 1: x += a; break;
+                case 2: x += b; break;
+                case 3: x += (a + b) / 2; break;
+                case 4: {
+                    const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+                    x += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+                    break;
+                }
+                default: return false;
+            }
+            cur[i] = (uint8_t)x;
+        }
+    }
+    out.w = w, out.h = h, out.cin = (ctype == 0 || ctype == 4) ? 1 : 3;
+    out.px.assign((size_t)w * h * out.cin, 0);
+    for (int y = 0; y < h; y++) {
+        const uint8_t* row = &img[(size_t)y * stride];
+        for (int x = 0; x < w; x++) {
+            uint8_t* o = &out.px[((size_t)y * w + x) * out.cin];
+            if (depth < 8) {   // packed gray / palette indices, most significant bits first
+                const int per = 8 / depth, shift = 8 - depth * (x % per + 1);
+                const int v = (row[x / per] >> shift) & ((1 << depth) - 1);
+                if (ctype == 3) {
+                    if ((size_t)v * 3 + 2 >= plte.size()) return false;
+                    o[0] = plte[v * 3], o[1] = plte[v * 3 + 1], o[2] = plte[v * 3 + 2];
+                } else {
+                    o[0] = (uint8_t)(v * 255 / ((1 << depth) - 1));
+                }
+                continue;
+            }
+            const size_t bs = depth / 8;   // bytes per sample; 16-bit: the high byte comes first
+            const uint8_t* p = row + (size_t)x * spp * bs;
+            if (ctype == 3) {
+                const int v = p[0];
+                if ((size_t)v * 3 + 2 >= plte.size()) return false;
+                o[0] = plte[v * 3], o[1] = plte[v * 3 + 1], o[2] = plte[v * 3 + 2];
+            } else {
+                for (int k = 0; k < out.cin; k++) o[k] = p[k * bs];
+            }
+        }
+    }
+    return true;
+}
+#endif
+
+}  // namespace detail
+
+// cv::imread for PNG (when zlib is available) and binary PNM (P6 RGB / P5 gray, maxval 255).
+// flags 1: 3-channel BGR; flags 0: gray ((R*9798 + G*19235 + B*3735 + 16384) >> 15, libpng's
+// rgb_to_gray).  Empty Mat on failure (main_.cpp:108 tests empty()).
+inline Mat imread(const std::string& path, int flags = 1) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return Mat();
+    detail::Pixels d;
+    const int first = f.peek();
+#if SMAMD_HAVE_PNG
+    if (first == 0x89) {
+        std::vector<uint8_t> file((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        if (!detail::read_png(file, d)) return Mat();
+    } else
+#endif
+        if (first != 'P' || !detail::read_pnm(f, d)) {
+        return Mat();
+    }
+    const int w = d.w, h = d.h, cin = d.cin;
+    const std::vector<uint8_t>& px = d.px;
     Mat m(h, w, CV_8U, flags == 0 ? 1 : 3);
     for (size_t i = 0; i < (size_t)w * h; i++) {
         const uint8_t R = px[i * cin], G = px[i * cin + (cin - 1) / 2], B = px[i * cin + cin - 1];

@@ -120,10 +120,20 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #ifndef SM_CB_VG_AUX
 #define SM_CB_VG_AUX 0       // cache policy bits of the V sweeps' arm gathers (tuning)
 #endif
+// CB_NORM_SCAN sweeps (two S rings + the area ring: three waves per CU): tile and tiles in flight
+#ifndef SM_CB_T_NS
+#define SM_CB_T_NS 8
+#endif
+#ifndef SM_CB_PF_NS_H
+#define SM_CB_PF_NS_H 2
+#endif
+#ifndef SM_CB_PF_NS_V
+#define SM_CB_PF_NS_V 1
+#endif
 __host__ __device__ constexpr int cbca_win_ring(int T) { return 63 + T; }
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
     return mode == CB_SCAN ? (horiz ? SM_CB_T_SCAN_H : SM_CB_T_SCAN_V)
-                           : (mode == CB_NORM ? (horiz ? SM_CB_T_NORM_H : SM_CB_T_NORM_V) : 8);
+                           : (mode == CB_NORM ? (horiz ? SM_CB_T_NORM_H : SM_CB_T_NORM_V) : SM_CB_T_NS);
 }
 // V sweeps as workgroups of KW waves on KW adjacent columns of one 64-disparity chunk
 // (SM_CB_VGROUP): per tile the workgroup stages, for each arm set and row, the KW own-image words
@@ -176,7 +186,7 @@ template <bool HORIZ, int MODE, int KW = 1>
 struct CbCfg {
     static constexpr int T = (KW > 1 && MODE == CB_NORM) ? SM_CB_T_NORM_VG : cbca_tile(HORIZ, MODE);
     static constexpr int PF = MODE == CB_SCAN ? (HORIZ ? SM_CB_PF_SCAN_H : SM_CB_PF_SCAN_V)
-                                              : (MODE == CB_NORM ? (HORIZ ? SM_CB_PF_NORM_H : SM_CB_PF_NORM_V) : (HORIZ ? 2 : 1));
+                                              : (MODE == CB_NORM ? (HORIZ ? SM_CB_PF_NORM_H : SM_CB_PF_NORM_V) : (HORIZ ? SM_CB_PF_NS_H : SM_CB_PF_NS_V));
     // arm sets: 0 = pass pair at i (= j - lag), 1 = perpendicular pair at j, 2 = pass pair at j - 2 lag
     static constexpr int NSETS = MODE == CB_SCAN ? 1 : (MODE == CB_NORM ? 2 : 3);
     static constexpr int NW = KW > 1 ? NSETS * T * cbca_spw(KW) : 0;          // staged words per tile

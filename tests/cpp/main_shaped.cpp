@@ -3,7 +3,8 @@
 // namespace cv`) and the dataset paths taken from argv.  Test program (tests/test_cpp_facade.py):
 // it must compile unchanged against the facade, and on a GPU its DP[0] must equal the oracle's.
 // Usage: main_shaped IMGDIR MAXDISP REDUCE_COEFF OUT.i16
-//   IMGDIR holds left.ppm right.ppm (P6), disp.pgm all.pgm nonocc.pgm disc.pgm (P5);
+//   IMGDIR holds a Middlebury-2003-style object folder as main_.cpp reads it (teddy / cones
+//   entries of main:33-39): im2.png im6.png disp2.png all.png nonocc.png disc.png;
 //   OUT.i16 receives DP[0] as raw little-endian int16, rows x cols.
 #include "stereo_matching.hpp"
 
@@ -31,17 +32,23 @@ int main(int argc, char* argv[]) {
     const int i = 0;
     string dataset = "MD";
 
-    // main_.cpp:85-129
-    string leftimg = imgroot + "left.ppm";
-    string rightimg = imgroot + "right.ppm";
-    string img_disp = imgroot + "disp.pgm";
+    // main_.cpp:26-39, 85-129 (leftNameList / rightNameList / dispNameList of teddy and cones)
+    string all_maskN = "all.png";
+    string nonocc_maskN = "nonocc.png";
+    string disc_maskN = "disc.png";
+    string leftimg = imgroot + "im2" + ".png";
+    string rightimg = imgroot + "im6" + ".png";
+    string img_disp = imgroot + "disp2" + ".png";
+    string all_mask = imgroot + all_maskN;
+    string nonocc_mask = imgroot + nonocc_maskN;
+    string disc_mask = imgroot + disc_maskN;
     Mat I1_c = imread(leftimg, 1);
     Mat I2_c = imread(rightimg, 1);
     Mat I1 = imread(leftimg, 0);
     Mat I2 = imread(rightimg, 0);
-    Mat all_maskM = imread(imgroot + "all.pgm", 0);
-    Mat nonocc_maskM = imread(imgroot + "nonocc.pgm", 0);
-    Mat disc_maskM = imread(imgroot + "disc.pgm", 0);
+    Mat all_maskM = imread(all_mask, 0);
+    Mat nonocc_maskM = imread(nonocc_mask, 0);
+    Mat disc_maskM = imread(disc_mask, 0);
     Mat DT = imread(img_disp, 0);
     if (I1.empty() || I2.empty() || I1_c.empty() || I2_c.empty()) {
         cout << "can't read original img" << endl;

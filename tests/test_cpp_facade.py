@@ -27,6 +27,7 @@ def _compile(src, out, link=True):
     cmd = CXX + [src, "-o", out]
     if link:
         cmd += [f"-L{LIBDIR}", "-lsm_hip", f"-Wl,-rpath,{LIBDIR}"]
+    cmd += ["-lz"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
 
@@ -45,15 +46,21 @@ def write_pgm(path, g):
         f.write(np.ascontiguousarray(g, np.uint8).tobytes())
 
 
+def write_png(path, a):
+    from PIL import Image
+    Image.fromarray(np.ascontiguousarray(a)).save(path)
+
+
 def write_dataset(d, pair, reduce):
+    """A Middlebury-2003-style object folder as main_.cpp:85-107 reads it (teddy naming)."""
     os.makedirs(d, exist_ok=True)
-    write_ppm(os.path.join(d, "left.ppm"), pair["lbgr"])
-    write_ppm(os.path.join(d, "right.ppm"), pair["rbgr"])
+    write_png(os.path.join(d, "im2.png"), pair["lbgr"][..., ::-1])
+    write_png(os.path.join(d, "im6.png"), pair["rbgr"][..., ::-1])
     dt8 = np.clip(np.rint(pair["gt"] * reduce), 0, 255).astype(np.uint8)
-    write_pgm(os.path.join(d, "disp.pgm"), dt8)
-    write_pgm(os.path.join(d, "all.pgm"), pair["all"])
-    write_pgm(os.path.join(d, "nonocc.pgm"), pair["nonocc"])
-    write_pgm(os.path.join(d, "disc.pgm"), pair["nonocc"])
+    write_png(os.path.join(d, "disp2.png"), dt8)
+    write_png(os.path.join(d, "all.png"), pair["all"])
+    write_png(os.path.join(d, "nonocc.png"), pair["nonocc"])
+    write_png(os.path.join(d, "disc.png"), pair["nonocc"])
     return dt8
 
 
@@ -159,3 +166,65 @@ def test_sm_main_tool_matches_oracle(tmp_path, oracle):
     got = np.frombuffer(raw[len(hdr):], ">u2").reshape(H, W).astype(np.int32)
     want = oracle.run(pair, oracle.config(H, W, md))["disp"].astype(np.int32)
     np.testing.assert_array_equal(got, np.maximum(want, 0))
+
+
+PNG_CHECK = r"""
+#include "stereo_matching.hpp"
+#include <cstdio>
+using namespace smamd;
+std::string StereoMatching::costcalculation = "censusGrad", StereoMatching::aggregation = "CBCA",
+            StereoMatching::optimization = "sgm", StereoMatching::object = "";
+const std::string StereoMatching::root = "";
+int main(int argc, char** argv) {
+    for (int i = 1; i < argc; i++) {
+        Mat c = imread(argv[i], 1), g = imread(argv[i], 0);
+        if (c.empty() || g.empty()) { std::printf("E %d\n", i); continue; }
+        std::fwrite(c.data, 1, (size_t)c.rows * c.step, stdout);
+        std::fwrite(g.data, 1, (size_t)g.rows * g.step, stdout);
+    }
+    return 0;
+}
+"""
+
+
+def test_imread_png(tmp_path):
+    """smamd::imread on PNG files written by PIL: RGB, RGBA, gray, 16-bit gray, 1/4-bit gray and
+    palette images, several filter choices -- BGR for flags 1 and libpng's rgb_to_gray for flags 0,
+    as OpenCV's PNG decoder delivers them (main_.cpp:92-107 reads *.png)."""
+    from PIL import Image
+    from mystereomatching_amd import synthetic as S
+    src = tmp_path / "png_check.cpp"
+    src.write_text(PNG_CHECK)
+    exe = str(tmp_path / "png_check")
+    _compile(str(src), exe, link=False)
+    rng = np.random.default_rng(11)
+    H, W = 13, 21
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    rgb[:, :7] = rgb[:, 7:8]                       # flat runs: Sub / Up / Paeth filters get used
+    gray = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    g16 = rng.integers(0, 65536, (H, W), dtype=np.uint16)
+    bits1 = rng.integers(0, 2, (H, W), dtype=np.uint8)
+    g4 = rng.integers(0, 16, (H, W), dtype=np.uint8)
+    cases = []   # (file, expected RGB)
+    Image.fromarray(rgb).save(tmp_path / "rgb.png"); cases.append(("rgb.png", rgb))
+    Image.fromarray(rgb).save(tmp_path / "rgb9.png", compress_level=9, optimize=True); cases.append(("rgb9.png", rgb))
+    rgba = np.dstack([rgb, rng.integers(0, 256, (H, W), dtype=np.uint8)])
+    Image.fromarray(rgba, "RGBA").save(tmp_path / "rgba.png"); cases.append(("rgba.png", rgb))
+    Image.fromarray(gray).save(tmp_path / "gray.png"); cases.append(("gray.png", np.dstack([gray] * 3)))
+    Image.fromarray(g16).save(tmp_path / "g16.png"); g16h = (g16 >> 8).astype(np.uint8)
+    cases.append(("g16.png", np.dstack([g16h] * 3)))
+    Image.fromarray(bits1 * 255).convert("1").save(tmp_path / "b1.png"); cases.append(("b1.png", np.dstack([bits1 * 255] * 3)))
+    pal = Image.fromarray(rgb).quantize(colors=16)
+    pal.save(tmp_path / "pal.png"); cases.append(("pal.png", np.asarray(pal.convert("RGB"))))
+    r = subprocess.run([exe] + [str(tmp_path / f) for f, _ in cases], capture_output=True)
+    assert r.returncode == 0 and not r.stdout.startswith(b"E"), r.stdout[:200]
+    out = np.frombuffer(r.stdout, np.uint8)
+    pos = 0
+    for f, want in cases:
+        bgr = out[pos:pos + H * W * 3].reshape(H, W, 3)
+        pos += H * W * 3
+        g = out[pos:pos + H * W].reshape(H, W)
+        pos += H * W
+        np.testing.assert_array_equal(bgr, want[..., ::-1], err_msg=f)
+        np.testing.assert_array_equal(g, S.bgr_to_gray(np.ascontiguousarray(want[..., ::-1])), err_msg=f)
+    assert pos == out.size

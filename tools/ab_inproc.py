@@ -8,7 +8,7 @@ rounds A, B, C, A, B, C, ... and reports each variant's median per-kernel HIP-ev
 median ms per step over the rounds.
 
 usage: python tools/ab_inproc.py [--workload teddy] [--rounds 8] [--steps 5] v1 v2 ...
-       (variant v = tools/variants/libsm_hip_<v>.so; "base" = the in-tree library; v:ENV=VAL,...
+       (variant v = tools/abvar/libsm_hip_<v>.so; "base" = the in-tree library; v:ENV=VAL,...
        sets environment variables while that instance is created, v:key=N overrides sm_params)
 """
 import argparse
@@ -57,7 +57,7 @@ def main():
         if v == "base":
             os.environ.pop("SM_HIP_LIB", None)
         else:
-            os.environ["SM_HIP_LIB"] = os.path.join(ROOT, "tools", "variants", f"libsm_hip_{v}.so")
+            os.environ["SM_HIP_LIB"] = os.path.join(ROOT, "tools", "abvar", f"libsm_hip_{v}.so")
         sb = StereoBatch(md, H, W, B, sgm_paths=paths, aggregation=a.agg, **params)
         sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
         sb.run(0.3, download=False)

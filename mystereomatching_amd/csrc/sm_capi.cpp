@@ -1020,7 +1020,7 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->vm1, cap * c->nvol + vpad))) return s;
     if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
         if ((s = dalloc(c, &c->acc, cap * c->nvol + vpad))) return s;
-    if (p->optimization == SM_OPT_SGM && p->sgm_2pass && sm::sgm2_supported(p->num_disparities, p->sgm_paths)) {
+    if (p->optimization == SM_OPT_SGM && p->sgm_2pass && sm::sgm2_supported(p->num_disparities, p->sgm_paths, p->cols)) {
         if ((s = dalloc(c, &c->l2v, cap * c->nvol + vpad))) return s;
         if ((s = dalloc(c, &c->sgm2_sync, sm::sgm2_sync_words(p->rows, (int)cap)))) return s;
         HIP_TRY(c, hipMemset(c->sgm2_sync, 0, sm::sgm2_sync_words(p->rows, (int)cap) * 4));

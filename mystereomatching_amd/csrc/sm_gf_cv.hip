@@ -12,8 +12,8 @@
 //   q            = box(beta) + sum_c box(alpha_c) I_c
 //
 // gfx950 mapping.  The p-independent terms (mean_I and Sigma^-1 per pixel, 9 floats) come from
-// nine image planes, row-summed by one thread per row (k_gfcv_img_rows) and column-summed by one
-// thread per column (k_gfcv_img_cols, which also inverts Sigma).  The volume work is four line
+// nine image planes, row-summed by one thread per row (k_gfcv_img_rows), column-summed by one
+// thread per plane and column (k_gfcv_img_cols), Sigma inverted per pixel (k_gfcv_pix).  The volume work is four line
 // sweeps over [H][W][D] with lane = disparity and one wave per (line, 64-disparity chunk), each
 // carrying four channels:
 //   R0: row sums of (p, p B, p G, p R)          -> RS (four double volumes)
@@ -74,67 +74,88 @@ __global__ __launch_bounds__(256) void k_gfcv_img_rows(const uint32_t* __restric
     }
 }
 
-// one thread per (pair, column): ColumnSum<double, float> of the nine planes, then per pixel
-// mean_I and Sigma^-1 (the restatement's float cofactors / det) into pix[b][9][H][W]:
-// 0..2 = mean_I (B, G, R), 3..8 = inverse entries 00, 01, 02, 11, 12, 22
+// one thread per (pair, plane, column): ColumnSum<double, float> of the plane into pix[b][k]
+// (the means; planes 3..8 are replaced by Sigma^-1 in k_gfcv_pix).  The next rows' sums are
+// loaded while the current ones are added (a column walk is a chain of dependent adds).
 __global__ __launch_bounds__(256) void k_gfcv_img_cols(const double* __restrict__ rs, float* __restrict__ pix, int H, int W,
-                                                       int n, float eps) {
+                                                       int n) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * W) return;
-    const int x = t % W, b = t / W;
+    if (t >= n * 9 * W) return;
+    const int x = t % W, k = (t / W) % 9, b = t / (9 * W);
     const size_t npix = (size_t)H * W;
-    const double* base = rs + (size_t)b * 9 * npix + x;
-    float* out = pix + (size_t)b * 9 * npix + x;
+    const double* base = rs + ((size_t)b * 9 + k) * npix + x;
+    float* out = pix + ((size_t)b * 9 + k) * npix + x;
     const double scale = 1. / (GC_K * GC_K);
-    double SUM[9];
+    double SUM = 0;
+    for (int i = 0; i < GC_K - 1; i++) SUM += base[(size_t)refl(i - GC_R, H) * W];
+    constexpr int U = 4;
+    double sp[U], sm[U], np[U], nm[U];
+    auto fetch = [&](double (&p)[U], double (&m)[U], int y0) {
 #pragma unroll
-    for (int k = 0; k < 9; k++) {
-        SUM[k] = 0;
-        for (int i = 0; i < GC_K - 1; i++) SUM[k] += base[(size_t)k * npix + (size_t)refl(i - GC_R, H) * W];
-    }
-    for (int y = 0; y < H; y++) {
-        const size_t rp = (size_t)refl(y + GC_R, H) * W, rm = (size_t)refl(y - GC_R, H) * W;
-        float m[9];
-#pragma unroll
-        for (int k = 0; k < 9; k++) {
-            const double s0 = SUM[k] + base[(size_t)k * npix + rp];
-            m[k] = (float)(s0 * scale);
-            SUM[k] = s0 - base[(size_t)k * npix + rm];
+        for (int u = 0; u < U; u++) {
+            const int y = min(y0 + u, H - 1);
+            p[u] = base[(size_t)refl(y + GC_R, H) * W];
+            m[u] = base[(size_t)refl(y - GC_R, H) * W];
         }
-        // Sigma = box(I_i I_j) - m_i m_j, + eps on the diagonal
-        float a[6];
-        {
-            const int I0[6] = {0, 0, 0, 1, 1, 2}, I1[6] = {0, 1, 2, 1, 2, 2};
+    };
+    fetch(np, nm, 0);
+    for (int y0 = 0; y0 < H; y0 += U) {
 #pragma unroll
-            for (int v = 0; v < 6; v++) {
-                const float mm = m[I0[v]] * m[I1[v]];
-                a[v] = m[3 + v] - mm;
-                if (I0[v] == I1[v]) a[v] = a[v] + eps;
-            }
+        for (int u = 0; u < U; u++) {
+            sp[u] = np[u];
+            sm[u] = nm[u];
         }
-        const float a00 = a[0], a01 = a[1], a02 = a[2], a11 = a[3], a12 = a[4], a22 = a[5];
-        float b00 = a11 * a22, b01 = a02 * a12, b02 = a01 * a12, b11 = a00 * a22, b12 = a01 * a02, b22 = a00 * a11;
-        float mm;
-        mm = a12 * a12; b00 = b00 - mm;
-        mm = a01 * a22; b01 = b01 - mm;
-        mm = a02 * a11; b02 = b02 - mm;
-        mm = a02 * a02; b11 = b11 - mm;
-        mm = a00 * a12; b12 = b12 - mm;
-        mm = a01 * a01; b22 = b22 - mm;
-        float det = a00 * b00;
-        mm = a01 * b01; det = det + mm;
-        mm = a02 * b02; det = det + mm;
-        const size_t o = (size_t)y * W;
-        out[0 * npix + o] = m[0];
-        out[1 * npix + o] = m[1];
-        out[2 * npix + o] = m[2];
-        out[3 * npix + o] = b00 / det;
-        out[4 * npix + o] = b01 / det;
-        out[5 * npix + o] = b02 / det;
-        out[6 * npix + o] = b11 / det;
-        out[7 * npix + o] = b12 / det;
-        out[8 * npix + o] = b22 / det;
+        if (y0 + U < H) fetch(np, nm, y0 + U);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (y0 + u >= H) break;
+            const double s0 = SUM + sp[u];
+            out[(size_t)(y0 + u) * W] = (float)(s0 * scale);
+            SUM = s0 - sm[u];
+        }
     }
+}
+
+// per pixel: Sigma = box(I_i I_j) - m_i m_j (+ eps on the diagonal) and its inverse by the
+// restatement's float cofactors / det, written over the box(I_i I_j) planes 3..8 as the entries
+// 00, 01, 02, 11, 12, 22 (planes 0..2 keep mean_I)
+__global__ __launch_bounds__(256) void k_gfcv_pix(float* __restrict__ pix, int H, int W, int n, float eps) {
+    const size_t npix = (size_t)H * W;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= npix * n) return;
+    const size_t b = t / npix, i = t - b * npix;
+    float* pl = pix + b * 9 * npix + i;
+    float m[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) m[k] = pl[k * npix];
+    float a[6];
+    {
+        const int I0[6] = {0, 0, 0, 1, 1, 2}, I1[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+        for (int v = 0; v < 6; v++) {
+            const float mm = m[I0[v]] * m[I1[v]];
+            a[v] = m[3 + v] - mm;
+            if (I0[v] == I1[v]) a[v] = a[v] + eps;
+        }
+    }
+    const float a00 = a[0], a01 = a[1], a02 = a[2], a11 = a[3], a12 = a[4], a22 = a[5];
+    float b00 = a11 * a22, b01 = a02 * a12, b02 = a01 * a12, b11 = a00 * a22, b12 = a01 * a02, b22 = a00 * a11;
+    float mm;
+    mm = a12 * a12; b00 = b00 - mm;
+    mm = a01 * a22; b01 = b01 - mm;
+    mm = a02 * a11; b02 = b02 - mm;
+    mm = a02 * a02; b11 = b11 - mm;
+    mm = a00 * a12; b12 = b12 - mm;
+    mm = a01 * a01; b22 = b22 - mm;
+    float det = a00 * b00;
+    mm = a01 * b01; det = det + mm;
+    mm = a02 * b02; det = det + mm;
+    pl[3 * npix] = b00 / det;
+    pl[4 * npix] = b01 / det;
+    pl[5 * npix] = b02 / det;
+    pl[6 * npix] = b11 / det;
+    pl[7 * npix] = b12 / det;
+    pl[8 * npix] = b22 / det;
 }
 
 #ifndef SM_GFCV_T
@@ -368,8 +389,10 @@ void launch_gf_cv(const GfCvArgs& a, int n, hipStream_t st) {
         const int tr = n * 9 * a.H;
         hipLaunchKernelGGL(k_gfcv_img_rows, dim3((tr + 255) / 256), dim3(256), 0, st, a.px, a.px_pair_stride, a.img_rs, a.H,
                            a.W, n);
-        const int tc = n * a.W;
-        hipLaunchKernelGGL(k_gfcv_img_cols, dim3((tc + 255) / 256), dim3(256), 0, st, a.img_rs, a.pix, a.H, a.W, n, a.eps);
+        const int tc = n * 9 * a.W;
+        hipLaunchKernelGGL(k_gfcv_img_cols, dim3((tc + 255) / 256), dim3(256), 0, st, a.img_rs, a.pix, a.H, a.W, n);
+        const size_t tp = (size_t)n * a.H * a.W;
+        hipLaunchKernelGGL(k_gfcv_pix, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, st, a.pix, a.H, a.W, n, a.eps);
     }
     const int nchunks = (a.D + 63) / 64;
     hipLaunchKernelGGL(k_gfcv_rows<0>, dim3(a.H * nchunks * n), dim3(64), 0, st, a);

@@ -88,7 +88,7 @@ struct Sgm2Args {               // 4-path SGM in two 2-D wavefront passes (sm_sg
     float p1, p2;
     int redu, keep_final, signed_costs;
 };
-bool sgm2_supported(int D, int paths);
+bool sgm2_supported(int D, int paths, int W);
 size_t sgm2_sync_words(int H, int n);
 hipError_t launch_sgm2_pass(const Sgm2Args& a, bool pass_b, hipStream_t st);
 

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sm_device.h"
 #include "sm_kernels.h"
 
@@ -38,6 +40,12 @@
 #endif
 #ifndef SM_SGM2_TC
 #define SM_SGM2_TC 2         // columns per tile (= the skew between consecutive rows)
+#endif
+#ifndef SM_SGM2_PF
+#define SM_SGM2_PF 3         // tiles whose loads are in flight ahead of the one processed (<= 5), pass A
+#endif
+#ifndef SM_SGM2_PF_B
+#define SM_SGM2_PF_B 2       // the same for pass B (three volumes per tile: <= 128 VGPRs, two blocks per CU)
 #endif
 #ifndef SM_SGM2_SPIN
 #define SM_SGM2_SPIN (1 << 21)   // polls (an atomic load + s_sleep 2 each, ~1-2 us) before a wait gives up
@@ -87,12 +95,21 @@ struct Sg2Tile {
     float a0[TC][K];   // pass B: acc = 0 + L0
     float a2[TC][K];   // pass B: L2
     float xv[TC][K];   // first wave of a strip: the previous strip's vertical L for this tile
-    uint32_t fl[TC];   // penalty flags of the tile's pixels (wave-uniform)
 };
 
-template <int K, int R, int TC, bool PB, bool SG, bool KEEP>
+// s_waitcnt with vmcnt(n) only (expcnt / lgkmcnt left at their maxima)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xf << 8));
+}
+__device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
+
+template <int K, int R, int TC, int PF, bool PB, bool SG, bool KEEP>
 __global__ __launch_bounds__(64 * R) void k_sgm2(const Sgm2Args a) {
-    extern __shared__ float xch[];   // [R - 1][2][TC][64 K]: vertical L handed from wave r to r + 1
+    constexpr int NB = PF + 1;                         // tiles in the register ring
+    constexpr int NLT = TC * (PB ? 3 : 1);             // vector-memory loads per tile (C [+ acc, l2v])
+    extern __shared__ float xch[];   // [R - 1][2][TC][64 K] vertical L from wave r to r + 1, then the flags
     __shared__ int s_ticket;
     const int lane = threadIdx.x & 63;
     const int r = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -119,7 +136,6 @@ __global__ __launch_bounds__(64 * R) void k_sgm2(const Sgm2Args a) {
     const __amdgpu_buffer_rsrc_t rL = buf_rsrc(a.l2v + rowe, rowbytes);
     const int vprev = PB ? v - 1 : v + 1;                // the previous strip's last row (xin)
     const __amdgpu_buffer_rsrc_t rX = buf_rsrc(a.acc + ((size_t)b * npix + (size_t)(xin ? vprev : v) * W) * D, rowbytes);
-    const uint8_t* flrow = a.flags + (size_t)b * npix + (size_t)v * W;
     int16_t* drow = a.disp + (size_t)b * npix + (size_t)v * W;
     uint32_t* const prog_in = sync + SG2_SYNC_HDR + (size_t)b * NS + (s > 0 ? s - 1 : 0);
     uint32_t* const prog_out = sync + SG2_SYNC_HDR + (size_t)b * NS + s;
@@ -129,11 +145,48 @@ __global__ __launch_bounds__(64 * R) void k_sgm2(const Sgm2Args a) {
     const uint32_t lo = (uint32_t)lane * K * 4;          // lane byte offset inside a pixel
     auto col = [&](int j) { return PB ? j : W - 1 - j; };   // column of step j
 
+    // the row's penalty flags (two bits: this pass's vertical and horizontal directions) in LDS,
+    // so that no flag load joins the counted vector-memory loads of the tiles
+    uint8_t* const flg = (uint8_t*)(xch + (size_t)(R - 1) * 2 * TC * 64 * K) + (size_t)r * ((W + 3) & ~3);
+    if (rvalid) {
+        const __amdgpu_buffer_rsrc_t rF = buf_rsrc(a.flags + (size_t)b * npix + (size_t)v * W, W);
+        for (int i = lane * 4; i < W; i += 256) {
+            if (i + 4 <= W) {   // (a dword reaching past the resource's range would read as 0)
+                *(uint32_t*)(flg + i) = __builtin_amdgcn_raw_buffer_load_b32(rF, i, 0, 0);
+            } else {
+                for (int k = i; k < W; k++) flg[k] = __builtin_amdgcn_raw_buffer_load_b8(rF, k, 0, 0);
+            }
+        }
+        wait_vm<0>();
+    }
+
+    // The previous strip's progress as last seen, and an asynchronous poll of it issued at the
+    // start of every phase (before the phase's other loads) and read when a tile's values are
+    // needed, so that the counter's round trip overlaps the phase instead of stalling it.
+    uint32_t seen = 0;
+    uint32_t poll_v = 0;
+    bool poll_out = false;
+    auto poll_issue = [&]() {
+        if (!poll_out) {
+            poll_v = __hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            poll_out = true;
+        }
+    };
     // bounded wait for the previous strip's progress counter (wave-uniform)
     auto wait_prog = [&](uint32_t need) {
+        if (seen >= need) return;
+        if (poll_out) {
+            seen = max(seen, (uint32_t)__builtin_amdgcn_readfirstlane((int)poll_v));
+            poll_out = false;
+            if (seen >= need) {
+                compiler_fence();
+                return;
+            }
+        }
         for (int tries = 0;; tries++) {
             const uint32_t pv = (uint32_t)__builtin_amdgcn_readfirstlane(
                 (int)__hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            seen = pv;
             if (pv >= need) break;
             const uint32_t ab = (uint32_t)__builtin_amdgcn_readfirstlane(
                 (int)__hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -144,24 +197,24 @@ __global__ __launch_bounds__(64 * R) void k_sgm2(const Sgm2Args a) {
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        // order only: the exchange loads below read through the caches (sc1)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        compiler_fence();   // the exchange loads below read through the caches (sc1)
     };
-
-    auto load = [&](Sg2Tile<K, TC>& t, int ti) {
-        if (xin) wait_prog((uint32_t)min(ti + 1, ntiles));   // tile ti of the previous strip published
+    auto load = [&](Sg2Tile<K, TC>& t, int ti) {   // NLT loads (clamped past the row end)
 #pragma unroll
         for (int st = 0; st < TC; st++) {
-            const int j = min(ti * TC + st, W - 1);
-            const uint32_t off = (uint32_t)col(j) * D * 4 + lo;
+            const uint32_t off = (uint32_t)col(min(ti * TC + st, W - 1)) * D * 4 + lo;
             ldK<K, AUX_NT>(rC, off, t.c[st]);
             if (PB) {
                 ldK<K, AUX_NT>(rA, off, t.a0[st]);
                 ldK<K, AUX_NT>(rL, off, t.a2[st]);
             }
-            if (xin) ldK<K, AUX_DEV>(rX, off, t.xv[st]);
-            t.fl[st] = flrow[col(j)];
         }
+    };
+    auto load_x = [&](Sg2Tile<K, TC>& t, int ti) {   // the previous strip's values of tile ti
+        wait_prog((uint32_t)(ti + 1));
+#pragma unroll
+        for (int st = 0; st < TC; st++)
+            ldK<K, AUX_DEV>(rX, (uint32_t)col(min(ti * TC + st, W - 1)) * D * 4 + lo, t.xv[st]);
     };
 
     float Lh[K];            // horizontal path: L of the previous step of this row
@@ -203,7 +256,7 @@ __global__ __launch_bounds__(64 * R) void k_sgm2(const Sgm2Args a) {
             const int j = ti * TC + st;
             if (j >= W) break;   // wave-uniform
             const uint32_t off = (uint32_t)col(j) * D * 4 + lo;
-            const uint32_t fl = t.fl[st];
+            const uint32_t fl = flg[col(j)];
             // vertical path: the previous row's L of this column
             float Lv[K];
             if (first_row) {
@@ -271,37 +324,72 @@ __global__ __launch_bounds__(64 * R) void k_sgm2(const Sgm2Args a) {
             mh = wmin(Lq);
         }
         if (PB && lane < TC && ti * TC + lane < W) drow[col(ti * TC + lane)] = (int16_t)dacc;
-        if (xout) {
-            // publish tile ti: every store of this wave (the sc1 exchange row included) completes
-            // first, then the counter (device-scope atomic store)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));   // vmcnt(0)
-            if (lane == 0) __hip_atomic_store(prog_out, (uint32_t)(ti + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     };
 
-    // phases: wave r processes tile p - r; tile t + 1's loads are issued while tile t is processed
-    Sg2Tile<K, TC> ta, tb;
-    if (r == 0 && rvalid) load(ta, 0);
-    const int nphase = ntiles + R - 1;
-    auto phase = [&](Sg2Tile<K, TC>& cur, Sg2Tile<K, TC>& nxt, int p) {
-        const int ti = p - r;
-        if (rvalid && ti >= -1 && ti + 1 < ntiles) load(nxt, ti + 1);
-        if (rvalid && ti >= 0 && ti < ntiles) process(cur, ti, p);
+    // Phases: wave r processes its tile q in phase q + r (one barrier per phase: wave r first
+    // passes r idle phases, then its ntiles tiles, then R - 1 - r idle phases).  A tile's loads
+    // are issued PF tiles ahead, after the stores of the tile just processed, so that the
+    // publishing wave can wait for its exchange stores (vmcnt counts in issue order) without
+    // waiting for the prefetches: it raises its progress counter for tile q - 1 at the start of
+    // tile q's phase.  The first wave of a later strip fetches the previous strip's values one
+    // tile ahead, before the prefetches.
+    Sg2Tile<K, TC> tl[NB];
+    if (rvalid) {
+#pragma unroll
+        for (int q = 0; q < PF; q++)
+            if (q < ntiles) load(tl[q], q);
+        if (xin) load_x(tl[0], 0);
+    }
+    for (int i = 0; i < r; i++) __syncthreads();
+    bool pending = false;   // xout: tile q - 1's exchange stores issued, counter not raised yet
+    int pend_loads = 0;     // loads issued after those stores
+    auto publish = [&](int q) {
+        if (!pending) return;
+        if (pend_loads) wait_vm<NLT>();   // the exchange stores, not the NLT prefetch loads after them
+        else wait_vm<0>();
+        compiler_fence();
+        if (lane == 0) __hip_atomic_store(prog_out, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pending = false;
+    };
+    auto step_q = [&](auto SLOT, int q) {
+        constexpr int sl = decltype(SLOT)::value;
+        const int p = q + r;
+        if (rvalid) {
+            if (xout) publish(q);
+            if (xin) poll_issue();
+            process(tl[sl], q, p);
+            compiler_fence();
+            if (xin && q + 1 < ntiles) load_x(tl[(sl + 1) % NB], q + 1);
+            const bool more = q + PF < ntiles;
+            if (more) load(tl[(sl + PF) % NB], q + PF);
+            if (xout) {
+                pending = true;
+                pend_loads = more ? NLT : 0;
+            }
+        }
         __syncthreads();
     };
-    for (int p = 0; p < nphase; p += 2) {
-        phase(ta, tb, p);
-        if (p + 1 < nphase) phase(tb, ta, p + 1);
+    for (int q0 = 0; q0 < ntiles; q0 += NB) {
+        step_q(std::integral_constant<int, 0>{}, q0);
+#define SG2_SLOT(I) \
+        if constexpr (NB > I) { if (q0 + I < ntiles) step_q(std::integral_constant<int, I>{}, q0 + I); }
+        SG2_SLOT(1)
+        SG2_SLOT(2)
+        SG2_SLOT(3)
+        SG2_SLOT(4)
+        SG2_SLOT(5)
+#undef SG2_SLOT
     }
+    if (rvalid && xout) publish(ntiles);
+    for (int i = r + 1; i < R; i++) __syncthreads();
 }
 
 template <int K, bool PB, bool SG, bool KEEP>
 void launch_k2(const Sgm2Args& a, hipStream_t st) {
-    constexpr int R = SM_SGM2_R, TC = SM_SGM2_TC;
+    constexpr int R = SM_SGM2_R, TC = SM_SGM2_TC, PF = PB ? SM_SGM2_PF_B : SM_SGM2_PF;
     const int NS = (a.H + R - 1) / R;
-    const size_t shm = (size_t)(R - 1) * 2 * TC * 64 * K * 4;
-    hipLaunchKernelGGL((k_sgm2<K, R, TC, PB, SG, KEEP>), dim3(a.n * NS), dim3(64 * R), shm, st, a);
+    const size_t shm = (size_t)(R - 1) * 2 * TC * 64 * K * 4 + (size_t)R * ((a.W + 3) & ~3);
+    hipLaunchKernelGGL((k_sgm2<K, R, TC, PF, PB, SG, KEEP>), dim3(a.n * NS), dim3(64 * R), shm, st, a);
 }
 
 template <int K>
@@ -320,7 +408,8 @@ void launch_pass(const Sgm2Args& a, bool pass_b, hipStream_t st) {
 
 }  // namespace
 
-bool sgm2_supported(int D, int paths) { return paths == 4 && (D == 64 || D == 128 || D == 256); }
+// D = 64 K (K = 1, 2, 4); the row's flags live in LDS next to the hand-over buffers (W <= 8192)
+bool sgm2_supported(int D, int paths, int W) { return paths == 4 && (D == 64 || D == 128 || D == 256) && W <= 8192; }
 size_t sgm2_sync_words(int H, int n) { return SG2_SYNC_HDR + (size_t)n * ((H + SM_SGM2_R - 1) / SM_SGM2_R); }
 
 hipError_t launch_sgm2_pass(const Sgm2Args& a, bool pass_b, hipStream_t st) {

@@ -391,7 +391,9 @@ sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
         a.do_grad = grad;
         a.do_arms = arms;
         a.do_flags = flags;
-        return timed(c, "prep", (double)n * 2 * c->npix * (1 + 3 + (census ? 16 : 0) + (grad ? 8 : 0) + (arms ? 4 : 0)) +
+        // the packed BGR plane's later readers: the GF image planes, so, refine's properIpol
+        a.pack_px = p.aggregation == SM_AGG_GF || p.optimization == SM_OPT_SO || p.do_refine;
+        return timed(c, "prep", (double)n * 2 * c->npix * (1 + 3 + (census ? 16 : 0) + (grad ? 8 : 0) + (arms ? 8 : 0)) +
                                     (flags ? (double)n * c->npix * n_views(p) : 0),
                      [&] { sm::launch_prep(a, n, c->st); });
     }

@@ -181,6 +181,25 @@ __host__ __device__ constexpr int cbca_spw(int kw) { return 2 * kw + 63; }
 __host__ __device__ constexpr int cbca_wpb(bool horiz, int mode) {
     return (horiz || SM_CB_VGROUP) ? 1 : (mode == CB_SCAN ? SM_CB_WPB_SCAN_V : (mode == CB_NORM ? SM_CB_WPB_NORM_V : 1));
 }
+// V sweeps with CPW adjacent columns per wave (SM_CB_CPW_*_V): lane l runs column u0 + l / CW at
+// disparity c + l % CW (CW = 64 / CPW disparities per chunk).  A row's other-image gather of the
+// wave then reads columns u0 + cl - d of both halves, which overlap in all but one word: 33 distinct
+// words (one or two 128-byte lines) instead of 64 (two or three), the effect timing probe 4 showed
+// (DESIGN §5).  The rings stay one slot per lane; the volume accesses become CPW segments of
+// 4 CW bytes.  The pixel's own arm pair differs between the halves: two readlanes and a select
+// (SM_CB_CPW_OWN 0) or one ds_bpermute (1) per set and position instead of one readlane.
+#ifndef SM_CB_CPW_SCAN_V
+#define SM_CB_CPW_SCAN_V 1
+#endif
+#ifndef SM_CB_CPW_NORM_V
+#define SM_CB_CPW_NORM_V 1
+#endif
+#ifndef SM_CB_CPW_OWN
+#define SM_CB_CPW_OWN 0
+#endif
+__host__ __device__ constexpr int cbca_cpw(bool horiz, int mode, int kw, int wpb) {
+    return (horiz || kw > 1 || wpb > 1 || !SM_CB_V_READLANE) ? 1 : (mode == CB_SCAN ? SM_CB_CPW_SCAN_V : (mode == CB_NORM ? SM_CB_CPW_NORM_V : 1));
+}
 
 template <bool HORIZ, int MODE, int KW = 1>
 struct CbCfg {
@@ -242,9 +261,11 @@ struct CbTile {
 // RV: the right view's volume vm[1] (cbca_core's LOR = 1, run when Do_refine): the pixel's own
 // arms are the right image's, and lane d pairs them with the LEFT image's arms at u + d
 // (HVL_INTERSECTION[1], cpp:2794-2845) — zero once u + d >= W.
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW = 1>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW = 1, int CPW = 1>
 struct CbLine {
+    static constexpr int CW = 64 / CPW;   // disparities per chunk (lanes per column)
     static constexpr int T = CbCfg<HORIZ, MODE, KW>::T;
+    static_assert(T <= CW, "a column's own arm words of a tile are one lane each");
     static constexpr int NSETS = CbCfg<HORIZ, MODE, KW>::NSETS;
     static constexpr int NW = CbCfg<HORIZ, MODE, KW>::NW;
     static constexpr int NV = CbCfg<HORIZ, MODE, KW>::NV;
@@ -263,6 +284,8 @@ struct CbLine {
     uint32_t ov;              // lane's store offset (lanes past D: out of range, dropped)
     uint32_t vsb;             // bytes between consecutive positions
     int lane;
+    int kk, cl;               // V, CPW > 1: lane = cl * CW + kk (column u0 + cl, chunk lane kk)
+    bool colok;               // column u0 + cl < W
     __amdgpu_buffer_rsrc_t A0r[NSETS];  // left-image arm-pair plane of each set over the line
     __amdgpu_buffer_rsrc_t A1r[NSETS];  // H: right-image plane over the line
     const char* A1v[NSETS];     // V: right-image plane, row 0 (uniform)
@@ -342,8 +365,8 @@ struct CbLine {
             const int base = j0 - set_off(s);
             // (only lanes k < T are read back; the others stay off the memory system, which
             // matters for the strided column loads of vertical sweeps)
-            const int p0 = base + lane;
-            t.a0[s] = buf_ld_u32(A0r[s], (lane < T && (unsigned)p0 < (unsigned)len) ? (uint32_t)(p0 * pstride) * 4u : 0x80000000u, 0);
+            const int p0 = base + kk;
+            t.a0[s] = buf_ld_u32(A0r[s], (kk < T && colok && (unsigned)p0 < (unsigned)len) ? (uint32_t)(p0 * pstride + cl) * 4u : 0x80000000u, 0);
             if (HORIZ && SM_CB_LDS_WIN) {
                 // the other image's arm pairs that lanes c64 .. c64 + 63 pair with at positions
                 // base .. base + T - 1: left view q = p - d in [base - c64 - 63, base - c64 + T - 1],
@@ -394,7 +417,19 @@ struct CbLine {
             return pkmin(row[wv], row[KW + (RV ? wv + lane : wv + 63 - lane)]);
         }
         if (!HORIZ && SM_CB_V_READLANE) {
-            const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
+            uint32_t a0;
+            if constexpr (CPW == 1) {
+                a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
+            } else if constexpr (SM_CB_CPW_OWN == 1) {
+                a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((cl * CW + k) * 4, (int)t.a0[s]);
+            } else {
+                a0 = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], k);
+#pragma unroll
+                for (int c = 1; c < CPW; c++) {
+                    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)t.a0[s], c * CW + k);
+                    a0 = cl == c ? x : a0;
+                }
+            }
             return pkmin(a0, t.a1[s][k]);
         }
         if (SM_CB_LDS_WIN) {
@@ -597,14 +632,18 @@ struct CbLine {
 
 template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, int WPB>
 __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
-    CbLine<HORIZ, MODE, FULL, SCALE, RV, KW> L;
+    constexpr int CPW = cbca_cpw(HORIZ, MODE, KW, WPB);
+    constexpr int CW = 64 / CPW;
+    CbLine<HORIZ, MODE, FULL, SCALE, RV, KW, CPW> L;
     constexpr int T = CbCfg<HORIZ, MODE, KW>::T;
     constexpr int NSETS = CbCfg<HORIZ, MODE, KW>::NSETS;
     L.lane = (KW > 1 || WPB > 1) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+    L.kk = L.lane % CW;
+    L.cl = L.lane / CW;
     L.wv = KW > 1 ? (int)(threadIdx.x >> 6) : 0;
     const int wb = WPB > 1 ? (int)(threadIdx.x >> 6) : 0;      // independent wave of a WPB block
-    const int nchunks = (a.D + 63) >> 6;
-    const int ngroups = ((HORIZ ? a.H : a.W) + KW * WPB - 1) / (KW * WPB);   // KW = WPB = 1: one line per block
+    const int nchunks = (a.D + CW - 1) / CW;
+    const int ngroups = ((HORIZ ? a.H : a.W) + KW * WPB * CPW - 1) / (KW * WPB * CPW);   // KW = WPB = CPW = 1: one line per block
     const int per_pair = ngroups * nchunks;
     const int b = blk / per_pair;
     const int lc = blk - b * per_pair;
@@ -614,7 +653,8 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     const bool cmaj = !HORIZ && SM_CB_CHUNK_MAJOR_V;
     const int grp = cmaj ? lc % ngroups : lc / nchunks;
     const int chunk = cmaj ? lc / ngroups : lc - grp * nchunks;
-    L.line = grp * KW * WPB + L.wv + wb;
+    L.line = grp * KW * WPB * CPW + L.wv + wb;   // CPW > 1: the wave's first column u0
+    L.colok = CPW == 1 || L.line + L.cl < a.W;
     // a WPB block's spare waves (past the last column) only zero their rings and pass the barrier
     const bool spare = WPB > 1 && L.line >= (HORIZ ? a.H : a.W);
     if (spare) L.line = (HORIZ ? a.H : a.W) - 1;
@@ -627,13 +667,16 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     const size_t first_pix = HORIZ ? (size_t)L.line * a.W : (size_t)L.line;
     L.pstride = HORIZ ? 1 : a.W;
     L.vsb = (uint32_t)(L.pstride * a.D * 4);
-    L.xline = (const char*)(a.vm + ((size_t)b * npix + first_pix) * a.D + (size_t)chunk * 64);
-    const int dl = chunk * 64 + L.lane;  // true disparity (also for masked lanes)
+    L.xline = (const char*)(a.vm + ((size_t)b * npix + first_pix) * a.D + (size_t)chunk * CW);
+    const int dl = chunk * CW + L.kk;  // true disparity (also for masked lanes)
     {
-        const uint32_t xv = FULL ? (uint32_t)L.lane * 4u : (uint32_t)min(L.lane, a.D - 1 - chunk * 64) * 4u;
+        // CPW > 1: lane's element of column u0 + cl; lanes of columns past W (non-FULL launches
+        // only) load column W - 1 and store nothing
+        const int lc = CPW == 1 ? 0 : min(L.cl, a.W - 1 - L.line);
+        const uint32_t xv = FULL ? (uint32_t)(L.cl * a.D + L.kk) * 4u : (uint32_t)(lc * a.D + min(L.kk, a.D - 1 - chunk * CW)) * 4u;
 #pragma unroll
         for (int k = 0; k < T; k++) L.xo[k] = xv + (uint32_t)k * L.vsb;
-        L.ov = (FULL || dl < a.D) ? (uint32_t)L.lane * 4u : 0x80000000u;
+        L.ov = (FULL || (dl < a.D && L.colok)) ? (uint32_t)(L.cl * a.D + L.kk) * 4u : 0x80000000u;
     }
     L.xend = (const char*)a.vm_end;
     L.aend = (const char*)a.arms_end;
@@ -642,7 +685,7 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     const int pass_plane = HORIZ ? 0 : 1, perp_plane = HORIZ ? 1 : 0;
     const int own = RV ? 2 : 0, other = RV ? 0 : 2;
     const uint32_t* planeL = a.arms + ((size_t)b * 4) * npix + first_pix;
-    const int line_bytes = (((HORIZ ? a.W : a.H) - 1) * L.pstride + 1) * 4;
+    const int line_bytes = (((HORIZ ? a.W : a.H) - 1) * L.pstride + CPW) * 4;   // CPW columns from u0
 #pragma unroll
     for (int s = 0; s < NSETS; s++) {
         const int pl = (s == 1) ? perp_plane : pass_plane;
@@ -655,8 +698,9 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         // other image's column: u - d (left view) or u + d (right view); lanes whose column lies
         // outside the image get an out-of-range offset, so their gathers return the reference's
         // zeroed intersection (cpp:2794-2845) without a mask per position
-        bool out = RV ? L.line + dl >= a.W : L.line - dl < 0;
-        uint32_t col = (uint32_t)(RV ? L.line + dl : L.line - dl) * 4u;
+        const int u = L.line + L.cl;
+        bool out = RV ? u + dl >= a.W : u - dl < 0;
+        uint32_t col = (uint32_t)(RV ? u + dl : u - dl) * 4u;
         if (SM_CB_PROBE_NOVG == 3) {   // timing probe: every wave gathers columns 0..63 of the right rows
             out = false;
             col = (uint32_t)L.lane * 4u;
@@ -667,7 +711,7 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
 #pragma unroll
         for (int k = 0; k < (HORIZ ? 1 : T); k++) L.ao[k] = out ? 0x80000000u : col + (uint32_t)(k * a.W * 4);
     }
-    L.c64 = chunk * 64;
+    L.c64 = chunk * CW;
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
     L.ring = cbca_ring(a.lag, HORIZ, MODE, KW);
@@ -743,7 +787,7 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         }
     }
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    typename CbLine<HORIZ, MODE, FULL, SCALE, RV, KW>::Tile ta, tb, tc, td;
+    typename CbLine<HORIZ, MODE, FULL, SCALE, RV, KW, CPW>::Tile ta, tb, tc, td;
     if constexpr (CbCfg<HORIZ, MODE, KW>::PF == 3) {
         L.load(ta, 0);
         L.load(tb, T);
@@ -802,11 +846,12 @@ __global__ __launch_bounds__(64 * KW * WPB) void k_cbca(const CbcaArgs a, const 
 
 template <bool HORIZ, int MODE, bool SCALE, int KW, int WPB = 1>
 static void launch_kw(const CbcaArgs& a, int n, hipStream_t st) {
-    const int nchunks = (a.D + 63) / 64;
-    const int groups = ((HORIZ ? a.H : a.W) + KW * WPB - 1) / (KW * WPB);
+    constexpr int CPW = cbca_cpw(HORIZ, MODE, KW, WPB);
+    const int nchunks = (a.D + 64 / CPW - 1) / (64 / CPW);
+    const int groups = ((HORIZ ? a.H : a.W) + KW * WPB * CPW - 1) / (KW * WPB * CPW);
     const int nlines = groups * nchunks * n;
     const size_t shm = 4 * (size_t)(KW > 1 ? cbca_smem_words_vg(a.lag, MODE, KW) : WPB * cbca_smem_words(a.lag, HORIZ, MODE));
-    const bool full = a.D % 64 == 0;
+    const bool full = a.D % (64 / CPW) == 0 && (HORIZ || a.W % CPW == 0);
     constexpr bool PERSIST = !HORIZ && KW == 1 && WPB == 1 && SM_CB_PERSIST_V;
     int nblk = nlines;
     if (PERSIST) {

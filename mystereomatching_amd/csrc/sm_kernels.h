@@ -27,6 +27,7 @@ struct PrepArgs {
     int H, W, rv, ru, ring;
     int L, L_out, C_D, C_D_out, minL, cor_thres;
     int do_census, do_grad, do_arms, do_flags;
+    int pack_px;                // the packed-BGR plane px is read later (GF, so, refine)
 };
 
 struct CostArgs {

@@ -163,6 +163,140 @@ constexpr uint32_t PREP_OUT = 0xffffffffu;   // fused regions: a pixel outside t
 #ifndef SM_PREP_PROBE
 #define SM_PREP_PROBE 0   // timing probes: 1 = no arms, 2 = no census, 3 = neither (results wrong)
 #endif
+// census code (genCensusCode_NC_Sur, h:867-934) and x/y gradients of one pixel; g = the pixel in
+// the block's gray tile (row stride gw, REFLECT_101 halo of max(rv, 1) rows / max(ru, 1) columns)
+template <int TRV, int TRU, int TRING>
+__device__ __forceinline__ void prep_census_grad(const PrepArgs& a, const uint8_t* g, int gw, int rv, int ru, int ring,
+                                                 int u, int v, size_t o) {
+    const int H = a.H, W = a.W;
+    if (TRV >= 0 && a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
+        // compile-time geometry: every bit's position is a constant, so the bits go into four
+        // 32-bit accumulators (acc = 2 acc + bit: a compare and an add-with-carry per bit)
+        // instead of a 64-bit shift register; the words are then assembled exactly as the
+        // reference's 64-bit chunks (MSB first, a partial last chunk in the low bits)
+        const int c = g[0];
+        uint32_t acc[4] = {0, 0, 0, 0};
+        int k = 0;
+#pragma unroll
+        for (int dv = -rv; dv <= rv; dv++)
+#pragma unroll
+            for (int du = -ru; du <= ru; du++, k++)
+                acc[k >> 5] = acc[k >> 5] + acc[k >> 5] + (uint32_t)(c < (int)g[dv * gw + du]);
+        if (ring) {
+            const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
+            const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
+#pragma unroll
+            for (int i = 0; i < 8; i++, k++)
+                acc[k >> 5] = acc[k >> 5] + acc[k >> 5] +
+                              (uint32_t)((int)g[dvs[i] * gw + dus[i]] < (int)g[dvs[i + 1] * gw + dus[i + 1]]);
+        }
+        const int nb0 = k < 64 ? k : 64, nb1 = k - nb0;   // bits of chunk 0 and chunk 1
+        const uint64_t w0 = nb0 > 32 ? ((uint64_t)acc[0] << (nb0 - 32)) | acc[1] : acc[0];
+        const uint64_t w1 = nb1 > 32 ? ((uint64_t)acc[2] << (nb1 - 32)) | acc[3] : acc[2];
+        a.code[o] = make_ulonglong2(w0, w1);
+    } else if (a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
+        const int c = g[0];
+        uint64_t w[2] = {0, 0};
+        uint64_t cs = 0;
+        int step = 0, dep = 0;
+#pragma unroll
+        for (int dv = -rv; dv <= rv; dv++)
+#pragma unroll
+            for (int du = -ru; du <= ru; du++) {
+                if (step > 63) {
+                    w[dep & 1] = cs;
+                    cs = 0;
+                    step = 0;
+                    dep++;
+                }
+                cs <<= 1;
+                if (c - (int)g[dv * gw + du] < 0) cs++;
+                step++;
+            }
+        if (ring) {
+            const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
+            const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int pre = g[dvs[i] * gw + dus[i]], aft = g[dvs[i + 1] * gw + dus[i + 1]];
+                if (step > 63) {
+                    w[dep & 1] = cs;
+                    cs = 0;
+                    step = 0;
+                    dep++;
+                }
+                cs <<= 1;
+                if (pre - aft < 0) cs++;
+                step++;
+            }
+        }
+        if (step > 0) w[dep & 1] = cs;
+        a.code[o] = make_ulonglong2(w[0], w[1]);
+    }
+    // gradients (calGrad / calGrad_y single-channel, cpp:271-350); the one-sided border
+    // differences only touch interior rows/cols, so the reflected halo never enters them
+    if (a.do_grad) {
+        float gxv, gyv;
+        if (u == 0)
+            gxv = (float)(g[1] - g[0]);
+        else if (u == W - 1)
+            gxv = (float)(g[0] - g[-1]);
+        else
+            gxv = 0.5f * (float)(g[1] - g[-1]);
+        if (v == 0)
+            gyv = (float)(g[gw] - g[0]);
+        else if (v == H - 1)
+            gyv = (float)(g[0] - g[-gw]);
+        else
+            gyv = 0.5f * (float)(g[gw] - g[-gw]);
+        a.gx[o] = gxv;
+        a.gy[o] = gyv;
+    }
+}
+
+// One arm walk over an LDS strip of arm-walk words (calHorVerDis, cpp:2959-3050): sp = the centre
+// pixel's word, sst = the step between words, fb = the C_D flag bit of this direction, (ca, cb) the
+// centre's guard-bit operands for steps <= Lin (C_D) and beyond (C_D_out).  Returns the first step
+// that fails (1 .. Lo + 1).
+__device__ __forceinline__ int strip_walk(const uint32_t* sp, int sst, uint32_t fb, uint32_t ca1, uint32_t cb1, uint32_t ca2,
+                                          uint32_t cb2, int Lin, int Lo) {
+    const uint32_t want = ARM_B9 | fb;
+    auto pass = [&](uint32_t p, uint32_t ca, uint32_t cb) { return ((((ca - p) & ~(cb - p)) & ARM_B9) | (p & fb)) == want; };
+    int arm = 1;
+#if SM_PREP_WALK > 1
+    // chunks of SM_PREP_WALK steps: a chunk's LDS reads are issued together, then its first
+    // failing step (or Lo + 1) ends the walk
+    for (;;) {
+        uint32_t pw[SM_PREP_WALK];
+#pragma unroll
+        for (int j = 0; j < SM_PREP_WALK; j++) pw[j] = sp[min(arm + j, Lo) * sst];
+        int ff = SM_PREP_WALK;
+#pragma unroll
+        for (int j = SM_PREP_WALK - 1; j >= 0; j--) {
+            const int st = arm + j;
+            const bool in1 = st <= Lin;
+            if (st > Lo || !pass(pw[j], in1 ? ca1 : ca2, in1 ? cb1 : cb2)) ff = j;
+        }
+        arm += ff;
+        if (ff < SM_PREP_WALK) break;
+    }
+#else
+    for (; arm <= Lin; arm++)
+        if (!pass(sp[arm * sst], ca1, cb1)) break;
+    if (arm > Lin)
+        for (; arm <= Lo; arm++)
+            if (!pass(sp[arm * sst], ca2, cb2)) break;
+#endif
+    return arm;
+}
+// The arm length kept from a walk that failed at step `arm` (cpp:3035-3046): the walked length
+// when it reaches minL, else the longest length <= minL that stays inside the image.
+__device__ __forceinline__ int arm_final(int arm, int minL, int u, int v, int du, int dv, int W, int H) {
+    if (--arm >= minL) return arm;
+    for (int len = minL; len >= 0; len--)
+        if (u + len * du >= 0 && u + len * du <= W - 1 && v + len * dv >= 0 && v + len * dv <= H - 1) return len;
+    return 0;
+}
 // TRV/TRU/TRING >= 0: census geometry fixed at compile time (the default 7 x 9 window with the
 // ring bits), so the bit loop unrolls into straight-line compares with immediate LDS offsets;
 // -1: the runtime geometry.  STRIPS: arm walks over the LDS strips (else over global memory).
@@ -323,93 +457,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         const int u = u0 + x, v = v0 + yy;
         if (u >= W || v >= H) continue;
         const size_t o = img * npix + (size_t)v * W + u;
-        // census (genCensusCode_NC_Sur, h:867-934)
-        if (TRV >= 0 && a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
-            // compile-time geometry: every bit's position is a constant, so the bits go into four
-            // 32-bit accumulators (acc = 2 acc + bit: a compare and an add-with-carry per bit)
-            // instead of a 64-bit shift register; the words are then assembled exactly as the
-            // reference's 64-bit chunks (MSB first, a partial last chunk in the low bits)
-            const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
-            const int c = g[0];
-            uint32_t acc[4] = {0, 0, 0, 0};
-            int k = 0;
-#pragma unroll
-            for (int dv = -rv; dv <= rv; dv++)
-#pragma unroll
-                for (int du = -ru; du <= ru; du++, k++)
-                    acc[k >> 5] = acc[k >> 5] + acc[k >> 5] + (uint32_t)(c < (int)g[dv * gw + du]);
-            if (ring) {
-                const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
-                const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
-#pragma unroll
-                for (int i = 0; i < 8; i++, k++)
-                    acc[k >> 5] = acc[k >> 5] + acc[k >> 5] +
-                                  (uint32_t)((int)g[dvs[i] * gw + dus[i]] < (int)g[dvs[i + 1] * gw + dus[i + 1]]);
-            }
-            const int nb0 = k < 64 ? k : 64, nb1 = k - nb0;   // bits of chunk 0 and chunk 1
-            const uint64_t w0 = nb0 > 32 ? ((uint64_t)acc[0] << (nb0 - 32)) | acc[1] : acc[0];
-            const uint64_t w1 = nb1 > 32 ? ((uint64_t)acc[2] << (nb1 - 32)) | acc[3] : acc[2];
-            a.code[o] = make_ulonglong2(w0, w1);
-        } else if (a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
-            const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
-            const int c = g[0];
-            uint64_t w[2] = {0, 0};
-            uint64_t cs = 0;
-            int step = 0, dep = 0;
-#pragma unroll
-            for (int dv = -rv; dv <= rv; dv++)
-#pragma unroll
-                for (int du = -ru; du <= ru; du++) {
-                    if (step > 63) {
-                        w[dep & 1] = cs;
-                        cs = 0;
-                        step = 0;
-                        dep++;
-                    }
-                    cs <<= 1;
-                    if (c - (int)g[dv * gw + du] < 0) cs++;
-                    step++;
-                }
-            if (ring) {
-                const int dvs[9] = {-1, -1, -1, 0, 1, 1, 1, 0, -1};
-                const int dus[9] = {-1, 0, 1, 1, 1, 0, -1, -1, -1};
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int pre = g[dvs[i] * gw + dus[i]], aft = g[dvs[i + 1] * gw + dus[i + 1]];
-                    if (step > 63) {
-                        w[dep & 1] = cs;
-                        cs = 0;
-                        step = 0;
-                        dep++;
-                    }
-                    cs <<= 1;
-                    if (pre - aft < 0) cs++;
-                    step++;
-                }
-            }
-            if (step > 0) w[dep & 1] = cs;
-            a.code[o] = make_ulonglong2(w[0], w[1]);
-        }
-        // gradients (calGrad / calGrad_y single-channel, cpp:271-350); the one-sided border
-        // differences only touch interior rows/cols, so the reflected halo never enters them
-        if (a.do_grad) {
-            const uint8_t* g = gt + (yy + hv) * gw + (x + hu);
-            float gxv, gyv;
-            if (u == 0)
-                gxv = (float)(g[1] - g[0]);
-            else if (u == W - 1)
-                gxv = (float)(g[0] - g[-1]);
-            else
-                gxv = 0.5f * (float)(g[1] - g[-1]);
-            if (v == 0)
-                gyv = (float)(g[gw] - g[0]);
-            else if (v == H - 1)
-                gyv = (float)(g[0] - g[-gw]);
-            else
-                gyv = 0.5f * (float)(g[gw] - g[-gw]);
-            a.gx[o] = gxv;
-            a.gy[o] = gyv;
-        }
+        prep_census_grad<TRV, TRU, TRING>(a, gt + (yy + hv) * gw + (x + hu), gw, rv, ru, ring, u, v, o);
         const uint32_t* pc = P + (size_t)v * W + u;
         // cross arms (calHorVerDis 7-arg, cpp:2959-3050), direction order L, R, U, D; the walks
         // read the packed image (lanes = consecutive pixels, so every step is one coalesced load)
@@ -430,37 +478,9 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
                 const int dv = direc == 2 ? -1 : (direc == 3 ? 1 : 0);
                 int arm = 1;
                 if (STRIPS) {
-                    const uint32_t* sp = direc < 2 ? hc : vc;
-                    const int sst = direc == 0 ? -1 : (direc == 1 ? 1 : (direc == 2 ? -PREP_TX : PREP_TX));
                     const uint32_t fb = (direc == 0 || direc == 2) ? (1u << 30) : (1u << 31);
-                    const uint32_t want = ARM_B9 | fb;
-                    auto pass = [&](uint32_t p, uint32_t ca, uint32_t cb) {
-                        return ((((ca - p) & ~(cb - p)) & ARM_B9) | (p & fb)) == want;
-                    };
-#if SM_PREP_WALK > 1
-                    // chunks of SM_PREP_WALK steps: a chunk's LDS reads are issued together, then
-                    // its first failing step (or Lo + 1) ends the walk
-                    for (;;) {
-                        uint32_t pw[SM_PREP_WALK];
-#pragma unroll
-                        for (int j = 0; j < SM_PREP_WALK; j++) pw[j] = sp[min(arm + j, Lo) * sst];
-                        int ff = SM_PREP_WALK;
-#pragma unroll
-                        for (int j = SM_PREP_WALK - 1; j >= 0; j--) {
-                            const int st = arm + j;
-                            const bool in1 = st <= Lin;
-                            if (st > Lo || !pass(pw[j], in1 ? ca1 : ca2, in1 ? cb1 : cb2)) ff = j;
-                        }
-                        arm += ff;
-                        if (ff < SM_PREP_WALK) break;
-                    }
-#else
-                    for (; arm <= Lin; arm++)
-                        if (!pass(sp[arm * sst], ca1, cb1)) break;
-                    if (arm > Lin)
-                        for (; arm <= Lo; arm++)
-                            if (!pass(sp[arm * sst], ca2, cb2)) break;
-#endif
+                    arm = strip_walk(direc < 2 ? hc : vc, direc == 0 ? -1 : (direc == 1 ? 1 : (direc == 2 ? -PREP_TX : PREP_TX)),
+                                     fb, ca1, cb1, ca2, cb2, Lin, Lo);
                 } else {
                     const int off = dv * W + du;
                     uint32_t prev = center;
@@ -474,23 +494,232 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
                         prev = cur;
                     }
                 }
-                int outv = 0;
-                if (--arm >= a.minL)
-                    outv = arm;
-                else {
-                    for (int len = a.minL; len >= 0; len--)
-                        if (u + len * du >= 0 && u + len * du <= W - 1 && v + len * dv >= 0 && v + len * dv <= H - 1) {
-                            outv = len;
-                            break;
-                        }
-                }
-                packed |= (uint32_t)outv << (8 * direc);
+                packed |= (uint32_t)arm_final(arm, a.minL, u, v, du, dv, W, H) << (8 * direc);
             }
             // two u16-pair planes: (L | R << 16) and (U | D << 16)
             uint32_t* planes = (uint32_t*)a.arms + img * 2 * npix + (size_t)v * W + u;
             planes[0] = (packed & 0xffu) | ((packed >> 8 & 0xffu) << 16);
             planes[npix] = (packed >> 16 & 0xffu) | ((packed >> 24) << 16);
         }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Split prep (SM_PREP_SPLIT): two kernels that make the arm-walk words in LDS from the colour
+// bytes, so no packed plane (px / pxh / pxv) goes through HBM, and whose tiles are long along
+// their walk axis, so the walk halo is re-read 1.3-2.1 times instead of the 16-row tile's 5.3:
+//   k_prep_h  tiles of 256 columns x 4 rows: census, gradients, the SGM penalty flags and the
+//             L / R arms (arm plane 0), from a gray tile and a strip of packed pixels (rows
+//             v0 - 1 .. v0 + 4, columns u0 - Lo - 1 .. u0 + 256 + Lo);
+//   k_prep_v  tiles of 64 columns x 64 rows: the U / D arms (arm plane 1) from a strip of rows
+//             v0 - Lo - 1 .. v0 + 64 + Lo.
+// The packed-BGR plane is made (k_pack_bgr) only for the kernels that read it (GF, so, refine).
+// ---------------------------------------------------------------------------------------
+#ifndef SM_PREP_SPLIT
+#define SM_PREP_SPLIT 0   // (until validated on the GPU)
+#endif
+constexpr int PH_TW = 256, PH_TH = 4, PV_TW = 64, PV_TH = 64;
+__host__ __device__ inline int preph_gray_bytes(int rv, int ru) {
+    const int hv = rv > 1 ? rv : 1, hu = ru > 1 ? ru : 1;
+    return ((PH_TW + 2 * hu) * (PH_TH + 2 * hv) + 15) / 16 * 16;
+}
+__host__ __device__ inline int preph_hc(int Lo) { return PH_TW + 2 * Lo + 2; }
+__host__ __device__ inline int preph_bytes(int rv, int ru, int Lo) { return preph_gray_bytes(rv, ru) + 4 * (PH_TH + 2) * preph_hc(Lo); }
+__host__ __device__ inline int prepv_bytes(int Lo) { return 4 * (PV_TH + 2 * Lo + 2) * PV_TW; }
+
+// packed pixel (pack10) of image pixel (vv, uu) from the colour bytes, PREP_OUT outside the image
+__device__ __forceinline__ uint32_t pack10_at(const uint8_t* bgr, int vv, int uu, int H, int W) {
+    if ((unsigned)vv >= (unsigned)H || (unsigned)uu >= (unsigned)W) return PREP_OUT;
+    const uint8_t* q = bgr + ((size_t)vv * W + uu) * 3;
+    return (uint32_t)q[0] | ((uint32_t)q[1] << 10) | ((uint32_t)q[2] << 20);
+}
+// arm-walk word of packed pixel p (k_pack_arms): bit 30 / 31 = its C_D test against the walk's
+// previous pixel nb30 / nb31 (the neighbour towards the walk's start); 0 outside the image
+__device__ __forceinline__ uint32_t walk_word(uint32_t p, uint32_t nb30, uint32_t nb31, uint32_t ka, uint32_t kb) {
+    if (p == PREP_OUT) return 0u;
+    uint32_t w = p;
+    if (nb30 != PREP_OUT && ok10(p, nb30, ka, kb)) w |= 1u << 30;
+    if (nb31 != PREP_OUT && ok10(p, nb31, ka, kb)) w |= 1u << 31;
+    return w;
+}
+// tile fill with the loads of FB entries per thread issued before any of them is stored
+template <typename T, typename F>
+__device__ __forceinline__ void prep_fill(T* dst, int count, F&& load) {
+    constexpr int FB = 8;
+    for (int i0 = 0; i0 < count; i0 += FB * 256) {
+        uint32_t r[FB];
+#pragma unroll
+        for (int k = 0; k < FB; k++) {
+            const int i = i0 + k * 256 + (int)threadIdx.x;
+            r[k] = i < count ? load(i) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < FB; k++) {
+            const int i = i0 + k * 256 + (int)threadIdx.x;
+            if (i < count) dst[i] = (T)r[k];
+        }
+    }
+}
+
+template <int TRV, int TRU, int TRING>
+__global__ __launch_bounds__(256) void k_prep_h(const PrepArgs a) {
+    extern __shared__ __align__(16) unsigned char prep_raw[];
+    const int H = a.H, W = a.W, Lo = a.do_arms ? a.L_out : 0;
+    const int rv = TRV >= 0 ? TRV : a.rv, ru = TRU >= 0 ? TRU : a.ru;
+    const int ring = TRING >= 0 ? TRING : a.ring;
+    const int u0 = blockIdx.x * PH_TW, v0 = blockIdx.y * PH_TH;
+    const int b = blockIdx.z >> 1, view = blockIdx.z & 1;
+    const size_t npix = (size_t)H * W;
+    const size_t img = (size_t)b * 2 + view;
+    const int tid = threadIdx.x;
+    const int hv = max(rv, 1), hu = max(ru, 1);
+    const int gw = PH_TW + 2 * hu, gh = PH_TH + 2 * hv;
+    uint8_t* gt = prep_raw;
+    const bool words = a.do_arms && SM_PREP_PROBE != 1 && SM_PREP_PROBE != 3;
+    const bool flags = a.do_flags && (view == 0 || a.flags1);
+    if (a.do_census || a.do_grad) {
+        const uint8_t* G = a.gray + img * npix;
+        prep_fill(gt, gw * gh, [&](int i) -> uint32_t {
+            const int ty = i / gw, tx = i - ty * gw;
+            return G[(size_t)reflect101(v0 - hv + ty, H) * W + reflect101(u0 - hu + tx, W)];
+        });
+    }
+    const int hc = preph_hc(Lo);
+    uint32_t* PH = (uint32_t*)(prep_raw + preph_gray_bytes(rv, ru));   // [PH_TH + 2][hc]
+    if (words || flags) {
+        const uint8_t* C = a.bgr + img * npix * 3;
+        const float rinv = 1.0f / (float)hc;   // row by a float reciprocal (exact for i < 2^22)
+        prep_fill(PH, (PH_TH + 2) * hc, [&](int i) -> uint32_t {
+            const int r = (int)(((float)i + 0.5f) * rinv);
+            return pack10_at(C, v0 - 1 + r, u0 - Lo - 1 + (i - r * hc), H, W);
+        });
+    }
+    __syncthreads();
+    if (flags) {   // SGM penalty flags (updateCost, h:2223-2229) from the packed pixels and their rim
+        const int tf = min(max(a.cor_thres, -1), 255);
+        const uint32_t fa = (uint32_t)(512 + tf) * ARM_M, fb = (uint32_t)(511 - tf) * ARM_M;
+        const int u = u0 + tid;
+        // directions 0..7: (rv, ru) = (+1,0) (-1,0) (0,+1) (0,-1) (+1,-1) (+1,+1) (-1,+1) (-1,-1)
+        const int offs[8] = {hc, -hc, 1, -1, hc - 1, hc + 1, 1 - hc, -1 - hc};
+#pragma unroll
+        for (int yy = 0; yy < PH_TH; yy++) {
+            const int v = v0 + yy;
+            if (u >= W || v >= H) continue;
+            const uint32_t* q = PH + (yy + 1) * hc + tid + Lo + 1;
+            const uint32_t c = q[0];
+            uint32_t fl = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t nb = q[offs[k]];
+                if (nb != PREP_OUT && !ok10(c, nb, fa, fb)) fl |= 1u << k;
+            }
+            (view == 0 ? a.flags : a.flags1)[(size_t)b * npix + (size_t)v * W + u] = (uint8_t)fl;
+        }
+    }
+    if (words) {
+        // the walk rows' words, computed into registers and written over the packed pixels after
+        // every thread has read its neighbours
+        const int tc = min(max(a.C_D, -1), 255);
+        const uint32_t ka = (uint32_t)(512 + tc) * ARM_M, kb = (uint32_t)(511 - tc) * ARM_M;
+        constexpr int MH = (PH_TH * (PH_TW + 128) + 255) / 256;   // Lo <= 64
+        const int nw = hc - 2, nh = PH_TH * nw;
+        const float winv = 1.0f / (float)nw;
+        uint32_t wh[MH];
+#pragma unroll
+        for (int m = 0; m < MH; m++) {
+            const int i = m * 256 + tid;
+            if (i < nh) {
+                const int r = (int)(((float)i + 0.5f) * winv);
+                const uint32_t* q = PH + (r + 1) * hc + (i - r * nw) + 1;
+                wh[m] = walk_word(q[0], q[1], q[-1], ka, kb);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < MH; m++) {
+            const int i = m * 256 + tid;
+            if (i < nh) {
+                const int r = (int)(((float)i + 0.5f) * winv);
+                PH[(r + 1) * hc + (i - r * nw) + 1] = wh[m];
+            }
+        }
+        __syncthreads();
+    }
+    const int u = u0 + tid;
+    if (u >= W) return;
+    const int t1 = min(max(a.C_D, -1), 255), t2 = min(max(a.C_D_out, -1), 255);
+    const int Lin = min(a.L, Lo);
+#pragma unroll 1
+    for (int yy = 0; yy < PH_TH; yy++) {
+        const int v = v0 + yy;
+        if (v >= H) break;
+        const size_t o = img * npix + (size_t)v * W + u;
+        prep_census_grad<TRV, TRU, TRING>(a, gt + (yy + hv) * gw + (tid + hu), gw, rv, ru, ring, u, v, o);
+        if (words) {   // L and R arms (calHorVerDis 7-arg, cpp:2959-3050): arm plane 0 = L | R << 16
+            const uint32_t* q = PH + (yy + 1) * hc + tid + Lo + 1;
+            const uint32_t cf = q[0] & 0x3fffffffu;
+            const uint32_t ca1 = cf + (uint32_t)(512 + t1) * ARM_M, cb1 = cf + (uint32_t)(511 - t1) * ARM_M;
+            const uint32_t ca2 = cf + (uint32_t)(512 + t2) * ARM_M, cb2 = cf + (uint32_t)(511 - t2) * ARM_M;
+            const int al = arm_final(strip_walk(q, -1, 1u << 30, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, -1, 0, W, H);
+            const int ar = arm_final(strip_walk(q, 1, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, 1, 0, W, H);
+            ((uint32_t*)a.arms)[img * 2 * npix + (size_t)v * W + u] = (uint32_t)al | ((uint32_t)ar << 16);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_prep_v(const PrepArgs a) {
+    extern __shared__ __align__(16) unsigned char prep_raw[];
+    const int H = a.H, W = a.W, Lo = a.L_out;
+    const int u0 = blockIdx.x * PV_TW, v0 = blockIdx.y * PV_TH;
+    const int b = blockIdx.z >> 1, view = blockIdx.z & 1;
+    const size_t npix = (size_t)H * W;
+    const size_t img = (size_t)b * 2 + view;
+    const int tid = threadIdx.x;
+    uint32_t* PV = (uint32_t*)prep_raw;   // [PV_TH + 2 Lo + 2][PV_TW]: rows v0 - Lo - 1 ..
+    const uint8_t* C = a.bgr + img * npix * 3;
+    prep_fill(PV, (PV_TH + 2 * Lo + 2) * PV_TW,
+              [&](int i) -> uint32_t { return pack10_at(C, v0 - Lo - 1 + (i >> 6), u0 + (i & 63), H, W); });
+    __syncthreads();
+    {
+        const int tc = min(max(a.C_D, -1), 255);
+        const uint32_t ka = (uint32_t)(512 + tc) * ARM_M, kb = (uint32_t)(511 - tc) * ARM_M;
+        constexpr int MV = ((PV_TH + 128) * PV_TW + 255) / 256;   // Lo <= 64
+        const int nv = (PV_TH + 2 * Lo) * PV_TW;
+        uint32_t wv[MV];
+#pragma unroll
+        for (int m = 0; m < MV; m++) {
+            const int i = m * 256 + tid;
+            if (i < nv) {
+                const uint32_t* q = PV + PV_TW + i;
+                wv[m] = walk_word(q[0], q[PV_TW], q[-PV_TW], ka, kb);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < MV; m++) {
+            const int i = m * 256 + tid;
+            if (i < nv) PV[PV_TW + i] = wv[m];
+        }
+        __syncthreads();
+    }
+    const int x = tid & 63, u = u0 + x;
+    if (u >= W) return;
+    const int t1 = min(max(a.C_D, -1), 255), t2 = min(max(a.C_D_out, -1), 255);
+    const int Lin = min(a.L, Lo);
+    uint32_t* plane1 = (uint32_t*)a.arms + img * 2 * npix + npix;
+#pragma unroll 1
+    for (int yy = tid >> 6; yy < PV_TH; yy += 4) {
+        const int v = v0 + yy;
+        if (v >= H) break;
+        // U and D arms: arm plane 1 = U | D << 16
+        const uint32_t* q = PV + (yy + Lo + 1) * PV_TW + x;
+        const uint32_t cf = q[0] & 0x3fffffffu;
+        const uint32_t ca1 = cf + (uint32_t)(512 + t1) * ARM_M, cb1 = cf + (uint32_t)(511 - t1) * ARM_M;
+        const uint32_t ca2 = cf + (uint32_t)(512 + t2) * ARM_M, cb2 = cf + (uint32_t)(511 - t2) * ARM_M;
+        const int au = arm_final(strip_walk(q, -PV_TW, 1u << 30, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, 0, -1, W, H);
+        const int ad = arm_final(strip_walk(q, PV_TW, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, 0, 1, W, H);
+        plane1[(size_t)v * W + u] = (uint32_t)au | ((uint32_t)ad << 16);
     }
 }
 
@@ -513,7 +742,26 @@ static void launch_prep_g(const PrepArgs& a, dim3 grid, size_t shm, bool strips,
         hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, false, false>), grid, dim3(256), shm, st, a);
 }
 
+static void launch_prep_split(const PrepArgs& a, int n, hipStream_t st) {
+    const int Lo = a.do_arms ? a.L_out : 0;
+    const dim3 gh((a.W + PH_TW - 1) / PH_TW, (a.H + PH_TH - 1) / PH_TH, 2 * n);
+    const size_t shh = (size_t)preph_bytes(a.rv, a.ru, Lo);
+    if (a.rv == 3 && a.ru == 4 && a.ring == 1)   // the reference's default census window (cpp:815)
+        hipLaunchKernelGGL((k_prep_h<3, 4, 1>), gh, dim3(256), shh, st, a);
+    else
+        hipLaunchKernelGGL((k_prep_h<-1, -1, -1>), gh, dim3(256), shh, st, a);
+    if (a.do_arms)
+        hipLaunchKernelGGL(k_prep_v, dim3((a.W + PV_TW - 1) / PV_TW, (a.H + PV_TH - 1) / PV_TH, 2 * n), dim3(256),
+                           (size_t)prepv_bytes(a.L_out), st, a);
+}
+
 void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
+    const bool strips = a.do_arms && prep_strips(a.L_out);
+    const bool split = SM_PREP_SPLIT && (strips || !a.do_arms);
+    if (split && !a.pack_px) {
+        launch_prep_split(a, n, st);
+        return;
+    }
     const size_t total = (size_t)n * 2 * a.H * a.W;
     size_t blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
@@ -527,7 +775,10 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
     } else {
         hipLaunchKernelGGL(k_pack_bgr, dim3((unsigned)blocks), dim3(256), 0, st, a.bgr, a.px, total);
     }
-    const bool strips = a.do_arms && prep_strips(a.L_out);
+    if (split) {
+        launch_prep_split(a, n, st);
+        return;
+    }
     const bool fused = strips && SM_PREP_FUSED;   // words and flags made inside k_prep
     if (!fused && (strips || a.do_flags))   // arm-walk planes and the SGM penalty flags
         hipLaunchKernelGGL(k_pack_arms, dim3((a.W + 255) / 256, (a.H + SM_PACK_ROWS - 1) / SM_PACK_ROWS, 2 * n), dim3(256), 0,

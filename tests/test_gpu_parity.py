@@ -185,6 +185,30 @@ def test_arm_parameters(oracle, L, L_out, cT, cT_out, minL):
     np.testing.assert_array_equal(bits(sm.vm[0]), bits(ref["agg"]))
 
 
+@pytest.mark.parametrize("H,W,L_out", [(5, 300, 34), (140, 70, 34), (67, 513, 64), (130, 260, 17), (66, 257, 0)])
+def test_prep_tiles_arms_codes_flags(oracle, H, W, L_out):
+    """The split prep (k_prep_h: 256 x 4 tiles, k_prep_v: 64 x 64 tiles) across several tiles in
+    both directions: census codes and arms of both views, and the SGM penalty flags of all eight
+    directions through the final 8-path volume."""
+    md = 15
+    pair = S.make_pair(H, W, md + 1, 70 + H)
+    for k in ("lbgr", "rbgr"):   # flat and textured regions: arms of every length
+        pair[k][: H // 2] = (pair[k][: H // 2] // 96 * 96).astype(np.uint8)
+    pair["lgray"], pair["rgray"] = S.bgr_to_gray(pair["lbgr"]), S.bgr_to_gray(pair["rbgr"])
+    L = min(17, L_out)
+    cfg = oracle.config(H, W, md, sgm_paths=8, arm_L=L, arm_L_out=L_out)
+    sm = make_sm(pair, md, paths=8, cbca_crossL=[L, 0, 0], cbca_crossL_out=[L_out, 0, 0])
+    sm.costCalculate()
+    for view, g, c in ((0, "lgray", "lbgr"), (1, "rgray", "rbgr")):
+        np.testing.assert_array_equal(sm.census_codes(view), oracle.census(pair[g], cfg))
+        np.testing.assert_array_equal(sm.HVL[view], oracle.arms(pair[c], cfg))
+    ref = oracle.run(pair, cfg, dumps=True)
+    np.testing.assert_array_equal(bits(sm.vm[0]), bits(ref["agg"]))
+    _, agg, final, dp = run_reference_order(pair, md, paths=8, cbca_crossL=[L, 0, 0], cbca_crossL_out=[L_out, 0, 0])
+    np.testing.assert_array_equal(bits(final), bits(ref["final"]))
+    np.testing.assert_array_equal(dp, ref["disp"])
+
+
 @pytest.mark.parametrize("H,W,md,paths", [(2, 2, 0, 4), (3, 70, 63, 4), (70, 3, 5, 8), (17, 23, 64, 8),
                                           (25, 31, 127, 4), (13, 90, 191, 8), (9, 40, 255, 4),
                                           (11, 37, 199, 8), (7, 30, 130, 4)])

@@ -1,5 +1,6 @@
-"""GPU: the two-pass 4-path SGM (sm_sgm2.hip, sm_params.sgm_2pass = 1, the default for D = 64 / 128 /
-256) against the oracle and against the four path sweeps (sgm_2pass = 0), bit for bit.
+"""GPU: the two-pass 4-path SGM (sm_sgm2.hip, opt-in through sm_params.sgm_2pass = 1 for D = 64 / 128 /
+256: measured slower than the four path sweeps) against the oracle and against the four
+path sweeps (sgm_2pass = 0, the default), bit for bit.
 
 Pass A computes the paths r = (+1,0) and (0,+1) (L0, L2), pass B the paths (-1,0) and (0,-1)
 (L1, L3), the sum (((0 + L0) + L1) + L2) + L3 and the WTA (sgm / costScan / gen_sgm_vm /

@@ -1,0 +1,21 @@
+#!/bin/bash
+# CBCA V sweeps with CPW columns per wave (SM_CB_CPW_*_V): parity of the variants (the CBCA GPU
+# tests through SM_HIP_LIB), then same-process A/B at full resolution and Teddy x16.
+set -o pipefail
+O=gpurun_out/${1:-ab_cpw}
+mkdir -p $O
+for v in cpw2 cpw4nb; do
+  SM_HIP_LIB=$PWD/tools/abvar/libsm_hip_$v.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_gpu_parity.py tests/test_gpu_large_fixtures.py > $O/tests_$v.log 2>&1 || { tail -30 $O/tests_$v.log; exit 1; }
+  tail -1 $O/tests_$v.log
+done
+# (six full-resolution instances of 2 pairs = 148 GB of HBM)
+timeout -k 10 400 python tools/ab_inproc.py --workload fullres --rounds 5 --steps 3 --copies 2 --kernels cbca_v,step \
+  base cpw2 cpw4nb > $O/fullres.txt 2>&1 \
+ && tail -4 $O/fullres.txt \
+ && timeout -k 10 400 python tools/ab_inproc.py --workload fullres --rounds 5 --steps 3 --copies 2 --kernels cbca_v,step \
+  base cpw2b ns12:fuse_norm_scan=1 > $O/fullres2.txt 2>&1 \
+ && tail -4 $O/fullres2.txt \
+ && timeout -k 10 300 python tools/ab_inproc.py --workload teddy --rounds 8 --steps 10 --copies 2 --kernels cbca_v \
+  base cpw2 cpw2b cpw4n cpw4nb > $O/teddy.txt 2>&1 \
+ && tail -7 $O/teddy.txt

@@ -37,6 +37,12 @@ namespace {
 
 constexpr int GC_R = 9;              // gf_r[0] (h:297)
 constexpr int GC_K = 2 * GC_R + 1;   // box size
+#ifndef SM_GFCV_RING
+#define SM_GFCV_RING 1   // column sweeps keep the window's row sums in a register ring (k_gfcv_cols)
+#endif
+#ifndef SM_GFCV_PF
+#define SM_GFCV_PF 3     // rows of row sums prefetched ahead by the ring form (divides 18)
+#endif
 
 // OpenCV borderInterpolate(BORDER_REFLECT) for len >= GC_R (one reflection suffices)
 __device__ __forceinline__ int refl(int p, int len) { return p < 0 ? -p - 1 : (p >= len ? 2 * len - 1 - p : p); }
@@ -279,7 +285,108 @@ __global__ __launch_bounds__(64) void k_gfcv_cols(const GfCvArgs a) {
     const uint32_t* gw = a.px + (size_t)b * a.px_pair_stride + u;
     const double scale = 1. / (GC_K * GC_K);
 
+    // output row y from the box means m (MODE 0: alpha, beta -> AB; MODE 1: q -> vm)
+    auto emit = [&](int y, const float (&m)[4]) {
+        const size_t po = (size_t)y * W;
+        const size_t e = col0 - dd + d + (size_t)y * rstep;
+        if (MODE == 0) {
+            const float mI[3] = {pix[0 * npix + po], pix[1 * npix + po], pix[2 * npix + po]};
+            const float iv[6] = {pix[3 * npix + po], pix[4 * npix + po], pix[5 * npix + po],
+                                 pix[6 * npix + po], pix[7 * npix + po], pix[8 * npix + po]};
+            const float mP = m[0];
+            float cov[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float mm = mP * mI[c];
+                cov[c] = m[1 + c] - mm;
+            }
+            // inverse entry (g, k): 00 01 02 / 01 11 12 / 02 12 22
+            const int IX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+            float al[3];
+#pragma unroll
+            for (int g = 0; g < 3; g++) {
+                float acc = iv[IX[g][0]] * cov[0];
+#pragma unroll
+                for (int k = 1; k < 3; k++) {
+                    const float mm = iv[IX[g][k]] * cov[k];
+                    acc = acc + mm;
+                }
+                al[g] = acc;
+            }
+            float be = mP;
+#pragma unroll
+            for (int g = 0; g < 3; g++) {
+                const float mm = al[g] * mI[g];
+                be = be - mm;
+            }
+            if (live) {
+                ab[0 * ab_plane + e] = al[0];
+                ab[1 * ab_plane + e] = al[1];
+                ab[2 * ab_plane + e] = al[2];
+                ab[3 * ab_plane + e] = be;
+            }
+        } else {
+            const uint32_t w = gw[po];
+            const float I[3] = {(float)(w & 0xffu), (float)((w >> 8) & 0xffu), (float)((w >> 16) & 0xffu)};
+            float q = m[3];   // box(beta)
+#pragma unroll
+            for (int g = 0; g < 3; g++) {
+                const float mm = m[g] * I[g];
+                q = q + mm;
+            }
+            if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
+                float sum = 0.f;
+                sum += a.scale * q;
+                q = sum;
+            }
+            if (live) a.vm[e] = q;
+        }
+    };
     double SUM[4] = {0, 0, 0, 0};
+#if SM_GFCV_RING
+    // The row sums leaving the window (row y - r) are the ones that entered it 2r = 18 rows
+    // earlier: a register ring of 18 rows x 4 channels keeps them, so every RS element is read
+    // once (the tiled form below reads it twice, the second time 18 rows later, past L2).
+    // ring[i] starts as row refl(i - r), the rows the first 18 outputs drop; slot y mod 18.
+    constexpr int RK = GC_K - 1, PF = SM_GFCV_PF;
+    static_assert(RK % PF == 0, "prefetch slots repeat with the ring");
+    double ring[RK][4], nx[PF][4];
+#pragma unroll
+    for (int i = 0; i < RK; i++) {
+        const size_t e = col0 + (size_t)refl(i - GC_R, H) * rstep;
+#pragma unroll
+        for (int c = 0; c < 4; c++) ring[i][c] = rs[c * rs_plane + e];
+    }
+#pragma unroll
+    for (int i = 0; i < RK; i++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) SUM[c] += ring[i][c];
+    auto fetch = [&](double (&x)[4], int y) {
+        const size_t ep = col0 + (size_t)refl(min(y, H - 1) + GC_R, H) * rstep;
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[c] = rs[c * rs_plane + ep];
+    };
+#pragma unroll
+    for (int k = 0; k < PF; k++) fetch(nx[k], k);
+    for (int y0 = 0; y0 < H; y0 += RK) {
+#pragma unroll
+        for (int s = 0; s < RK; s++) {
+            const int y = y0 + s;
+            if (y >= H) break;   // wave-uniform
+            float m[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const double sp = nx[s % PF][c];
+                const double s0 = SUM[c] + sp;
+                m[c] = (float)(s0 * scale);
+                SUM[c] = s0 - ring[s][c];
+                ring[s][c] = sp;
+            }
+            fetch(nx[s % PF], y + PF);
+            emit(y, m);
+        }
+    }
+#else
     for (int i = 0; i < GC_K - 1; i++) {
         const size_t e = col0 + (size_t)refl(i - GC_R, H) * rstep;
 #pragma unroll
@@ -313,60 +420,7 @@ __global__ __launch_bounds__(64) void k_gfcv_cols(const GfCvArgs a) {
                 m[c] = (float)(s0 * scale);
                 SUM[c] = s0 - t.sm[s][c];
             }
-            const size_t po = (size_t)y * W;
-            const size_t e = col0 - dd + d + (size_t)y * rstep;
-            if (MODE == 0) {
-                const float mI[3] = {pix[0 * npix + po], pix[1 * npix + po], pix[2 * npix + po]};
-                const float iv[6] = {pix[3 * npix + po], pix[4 * npix + po], pix[5 * npix + po],
-                                     pix[6 * npix + po], pix[7 * npix + po], pix[8 * npix + po]};
-                const float mP = m[0];
-                float cov[3];
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    const float mm = mP * mI[c];
-                    cov[c] = m[1 + c] - mm;
-                }
-                // inverse entry (g, k): 00 01 02 / 01 11 12 / 02 12 22
-                const int IX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
-                float al[3];
-#pragma unroll
-                for (int g = 0; g < 3; g++) {
-                    float acc = iv[IX[g][0]] * cov[0];
-#pragma unroll
-                    for (int k = 1; k < 3; k++) {
-                        const float mm = iv[IX[g][k]] * cov[k];
-                        acc = acc + mm;
-                    }
-                    al[g] = acc;
-                }
-                float be = mP;
-#pragma unroll
-                for (int g = 0; g < 3; g++) {
-                    const float mm = al[g] * mI[g];
-                    be = be - mm;
-                }
-                if (live) {
-                    ab[0 * ab_plane + e] = al[0];
-                    ab[1 * ab_plane + e] = al[1];
-                    ab[2 * ab_plane + e] = al[2];
-                    ab[3 * ab_plane + e] = be;
-                }
-            } else {
-                const uint32_t w = gw[po];
-                const float I[3] = {(float)(w & 0xffu), (float)((w >> 8) & 0xffu), (float)((w >> 16) & 0xffu)};
-                float q = m[3];   // box(beta)
-#pragma unroll
-                for (int g = 0; g < 3; g++) {
-                    const float mm = m[g] * I[g];
-                    q = q + mm;
-                }
-                if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
-                    float sum = 0.f;
-                    sum += a.scale * q;
-                    q = sum;
-                }
-                if (live) a.vm[e] = q;
-            }
+            emit(y, m);
         }
     };
     Tile ta, tb;
@@ -378,6 +432,7 @@ __global__ __launch_bounds__(64) void k_gfcv_cols(const GfCvArgs a) {
         load(ta, y0 + 2 * T);
         process(tb, y0 + T);
     }
+#endif
 }
 
 }  // namespace

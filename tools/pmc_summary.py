@@ -49,8 +49,10 @@ def load(path: str, counter: str):
     for r in rows:
         if r["Counter_Name"] != counter:
             continue
-        # a step of "prep" is three dispatches (k_pack_bgr4, k_pack_arms, k_prep): count steps by k_prep
-        step = "k_prep" in r["Kernel_Name"] or "k_pack" not in r["Kernel_Name"]
+        # a step of "prep" is several dispatches (k_pack_bgr4, k_pack_arms, k_prep, or the split
+        # prep's k_prep_h, k_prep_v): count steps by k_prep / k_prep_h only
+        k = r["Kernel_Name"]
+        step = "k_pack" not in k and "k_prep_v" not in k
         out.append((profile_name(r["Kernel_Name"], seen), float(r["Counter_Value"]) * 1024.0, step))
     return out
 

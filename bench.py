@@ -109,8 +109,9 @@ def parse():
                          "int16 maps in pinned host memory, SURVEY §8d's `disp_out` ready)")
     ap.add_argument("--sub-batch", type=int, default=0, help="sm_params.sub_batch: run the pairs in groups of k")
     ap.add_argument("--streams", type=int, default=1, help="sm_params.num_streams: groups alternate over s streams")
-    ap.add_argument("--fuse-norm-scan", action="store_true",
-                    help="CBCA: fuse iteration k's normalising sweep with iteration k+1's scan (sm_params.fuse_norm_scan)")
+    ap.add_argument("--fuse-norm-scan", choices=["auto", "on", "off"], default="auto",
+                    help="CBCA: fuse iteration k's normalising sweep with iteration k+1's scan (sm_params.fuse_norm_scan; "
+                         "auto = for volumes >= 256 MiB per pair)")
     ap.add_argument("--e2e", action="store_true",
                     help="time the product multi-GPU path instead of resident batches: rank 0 holds the global "
                          "batch on the host; each step broadcasts the header, scatters the pairs (RCCL), runs "
@@ -167,7 +168,7 @@ def main():
     # this rank's shard of the global batch: pair indices [rank*B, rank*B + B)
     batch = S.make_batch(B, H, W, D, first_index=rank * B)
     sb = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt,
-                     aggregation=args.agg, fuse_norm_scan=int(args.fuse_norm_scan), sub_batch=args.sub_batch,
+                     aggregation=args.agg, fuse_norm_scan={"auto": -1, "on": 1, "off": 0}[args.fuse_norm_scan], sub_batch=args.sub_batch,
                      num_streams=args.streams)
     if args.agg != "CBCA":
         agg_name = {"GF": "GF (ximgproc::guidedFilter, r 9, eps 1e-4)", "NL": "NL (MST tree filter)"}[args.agg]

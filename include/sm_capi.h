@@ -120,7 +120,10 @@ typedef struct sm_params {
     int32_t sub_batch;           /* run the n pairs in groups of k (0 = one group), stages back to back */
     int32_t num_streams;         /* 0/1: one stream; 2-4: groups alternate over that many streams,
                                   * group k + 1 starting once group k's CBCA is done */
-    int32_t fuse_norm_scan;      /* 1: CBCA normalising sweep fused with the next scan (measured slower) */
+    int32_t fuse_norm_scan;      /* CBCA: iteration k's normalising sweep fused with iteration k+1's
+                                  * scan (one sweep, 8 B per element less): 1 = always, 0 = never,
+                                  * -1 (default) = when a pair's volume is >= 256 MiB (measured
+                                  * faster at 1080p and full resolution, slower at Teddy size) */
     /* alternative aggregators */
     float gf_eps;                /* gf_eps[0] = 0.0001 (h:298; radius gf_r[0] = 9, h:297) */
     int32_t gf_mode;             /* sm_gf_mode: SM_GF_XIMGPROC (default, the shipped build) or SM_GF_MY_GUIDE */

@@ -120,15 +120,19 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #ifndef SM_CB_VG_AUX
 #define SM_CB_VG_AUX 0       // cache policy bits of the V sweeps' arm gathers (tuning)
 #endif
-// CB_NORM_SCAN sweeps (two S rings + the area ring: three waves per CU): tile and tiles in flight
+// CB_NORM_SCAN sweeps (two S rings + the area ring): tile and tiles in flight.  T = 12 with three
+// tiles in flight (two waves per CU by LDS, one per SIMD by VGPRs) measured fastest among T = 6-20,
+// PF = 1-3 (same-process A/B, profiles/r3c, r3i): full resolution v_norm + v_scan 12.20 ms ->
+// 11.09 ms fused, 1080p 16.38 -> 15.68 ms; Teddy 0.76 -> 0.82 ms (hence sm_params.fuse_norm_scan's
+// auto mode: fused for volumes >= 256 MiB per pair)
 #ifndef SM_CB_T_NS
-#define SM_CB_T_NS 8
+#define SM_CB_T_NS 12
 #endif
 #ifndef SM_CB_PF_NS_H
 #define SM_CB_PF_NS_H 2
 #endif
 #ifndef SM_CB_PF_NS_V
-#define SM_CB_PF_NS_V 1
+#define SM_CB_PF_NS_V 3
 #endif
 __host__ __device__ constexpr int cbca_win_ring(int T) { return 63 + T; }
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {

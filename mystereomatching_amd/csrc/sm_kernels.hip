@@ -289,6 +289,53 @@ __device__ __forceinline__ int strip_walk(const uint32_t* sp, int sst, uint32_t 
 #endif
     return arm;
 }
+// Two walks from one centre (the split prep's L / R and U / D pairs) advanced together in chunks
+// of SM_PREP_WALK2 steps: both chunks' LDS reads are issued before either is tested, so a thread
+// has 2 x SM_PREP_WALK2 reads in flight instead of one dependent read per step.  Same results as
+// two strip_walk calls (a chunk's first failing step ends that walk; steps past Lo fail).
+#ifndef SM_PREP_WALK2
+#define SM_PREP_WALK2 4
+#endif
+__device__ __forceinline__ void strip_walk2(const uint32_t* sp, int sa, uint32_t fa, int sb, uint32_t fb, uint32_t ca1,
+                                            uint32_t cb1, uint32_t ca2, uint32_t cb2, int Lin, int Lo, int& arm_a,
+                                            int& arm_b) {
+    constexpr int CW = SM_PREP_WALK2 > 0 ? SM_PREP_WALK2 : 1;
+    auto first_fail = [&](const uint32_t (&pw)[CW], int arm, uint32_t f) {
+        const uint32_t want = ARM_B9 | f;
+        int ff = CW;
+#pragma unroll
+        for (int j = CW - 1; j >= 0; j--) {
+            const int st = arm + j;
+            const bool in1 = st <= Lin;
+            const uint32_t ca = in1 ? ca1 : ca2, cb = in1 ? cb1 : cb2;
+            const bool ok = ((((ca - pw[j]) & ~(cb - pw[j])) & ARM_B9) | (pw[j] & f)) == want;
+            if (st > Lo || !ok) ff = j;
+        }
+        return ff;
+    };
+    int a = 1, b = 1;
+    bool da = false, db = false;
+    while (!(da && db)) {
+        uint32_t pa[CW], pb[CW];
+#pragma unroll
+        for (int j = 0; j < CW; j++) {
+            pa[j] = sp[min(a + j, Lo) * sa];
+            pb[j] = sp[min(b + j, Lo) * sb];
+        }
+        if (!da) {
+            const int ff = first_fail(pa, a, fa);
+            a += ff;
+            da = ff < CW;
+        }
+        if (!db) {
+            const int ff = first_fail(pb, b, fb);
+            b += ff;
+            db = ff < CW;
+        }
+    }
+    arm_a = a;
+    arm_b = b;
+}
 // The arm length kept from a walk that failed at step `arm` (cpp:3035-3046): the walked length
 // when it reaches minL, else the longest length <= minL that stays inside the image.
 __device__ __forceinline__ int arm_final(int arm, int minL, int u, int v, int du, int dv, int W, int H) {
@@ -517,9 +564,12 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
 // The packed-BGR plane is made (k_pack_bgr) only for the kernels that read it (GF, so, refine).
 // ---------------------------------------------------------------------------------------
 #ifndef SM_PREP_SPLIT
-#define SM_PREP_SPLIT 0   // (until validated on the GPU)
+#define SM_PREP_SPLIT 1
 #endif
 constexpr int PH_TW = 256, PH_TH = 4, PV_TW = 64, PV_TH = 64;
+#ifndef SM_PREP_QUAD
+#define SM_PREP_QUAD 1   // strips filled four pixels per load_quad_bgr (else three byte loads per pixel)
+#endif
 __host__ __device__ inline int preph_gray_bytes(int rv, int ru) {
     const int hv = rv > 1 ? rv : 1, hu = ru > 1 ? ru : 1;
     return ((PH_TW + 2 * hu) * (PH_TH + 2 * hv) + 15) / 16 * 16;
@@ -533,6 +583,59 @@ __device__ __forceinline__ uint32_t pack10_at(const uint8_t* bgr, int vv, int uu
     if ((unsigned)vv >= (unsigned)H || (unsigned)uu >= (unsigned)W) return PREP_OUT;
     const uint8_t* q = bgr + ((size_t)vv * W + uu) * 3;
     return (uint32_t)q[0] | ((uint32_t)q[1] << 10) | ((uint32_t)q[2] << 20);
+}
+// Four consecutive pixels' colours (B | G << 8 | R << 16 each) from the 12 bytes at q, any
+// alignment: four dword loads from the dword below q and three byte-aligning funnel shifts (the
+// colour allocation carries a 16-byte tail pad for the fourth dword)
+__device__ __forceinline__ uint4 load_quad_bgr(const uint8_t* q) {
+    const uintptr_t ad = (uintptr_t)q;
+    const uint32_t* d = (const uint32_t*)(ad & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(ad & 3u);
+    const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3];
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh),
+                   x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+    return make_uint4(x0 & 0xffffffu, (x0 >> 24) | ((x1 & 0xffffu) << 8), (x1 >> 16) | ((x2 & 0xffu) << 16), x2 >> 8);
+}
+// Fill `rows` rows of a packed-pixel strip (pack10 words, PREP_OUT outside the image) covering
+// columns c0 .. c0 + width - 1 of image rows r0 .. r0 + rows - 1, row stride `stride` words:
+// quads of four columns from one load_quad_bgr each, four quads per thread in flight.
+__device__ __forceinline__ void fill_strip_quads(uint32_t* dst, int stride, const uint8_t* C, int r0, int rows, int c0,
+                                                 int width, int H, int W) {
+    const int qpr = (width + 3) >> 2;   // quads per row (the last may be partial)
+    const int nq = rows * qpr;
+    for (int i0 = 0; i0 < nq; i0 += 4 * 256) {
+        uint4 px[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int i = i0 + k * 256 + (int)threadIdx.x;
+            const int r = i / qpr, x = 4 * (i - r * qpr), vv = r0 + r, uu = c0 + x;
+            // whole quad inside the image: one funnel-shifted load; else per-pixel bytes
+            const bool row_in = i < nq && (unsigned)vv < (unsigned)H;
+            if (row_in && uu >= 0 && uu + 3 < W) {
+                px[k] = load_quad_bgr(C + ((size_t)vv * W + uu) * 3);
+            } else {
+                uint32_t t[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int u = uu + j;
+                    const uint8_t* b = C + ((size_t)vv * W + u) * 3;
+                    t[j] = (row_in && (unsigned)u < (unsigned)W) ? ((uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16))
+                                                               : 0xffffffffu;
+                }
+                px[k] = make_uint4(t[0], t[1], t[2], t[3]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int i = i0 + k * 256 + (int)threadIdx.x;
+            if (i >= nq) continue;
+            const int r = i / qpr, x = 4 * (i - r * qpr);
+            const uint32_t v[4] = {px[k].x, px[k].y, px[k].z, px[k].w};
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (x + j < width) dst[r * stride + x + j] = v[j] == 0xffffffffu ? PREP_OUT : pack10(v[j]);
+        }
+    }
 }
 // arm-walk word of packed pixel p (k_pack_arms): bit 30 / 31 = its C_D test against the walk's
 // previous pixel nb30 / nb31 (the neighbour towards the walk's start); 0 outside the image
@@ -589,11 +692,15 @@ __global__ __launch_bounds__(256) void k_prep_h(const PrepArgs a) {
     uint32_t* PH = (uint32_t*)(prep_raw + preph_gray_bytes(rv, ru));   // [PH_TH + 2][hc]
     if (words || flags) {
         const uint8_t* C = a.bgr + img * npix * 3;
-        const float rinv = 1.0f / (float)hc;   // row by a float reciprocal (exact for i < 2^22)
-        prep_fill(PH, (PH_TH + 2) * hc, [&](int i) -> uint32_t {
-            const int r = (int)(((float)i + 0.5f) * rinv);
-            return pack10_at(C, v0 - 1 + r, u0 - Lo - 1 + (i - r * hc), H, W);
-        });
+        if (SM_PREP_QUAD) {
+            fill_strip_quads(PH, hc, C, v0 - 1, PH_TH + 2, u0 - Lo - 1, hc, H, W);
+        } else {
+            const float rinv = 1.0f / (float)hc;   // row by a float reciprocal (exact for i < 2^22)
+            prep_fill(PH, (PH_TH + 2) * hc, [&](int i) -> uint32_t {
+                const int r = (int)(((float)i + 0.5f) * rinv);
+                return pack10_at(C, v0 - 1 + r, u0 - Lo - 1 + (i - r * hc), H, W);
+            });
+        }
     }
     __syncthreads();
     if (flags) {   // SGM penalty flags (updateCost, h:2223-2229) from the packed pixels and their rim
@@ -661,8 +768,15 @@ __global__ __launch_bounds__(256) void k_prep_h(const PrepArgs a) {
             const uint32_t cf = q[0] & 0x3fffffffu;
             const uint32_t ca1 = cf + (uint32_t)(512 + t1) * ARM_M, cb1 = cf + (uint32_t)(511 - t1) * ARM_M;
             const uint32_t ca2 = cf + (uint32_t)(512 + t2) * ARM_M, cb2 = cf + (uint32_t)(511 - t2) * ARM_M;
-            const int al = arm_final(strip_walk(q, -1, 1u << 30, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, -1, 0, W, H);
-            const int ar = arm_final(strip_walk(q, 1, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, 1, 0, W, H);
+            int wl, wr;
+            if (SM_PREP_WALK2 > 0) {
+                strip_walk2(q, -1, 1u << 30, 1, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo, wl, wr);
+            } else {
+                wl = strip_walk(q, -1, 1u << 30, ca1, cb1, ca2, cb2, Lin, Lo);
+                wr = strip_walk(q, 1, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo);
+            }
+            const int al = arm_final(wl, a.minL, u, v, -1, 0, W, H);
+            const int ar = arm_final(wr, a.minL, u, v, 1, 0, W, H);
             ((uint32_t*)a.arms)[img * 2 * npix + (size_t)v * W + u] = (uint32_t)al | ((uint32_t)ar << 16);
         }
     }
@@ -678,8 +792,12 @@ __global__ __launch_bounds__(256) void k_prep_v(const PrepArgs a) {
     const int tid = threadIdx.x;
     uint32_t* PV = (uint32_t*)prep_raw;   // [PV_TH + 2 Lo + 2][PV_TW]: rows v0 - Lo - 1 ..
     const uint8_t* C = a.bgr + img * npix * 3;
-    prep_fill(PV, (PV_TH + 2 * Lo + 2) * PV_TW,
-              [&](int i) -> uint32_t { return pack10_at(C, v0 - Lo - 1 + (i >> 6), u0 + (i & 63), H, W); });
+    if (SM_PREP_QUAD) {
+        fill_strip_quads(PV, PV_TW, C, v0 - Lo - 1, PV_TH + 2 * Lo + 2, u0, PV_TW, H, W);
+    } else {
+        prep_fill(PV, (PV_TH + 2 * Lo + 2) * PV_TW,
+                  [&](int i) -> uint32_t { return pack10_at(C, v0 - Lo - 1 + (i >> 6), u0 + (i & 63), H, W); });
+    }
     __syncthreads();
     {
         const int tc = min(max(a.C_D, -1), 255);
@@ -717,8 +835,15 @@ __global__ __launch_bounds__(256) void k_prep_v(const PrepArgs a) {
         const uint32_t cf = q[0] & 0x3fffffffu;
         const uint32_t ca1 = cf + (uint32_t)(512 + t1) * ARM_M, cb1 = cf + (uint32_t)(511 - t1) * ARM_M;
         const uint32_t ca2 = cf + (uint32_t)(512 + t2) * ARM_M, cb2 = cf + (uint32_t)(511 - t2) * ARM_M;
-        const int au = arm_final(strip_walk(q, -PV_TW, 1u << 30, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, 0, -1, W, H);
-        const int ad = arm_final(strip_walk(q, PV_TW, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo), a.minL, u, v, 0, 1, W, H);
+        int wu, wd;
+        if (SM_PREP_WALK2 > 0) {
+            strip_walk2(q, -PV_TW, 1u << 30, PV_TW, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo, wu, wd);
+        } else {
+            wu = strip_walk(q, -PV_TW, 1u << 30, ca1, cb1, ca2, cb2, Lin, Lo);
+            wd = strip_walk(q, PV_TW, 1u << 31, ca1, cb1, ca2, cb2, Lin, Lo);
+        }
+        const int au = arm_final(wu, a.minL, u, v, 0, -1, W, H);
+        const int ad = arm_final(wd, a.minL, u, v, 0, 1, W, H);
         plane1[(size_t)v * W + u] = (uint32_t)au | ((uint32_t)ad << 16);
     }
 }
@@ -750,9 +875,10 @@ static void launch_prep_split(const PrepArgs& a, int n, hipStream_t st) {
         hipLaunchKernelGGL((k_prep_h<3, 4, 1>), gh, dim3(256), shh, st, a);
     else
         hipLaunchKernelGGL((k_prep_h<-1, -1, -1>), gh, dim3(256), shh, st, a);
-    if (a.do_arms)
-        hipLaunchKernelGGL(k_prep_v, dim3((a.W + PV_TW - 1) / PV_TW, (a.H + PV_TH - 1) / PV_TH, 2 * n), dim3(256),
-                           (size_t)prepv_bytes(a.L_out), st, a);
+    if (a.do_arms) {
+        const dim3 gv((a.W + PV_TW - 1) / PV_TW, (a.H + PV_TH - 1) / PV_TH, 2 * n);
+        hipLaunchKernelGGL(k_prep_v, gv, dim3(256), (size_t)prepv_bytes(a.L_out), st, a);
+    }
 }
 
 void launch_prep(const PrepArgs& a, int n, hipStream_t st) {

@@ -31,6 +31,7 @@
 // so a tile costs one or two LDS round trips.  Rings hold 2*lag + T + 1 slots.
 #include <float.h>
 #include <algorithm>
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -134,6 +135,44 @@ __device__ __forceinline__ uint32_t shl1_in(uint32_t v, uint32_t in) {  // lane 
 #ifndef SM_CB_PF_NS_V
 #define SM_CB_PF_NS_V 3
 #endif
+// NORM_SCAN V sweeps at the reference's lag (cbca_crossL_out = 34, a compile-time LAGC): the scan
+// stage's pass intersection at position j is the norm stage's at j - lag (both are the pass pair
+// of row j - 2 lag), so the sweep keeps the last four tiles' norm intersections in registers and
+// drops the third set's own-arm load, readlane, pkmin and 64-word gather per position
+// (SM_CB_NS_REUSE; other lags run the generic sweep).
+#ifndef SM_CB_NS_REUSE
+#define SM_CB_NS_REUSE 1
+#endif
+// Normalising sweeps decide per TILE whether a dividend can lie in (0, 2^-110), where div_area
+// needs the IEEE division (SM_CB_SAFE_TILE): prefix sums of costs >= +0 never decrease along a
+// line, and a difference S(h) - S(t) with S(t) >= 2^-86 is 0 or >= ulp(S(t)) >= 2^-109.  Each lane
+// records per tile whether S at the tile's start reached 2^-86; a tile whose window start lies
+// at least ceil(2 lag / T) tiles back in a lane that had then reached it skips the per-position
+// check (the first tiles of a line, and lines of tiny costs, keep it).
+#ifndef SM_CB_SAFE_TILE
+#define SM_CB_SAFE_TILE 0
+#endif
+// Ring slots of a position's window ends as one packed u16 pair (SM_CB_PK_SLOTS): with the uniform
+// slot c of position i and the intersection pair (tail | head << 16), (pair ^ 0xffff) + (c, c) is
+// (c - tail - 1, c + head) modulo 2^16, and one packed add of (ring, -ring) plus a packed minimum
+// wraps both ends into [0, ring) -- four VALU for both slots instead of seven.
+#ifndef SM_CB_PK_SLOTS
+#define SM_CB_PK_SLOTS 1
+#endif
+// ... and each ring address is one v_mad_u32_u16 of the pair's half (op_sel) with the ring's
+// bytes per slot and the lane's byte offset (SM_CB_MAD_ADDR) instead of an extract and a shift-add
+#ifndef SM_CB_MAD_ADDR
+#define SM_CB_MAD_ADDR 1
+#endif
+template <int HI>
+__device__ __forceinline__ uint32_t mad_u32_u16(uint32_t a, uint32_t b, uint32_t c) {   // a.half * b.lo + c
+    uint32_t r;
+    if (HI)
+        asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    else
+        asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+}
 __host__ __device__ constexpr int cbca_win_ring(int T) { return 63 + T; }
 __host__ __device__ constexpr int cbca_tile(bool horiz, int mode) {
     return mode == CB_SCAN ? (horiz ? SM_CB_T_SCAN_H : SM_CB_T_SCAN_V)
@@ -265,7 +304,7 @@ struct CbTile {
 // RV: the right view's volume vm[1] (cbca_core's LOR = 1, run when Do_refine): the pixel's own
 // arms are the right image's, and lane d pairs them with the LEFT image's arms at u + d
 // (HVL_INTERSECTION[1], cpp:2794-2845) — zero once u + d >= W.
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW = 1, int CPW = 1>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW = 1, int CPW = 1, int LAGC = 0>
 struct CbLine {
     static constexpr int CW = 64 / CPW;   // disparities per chunk (lanes per column)
     static constexpr int T = CbCfg<HORIZ, MODE, KW>::T;
@@ -275,6 +314,10 @@ struct CbLine {
     static constexpr int NV = CbCfg<HORIZ, MODE, KW>::NV;
     static constexpr int SPW = cbca_spw(KW);
     using Tile = CbTile<HORIZ, T, NSETS, KW, NV>;
+    // SM_CB_NS_REUSE: scan-stage intersections from the norm stage's, LAGC positions back
+    static constexpr bool REUSE2 = LAGC > 0 && !HORIZ && MODE == CB_NORM_SCAN && KW == 1 && CPW == 1;
+    static_assert(!REUSE2 || (CbCfg<HORIZ, MODE, KW>::PF == 3 && LAGC + T - 1 <= 4 * T),
+                  "the history is the last four tiles of the four-tile loop");
 
     // Volume and V-sweep arm accesses are buffer instructions: the tile's first position in the
     // resource base, lane + k * stride in a loop-invariant VGPR.  Loads are not clamped: the
@@ -305,7 +348,11 @@ struct CbLine {
     float* r1;
     float* r2;
     uint16_t* ra;
+    uint32_t o1, o2, oa;      // SM_CB_MAD_ADDR: LDS address of this lane's slot-0 entry in r1, r2, ra
     float scale;
+    uint32_t ph[REUSE2 ? 4 : 1][REUSE2 ? T : 1];   // REUSE2: pass intersections of the last 4 tiles
+    uint32_t shist;           // SM_CB_SAFE_TILE: bit m = S at the start of the tile m back >= 2^-86
+    int msafe;                // tiles back to the tile holding the window start (> 31: never safe)
     // V group (KW > 1)
     int wv;                   // wave index in the workgroup = column u0 + wv
     bool active;              // column < W (the last group's spare waves only keep the barriers)
@@ -366,6 +413,7 @@ struct CbLine {
         }
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
+            if (REUSE2 && s == 2) continue;
             const int base = j0 - set_off(s);
             // (only lanes k < T are read back; the others stay off the memory system, which
             // matters for the strided column loads of vertical sweeps)
@@ -489,6 +537,27 @@ struct CbLine {
     }
     __device__ __forceinline__ int up(int s) const { return (int)min((uint32_t)s, (uint32_t)(s - ring)); }   // s in [0, 2 ring)
     __device__ __forceinline__ int dn(int s) const { return (int)min((uint32_t)s, (uint32_t)(s + ring)); }   // s in (-ring, ring)
+    // SM_CB_PK_SLOTS: (tail slot | head slot << 16) of intersection pair p at uniform slot c < 2 ring
+    __device__ __forceinline__ uint32_t slot_pair(uint32_t p, int c) const {
+        c = c >= ring ? c - ring : c;   // c < 2 ring: then c + head < 2 ring, c - tail - 1 > -ring
+        const us2 q = __builtin_bit_cast(us2, p ^ 0xffffu) + us2{(unsigned short)c, (unsigned short)c};
+        const us2 w = q + us2{(unsigned short)ring, (unsigned short)(-ring)};
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, w));
+    }
+    // LDS element of a ring of 4-byte / 2-byte entries at slot s (packed half h of sp) for this lane
+    // RG: 0 = r1, 1 = r2 (floats), 2 = ra (u16)
+    template <int H_, int RG, typename E = typename std::conditional<RG == 2, uint16_t, float>::type>
+    __device__ __forceinline__ E ring_at(uint32_t sp) const {
+        if (SM_CB_MAD_ADDR) {
+            const uint32_t o = RG == 2 ? oa : (RG == 1 ? o2 : o1);
+            // (an integer LDS address cast to an LDS pointer: no base add in front of the read)
+            typedef __attribute__((address_space(3))) const E lds_e;
+            return *(lds_e*)(size_t)mad_u32_u16<H_>(sp, 64u * (uint32_t)sizeof(E), o);
+        }
+        const uint32_t sl = H_ ? sp >> 16 : sp & 0xffffu;
+        const E* r = RG == 2 ? (const E*)ra : (const E*)(RG == 1 ? r2 : r1);
+        return r[sl * 64u + (uint32_t)lane];
+    }
 
     // (last pass only) SolveAll's `sum = 0; sum += w * v` (cpp:2189-2201): 0 + x == x for every
     // x except -0, and no CBCA value is ever -0 (costs are >= +0, prefix sums of them too, and
@@ -501,14 +570,16 @@ struct CbLine {
     // start read the zeroed ring, which is exactly the reference's border case
     // out = S[i + head] (cal1DCost, h:1643-1715).  Only the two ends of a line (GUARD) test
     // whether an output position exists before storing it.
-    template <bool GUARD>
+    template <bool GUARD, int R>
     __device__ __forceinline__ void tile(const Tile& t, int j0) {
         uint32_t pi[T], pi2[T];
+        if (MODE != CB_SCAN && SM_CB_SAFE_TILE) shist = (shist << 1) | (S1 >= 0x1p-86f ? 1u : 0u);   // S(j0 - 1)
         // ring % T == 0 and ws % T == 0, so the tile's write slots ws .. ws+T-1 never wrap
         float* w1 = r1 + ws * 64 + lane;
         uint16_t* wa = ra + ws * 64 + lane;
         const int si0 = uwrap(ws - lag);        // slot of i = j0 - lag
-        const int s20 = uwrap(ws - 2 * lag);    // slot of i2 = j0 - 2 lag
+        // (NORM_SCAN: r2 holds position p's S2 at slot (p + lag) mod ring, so the tile's S2 writes
+        // are slots ws .. ws + T - 1 and the slot of i2 = j0 - 2 lag in r2 is si0)
         const int i0 = j0 - lag;
         const __amdgpu_buffer_rsrc_t ob = tile_rsrc(i0);
         stage(t);
@@ -530,13 +601,34 @@ struct CbLine {
 #endif
                 wa[k * 64] = (uint16_t)Acc;
             }
-            if (MODE == CB_NORM_SCAN) pi2[k] = isect(t, 2, k);
+            if (MODE == CB_NORM_SCAN && !REUSE2) pi2[k] = isect(t, 2, k);
+        }
+        if constexpr (REUSE2) {
+            // position j0 + k - LAGC lies in tile R + dt (dt < 0) at index k - LAGC - dt T
+#pragma unroll
+            for (int k = 0; k < T; k++) {
+                const int q = k - LAGC;
+                const int dt = -((-q + T - 1) / T);
+                pi2[k] = ph[(R + dt + 8) & 3][q - dt * T];
+            }
+#pragma unroll
+            for (int k = 0; k < T; k++) ph[R][k] = pi[k];
         }
         // phase B: first-stage outputs at i = j - lag (reads batched, then arithmetic)
         float shv[T], stv[T];
         uint32_t ahv[T], atv[T];
 #pragma unroll
         for (int k = 0; k < T; k++) {
+            if (SM_CB_PK_SLOTS) {
+                const uint32_t sp = slot_pair(pi[k], si0 + k);   // slots of i - tail - 1, i + head
+                shv[k] = ring_at<1, 0>(sp);
+                stv[k] = ring_at<0, 0>(sp);
+                if (MODE != CB_SCAN) {
+                    ahv[k] = ring_at<1, 2>(sp);
+                    atv[k] = ring_at<0, 2>(sp);
+                }
+                continue;
+            }
             const int tl = pi[k] & 0xffff, hd = pi[k] >> 16;
             const int hs = up(si0 + k + hd);             // slot of i + head  (< 2 ring)
             const int ts = dn(hs - (hd + tl + 1));       // slot of i - tail - 1 (window < ring)
@@ -557,19 +649,24 @@ struct CbLine {
             // division (a uniform branch that never runs on real costs)
             float dv[T], qv[T];
             uint32_t av[T];
-            // dividends are >= +0 (prefix sums of costs >= 0; S - S = +0), so "0 < dv < 2^-110"
-            // is "bits(dv) - 1 < 0x087fffff" (unsigned); the tile's minimum of bits - 1 decides it
-            uint32_t tmin = 0xffffffffu;
 #pragma unroll
             for (int k = 0; k < T; k++) {
                 dv[k] = shv[k] - stv[k];
                 av[k] = (ahv[k] - atv[k]) & 0xffffu;
                 qv[k] = div_area(dv[k], av[k]);
-                tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
             }
-            if (__ballot(tmin < 0x087fffffu)) {
+            // SM_CB_SAFE_TILE: every lane's window start S >= 2^-86 (see the switch) -> no check
+            const bool check = !SM_CB_SAFE_TILE || msafe > 31 || __ballot(((shist >> msafe) & 1u) == 0u);
+            if (check) {
+                // dividends are >= +0 (prefix sums of costs >= 0; S - S = +0), so "0 < dv < 2^-110"
+                // is "bits(dv) - 1 < 0x087fffff" (unsigned); the tile's minimum of bits - 1 decides it
+                uint32_t tmin = 0xffffffffu;
 #pragma unroll
-                for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)av[k];
+                for (int k = 0; k < T; k++) tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
+                if (__ballot(tmin < 0x087fffffu)) {
+#pragma unroll
+                    for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)av[k];
+                }
             }
 #pragma unroll
             for (int k = 0; k < T; k++) {
@@ -579,7 +676,7 @@ struct CbLine {
                     float y = qv[k];                              // final value of iteration k at i
                     if (GUARD) y = (i0 + k >= 0) ? y : 0.f;       // nothing accumulates before the line
                     S2 = S2 + y;                                  // prefix of iteration k+1's first pass
-                    r2[up(si0 + k) * 64 + lane] = S2;
+                    r2[(ws + k) * 64 + lane] = S2;
                 }
             }
         }
@@ -588,8 +685,14 @@ struct CbLine {
             float s2h[T], s2t[T];
 #pragma unroll
             for (int k = 0; k < T; k++) {
+                if (SM_CB_PK_SLOTS) {
+                    const uint32_t sp = slot_pair(pi2[k], si0 + k);
+                    s2h[k] = ring_at<1, 1>(sp);
+                    s2t[k] = ring_at<0, 1>(sp);
+                    continue;
+                }
                 const int tl = pi2[k] & 0xffff, hd = pi2[k] >> 16;
-                const int hs = up(s20 + k + hd);
+                const int hs = up(si0 + k + hd);
                 s2h[k] = r2[hs * 64 + lane];
                 s2t[k] = r2[dn(hs - (hd + tl + 1)) * 64 + lane];
             }
@@ -603,13 +706,14 @@ struct CbLine {
         if (SM_CB_WIN_RING) wrs = (wrs + T >= cbca_win_ring(T)) ? wrs + T - cbca_win_ring(T) : wrs + T;
     }
 
+    template <int R = 0>   // R: the tile's slot in the four-tile loop (REUSE2 history)
     __device__ __forceinline__ void process(const Tile& t, int j0) {
         constexpr int stages = MODE == CB_NORM_SCAN ? 2 : 1;
         const int last_out = j0 + T - 1 - lag * stages;        // last output position of the tile
         if (j0 - lag >= 0 && last_out < len && (MODE != CB_NORM_SCAN || j0 - 2 * lag >= 0))
-            tile<false>(t, j0);
+            tile<false, R>(t, j0);
         else
-            tile<true>(t, j0);
+            tile<true, R>(t, j0);
     }
 };
 
@@ -634,11 +738,11 @@ struct CbLine {
 #define SM_CB_CHUNK_MAJOR_V 1
 #endif
 
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, int WPB>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, int WPB, int LAGC>
 __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
     constexpr int CPW = cbca_cpw(HORIZ, MODE, KW, WPB);
     constexpr int CW = 64 / CPW;
-    CbLine<HORIZ, MODE, FULL, SCALE, RV, KW, CPW> L;
+    CbLine<HORIZ, MODE, FULL, SCALE, RV, KW, CPW, LAGC> L;
     constexpr int T = CbCfg<HORIZ, MODE, KW>::T;
     constexpr int NSETS = CbCfg<HORIZ, MODE, KW>::NSETS;
     L.lane = (KW > 1 || WPB > 1) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
@@ -719,6 +823,14 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
     L.ring = cbca_ring(a.lag, HORIZ, MODE, KW);
+    L.shist = 0u;
+    L.msafe = (2 * a.lag + T - 1) / T;
+    if constexpr (decltype(L)::REUSE2) {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int k = 0; k < T; k++) L.ph[r][k] = 0u;   // positions before the line: zero arms
+    }
     if (HORIZ && RV && !SM_CB_LDS_WIN) {
         // right view: the window before each set's first position p0 = -off holds, in lane l, the
         // left image's arm pair at p0 - 1 + c64 + l (0 outside the line)
@@ -735,6 +847,12 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     L.r1 = mine;
     L.r2 = mine + (size_t)L.ring * 64;
     L.ra = (uint16_t*)(mine + (size_t)L.ring * 64 * (MODE == CB_NORM_SCAN ? 2 : 1));
+    {
+        typedef __attribute__((address_space(3))) char lds_c;
+        L.o1 = (uint32_t)(size_t)(lds_c*)L.r1 + 4u * (uint32_t)L.lane;
+        L.o2 = (uint32_t)(size_t)(lds_c*)L.r2 + 4u * (uint32_t)L.lane;
+        L.oa = (uint32_t)(size_t)(lds_c*)L.ra + 2u * (uint32_t)L.lane;
+    }
     L.wown = (uint32_t*)((KW > 1 ? smem : mine) + ring_words);
     L.wspan = L.wown + NSETS * T;
     L.scale = a.scale;
@@ -791,23 +909,23 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         }
     }
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
-    typename CbLine<HORIZ, MODE, FULL, SCALE, RV, KW, CPW>::Tile ta, tb, tc, td;
+    typename CbLine<HORIZ, MODE, FULL, SCALE, RV, KW, CPW, LAGC>::Tile ta, tb, tc, td;
     if constexpr (CbCfg<HORIZ, MODE, KW>::PF == 3) {
         L.load(ta, 0);
         L.load(tb, T);
         L.load(tc, 2 * T);
         for (int j0 = 0; j0 < nst; j0 += 4 * T) {
             L.load(td, j0 + 3 * T);
-            L.process(ta, j0);
+            L.template process<0>(ta, j0);
             if (j0 + T >= nst) break;
             L.load(ta, j0 + 4 * T);
-            L.process(tb, j0 + T);
+            L.template process<1>(tb, j0 + T);
             if (j0 + 2 * T >= nst) break;
             L.load(tb, j0 + 5 * T);
-            L.process(tc, j0 + 2 * T);
+            L.template process<2>(tc, j0 + 2 * T);
             if (j0 + 3 * T >= nst) break;
             L.load(tc, j0 + 6 * T);
-            L.process(td, j0 + 3 * T);
+            L.template process<3>(td, j0 + 3 * T);
         }
     } else if constexpr (CbCfg<HORIZ, MODE, KW>::PF == 2) {
         L.load(ta, 0);
@@ -834,16 +952,16 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     }
 }
 
-template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, bool PERSIST, int WPB>
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int KW, bool PERSIST, int WPB, int LAGC = 0>
 __global__ __launch_bounds__(64 * KW * WPB) void k_cbca(const CbcaArgs a, const int nlines) {
     extern __shared__ float smem[];
     const int slot = xcd_swizzle(blockIdx.x, gridDim.x);   // neighbouring lines on one XCD
     if (!PERSIST) {
-        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW, WPB>(a, slot, smem);
+        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW, WPB, LAGC>(a, slot, smem);
         return;
     }
     for (int blk = slot; blk < nlines; blk += gridDim.x) {   // every block exits after its last line
-        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW, WPB>(a, blk, smem);
+        cbca_run_line<HORIZ, MODE, FULL, SCALE, RV, KW, WPB, LAGC>(a, blk, smem);
         __syncthreads();   // the next line's ring zeroing follows this line's last ring reads
     }
 }
@@ -864,6 +982,18 @@ static void launch_kw(const CbcaArgs& a, int n, hipStream_t st) {
         nblk = std::min(nlines, per_cu * a.num_cu);
     }
     dim3 grid(nblk), block(64 * KW * WPB);
+    if constexpr (!HORIZ && MODE == CB_NORM_SCAN && KW == 1 && WPB == 1 && !PERSIST && SM_CB_NS_REUSE) {
+        if (a.lag == 34) {   // the reference's cbca_crossL_out (h:266)
+            if (a.view == 0) {
+                if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, false, KW, PERSIST, WPB, 34>), grid, block, shm, st, a, nlines);
+                else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, false, KW, PERSIST, WPB, 34>), grid, block, shm, st, a, nlines);
+            } else {
+                if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, true, KW, PERSIST, WPB, 34>), grid, block, shm, st, a, nlines);
+                else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, true, KW, PERSIST, WPB, 34>), grid, block, shm, st, a, nlines);
+            }
+            return;
+        }
+    }
     if (a.view == 0) {
         if (full) hipLaunchKernelGGL((k_cbca<HORIZ, MODE, true, SCALE, false, KW, PERSIST, WPB>), grid, block, shm, st, a, nlines);
         else hipLaunchKernelGGL((k_cbca<HORIZ, MODE, false, SCALE, false, KW, PERSIST, WPB>), grid, block, shm, st, a, nlines);

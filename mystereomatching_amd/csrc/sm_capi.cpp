@@ -19,9 +19,7 @@
 #include <thread>
 #include <vector>
 
-#include "sm_host_pool.h"
 #include "sm_kernels.h"
-#include "sm_nl_tree.h"
 
 namespace {
 
@@ -77,25 +75,25 @@ struct sm_ctx {
     float* gfc_ab = nullptr;
     double* gfc_img = nullptr;
     float* gfc_pix = nullptr;
-    // aggregation "NL": median image, edge weights, the tree (uploaded per call), filter values
+    // aggregation "NL": median image, edge weights, spanning trees, the tree walk, filter values
     uint8_t* nl_med = nullptr;  // [cap][npix][3]
     uint8_t* nl_ew = nullptr;   // [cap][ne]
-    int* nl_ints = nullptr;     // chain_start, chain_len, order_up, order_down: [cap][npix] each
-    int* nl_rec = nullptr;      // path-node records (4 ints) [cap][npix], zero padding on both sides
+    int* nl_ints = nullptr;     // two sets of: chain_start, chain_len, order_up, order_down [cap][npix] each
+    int* nl_rec = nullptr;      // two sets of path-node records (4 ints) [cap][npix], zero padding on both sides
     int* nl_par = nullptr;      // spanning-tree union-find parents [cap][npix] (sm_nl_mst.hip)
     unsigned long long* nl_best = nullptr;  // lightest edge key offered to each component [cap][npix]
     uint8_t* nl_mst = nullptr;              // spanning-tree work space (sm::nl_mst_scratch_bytes)
-    uint32_t* nl_adj = nullptr;             // tree neighbour lists [cap][npix] (downloaded)
-    double nl_table_h[256];     // the weight table (host copy)
-    std::vector<int> nl_tabs_h; // path tables on the host: [4][cap * npix] (page-locked, nl_reg)
-    std::vector<void*> nl_reg;  // host buffers page-locked with hipHostRegister (unregistered in free_all)
-    std::vector<sm::NlTree> nl_trees;   // per pair, kept so that rebuilding reuses their memory
-    std::unique_ptr<sm::HostPool> pool; // host workers of the NL tree builds (created on first use)
-    hipStream_t nl_st = nullptr;        // NL front (median, edge weights, spanning trees, list download)
-    hipEvent_t nl_ev_up = nullptr;      // the last uploads from the host tree buffers (on c->st)
+    uint32_t* nl_adj = nullptr;             // tree neighbour lists [cap][npix]
+    uint8_t* nl_walk = nullptr;             // tree-walk work space (sm::nl_walk_scratch_bytes)
+    int* nl_offs = nullptr;                 // round offsets + error flags (device)
+    int* nl_offs_h = nullptr;               // the same, page-locked host copy
+    int nl_set = 0;                         // record / table set of the next call (double-buffered)
+    hipStream_t nl_st = nullptr;        // NL front (median, edge weights, spanning trees, tree walk)
+    hipEvent_t nl_ev_set[2] = {nullptr, nullptr};   // the last filter reading each record / table set (on c->st)
     double* nl_table = nullptr; // [256]
     double* nl_val = nullptr;   // [cap][nvol]
-    float* nl_wsum = nullptr;   // [cap][npix]
+    double* nl_oup = nullptr;   // [cap][npix] the ones channel: up sums
+    double* nl_ofin = nullptr;  // [cap][npix] final sums
     int n_loaded = 0;
     int stage = 0;              // 0 none, 1 images, 2 cost+agg, 3 solve_all, 4 optimized, 5 refined
     float lut_a[1024], lut_b[1024];
@@ -281,7 +279,8 @@ void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
                     c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->l2v, c->sgm2_sync, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
-                    c->nl_table, c->nl_val, c->nl_wsum, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->luts};
+                    c->nl_table, c->nl_val, c->nl_oup, c->nl_ofin, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->nl_walk,
+                    c->nl_offs, c->luts};
     for (void* q : ptrs)
         if (q) hipFree(q);
     if (c->nl_st) {
@@ -289,13 +288,16 @@ void free_all(sm_ctx* c) {
         hipStreamDestroy(c->nl_st);
         c->nl_st = nullptr;
     }
-    if (c->nl_ev_up) {
-        hipEventSynchronize(c->nl_ev_up);
-        hipEventDestroy(c->nl_ev_up);
-        c->nl_ev_up = nullptr;
+    for (hipEvent_t& e : c->nl_ev_set)
+        if (e) {
+            hipEventSynchronize(e);
+            hipEventDestroy(e);
+            e = nullptr;
+        }
+    if (c->nl_offs_h) {
+        hipHostFree(c->nl_offs_h);
+        c->nl_offs_h = nullptr;
     }
-    for (void* q : c->nl_reg) hipHostUnregister(q);
-    c->nl_reg.clear();
     for (auto& r : c->recs) {
         if (r.start) hipEventDestroy(r.start);
         if (r.stop) hipEventDestroy(r.stop);
@@ -535,21 +537,31 @@ sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B, bool solve_all, floa
     return timed(c, view == 0 ? "gf" : "gf_r", bytes, [&] { sm::launch_gf(a, n, c->st); });
 }
 
-// NL() on vm[0] (cpp:4892-4917): edge weights and spanning trees on the GPU, the tree walk on the
-// host, the tree filter on the GPU (sm_nl.hip, sm_nl_mst.hip, sm_nl_tree.cpp)
+// NL() on vm[0] (cpp:4892-4917): edge weights, spanning trees, the tree walk and the tree filter,
+// all on the GPU (sm_nl.hip, sm_nl_mst.hip, sm_nl_walk.hip)
 sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, np = c->npix;
     const int H = c->p.rows, W = c->p.cols, D = c->p.num_disparities;
     const size_t ne = (size_t)H * (W - 1) + (size_t)(H - 1) * W;
-    // The front (median, edge weights, spanning trees and the download of their lists) runs on
-    // its own stream: it reads only the colour images, which change only through upload() (which
-    // synchronises), so it need not wait for the work still queued on c->st -- with inputs
-    // resident across calls, the host builds this call's trees while the GPU finishes the
-    // previous call's filter and optimisation.
+    const size_t slot = (size_t)c->cap * np;
+    // The front (median, edge weights, spanning trees, the tree walk) runs on its own stream: it
+    // reads only the colour images, which change only through upload() (which synchronises), so
+    // it need not wait for the work still queued on c->st -- with inputs resident across calls,
+    // this call's trees are built while the GPU finishes the previous call's filter and
+    // optimisation.  Records and path tables are double-buffered across calls; the walk waits
+    // only for the filter that last read the set it writes.
     if (!c->nl_st) {
         HIP_TRY(c, hipStreamCreateWithFlags(&c->nl_st, hipStreamNonBlocking));
-        HIP_TRY(c, hipEventCreateWithFlags(&c->nl_ev_up, hipEventDisableTiming));
+        for (hipEvent_t& e : c->nl_ev_set) {
+            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIP_TRY(c, hipEventRecord(e, c->st));
+        }
     }
+    const int set = c->nl_set;
+    c->nl_set ^= 1;
+    int* I = c->nl_ints + (size_t)set * 4 * slot;
+    int* rec_d = c->nl_rec + ((size_t)set * (slot + 2 * sm::NL_REC_PAD) + sm::NL_REC_PAD) * 4;
+    constexpr int NOFF = 2 * (sm::NL_LEVELS + 1) + 1;
     sm_status s;
     {
         struct Swap {   // the front's launches (and their profiling events) go to nl_st
@@ -569,142 +581,20 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
                               c->nl_mst, c->nl_adj + off * np, c->st);
         });
         if (s) return s;
+        HIP_TRY(c, hipStreamWaitEvent(c->st, c->nl_ev_set[set], 0));
+        // the tree walk (sm_nl_walk.hip); bytes = the records and path tables written
+        s = timed(c, "nl_walk", (double)n * np * 32, [&] {
+            sm::launch_nl_walk(c->nl_adj + off * np, H, W, n, c->nl_walk, (int4*)rec_d, I, I + slot, I + 2 * slot,
+                               I + 3 * slot, c->nl_offs, c->st);
+        });
+        if (s) return s;
+        HIP_TRY(c, hipMemcpyAsync(c->nl_offs_h, c->nl_offs, NOFF * sizeof(int), hipMemcpyDeviceToHost, c->st));
     }
-    // SM_NL_TRACE=1: host phase times on stderr (diagnostics); "outside" = since the last call's end
-    static const bool trace = getenv("SM_NL_TRACE") != nullptr;
-    static thread_local auto t_prev_end = std::chrono::steady_clock::now();
-    auto t_last = t_prev_end;
-    auto phase = [&](const char* what) {
-        if (!trace) return;
-        const auto now = std::chrono::steady_clock::now();
-        fprintf(stderr, "[nl] %-8s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
-        t_last = now;
-    };
-    phase("outside");
-    // Host buffers: per pair (NlTree scratch) the neighbour lists, records and weight sums, and
-    // the path tables of the context, all ordinary memory first touched by the pool's workers and
-    // page-locked once (hipHostRegister), so the copies are asynchronous DMA and the host passes
-    // read and write cached memory (random accesses to hipHostMalloc'ed staging measured several
-    // times slower).  Every earlier copy from them has completed by the event wait below.
-    if ((int)c->nl_trees.size() < n) c->nl_trees.resize(n);
-    std::vector<sm::NlTree>& trees = c->nl_trees;
-    if (!c->pool) c->pool.reset(new sm::HostPool(std::max(1, std::min(c->cap, (int)std::thread::hardware_concurrency()))));
-    auto parallel = [&](const std::function<void(int)>& body) { return c->pool->run(n, body); };
-    const size_t slot = (size_t)c->cap * np;
-    auto registered = [&](void* q, size_t bytes) -> bool {
-        if (std::find(c->nl_reg.begin(), c->nl_reg.end(), q) != c->nl_reg.end()) return true;
-        if (hipHostRegister(q, bytes, hipHostRegisterDefault) != hipSuccess) return false;
-        c->nl_reg.push_back(q);
-        return true;
-    };
-    if (trees[n - 1].s_wsum.size() != np) {
-        if (!parallel([&](int b) {
-                trees[b].s_adj.resize(np);
-                trees[b].s_rec.resize(np * 4);
-                trees[b].s_wsum.resize(np);
-            }))
-            return fail(c, SM_ENOMEM, "NL: host tree buffers could not be allocated");
-    }
-    if (c->nl_tabs_h.size() != 4 * slot) c->nl_tabs_h.resize(4 * slot);
-    bool reg_ok = registered(c->nl_tabs_h.data(), 4 * slot * 4);
-    for (int b = 0; b < n && reg_ok; b++)
-        reg_ok = registered(trees[b].s_adj.data(), np * 4) && registered(trees[b].s_rec.data(), np * 16) &&
-                 registered(trees[b].s_wsum.data(), np * 4);
-    if (!reg_ok) return fail(c, SM_ENOMEM, "NL: hipHostRegister of the host tree buffers failed");
-    for (int b = 0; b < n; b++)
-        HIP_TRY(c, hipMemcpyAsync(trees[b].s_adj.data(), c->nl_adj + (off + b) * np, np * 4, hipMemcpyDeviceToHost, c->nl_st));
-    HIP_TRY(c, hipStreamSynchronize(c->nl_st));
-    HIP_TRY(c, hipEventSynchronize(c->nl_ev_up));   // the previous call's uploads from the buffers below
-    phase("lists");
-    // host threads over the pairs: phase 1 builds each pair's tree, its records and its weight
-    // sums; phase 2 writes the concatenated path tables (paths of pair b: records from b * npix)
-    // and the paths of every round, ordered by round, then pair, then path (a counting sort whose
-    // offsets are summed between the phases)
-    std::vector<char> ok(n, 0);
-    std::vector<int> mx((size_t)n * 2, 0);
-    const bool built = parallel([&](int b) {
-        sm::NlTree& t = trees[b];
-        ok[b] = sm::nl_tree_from_lists(H, W, t.s_adj.data(), t, c->nl_table_h, b * (int)np, t.s_rec.data(), t.s_wsum.data());
-        if (!ok[b]) return;
-        // the pair's paths per round (histograms indexed by level)
-        t.s_cu.assign(1, 0);
-        t.s_cd.assign(1, 0);
-        for (size_t k = 0; k < t.up_level.size(); k++) {
-            const int u = t.up_level[k], d = t.down_level[k];
-            if (u >= (int)t.s_cu.size()) t.s_cu.resize(u + 1, 0);
-            if (d >= (int)t.s_cd.size()) t.s_cd.resize(d + 1, 0);
-            t.s_cu[u]++;
-            t.s_cd[d]++;
-        }
-        mx[2 * b] = (int)t.s_cu.size() - 1;
-        mx[2 * b + 1] = (int)t.s_cd.size() - 1;
-    });
-    if (!built) return fail(c, SM_ENOMEM, "NL: host tree construction ran out of memory");
-    for (int b = 0; b < n; b++)
-        if (!ok[b]) return fail(c, SM_EINVAL, "NL: spanning tree construction failed");
-    phase("trees");
-    int max_up = 0, max_dn = 0;
-    std::vector<int> coff(n + 1, 0);
-    for (int b = 0; b < n; b++) {
-        max_up = std::max(max_up, mx[2 * b]);
-        max_dn = std::max(max_dn, mx[2 * b + 1]);
-        coff[b + 1] = coff[b] + (int)trees[b].chain_len.size();
-    }
-    const int nchain = coff[n];
-    // per round: [pair][round] counts -> round offsets (up_off) and each pair's first slot in a round
-    const int nu = max_up + 1, nd = max_dn + 1;
-    std::vector<int> cu((size_t)n * nu, 0), cd((size_t)n * nd, 0);
-    for (int b = 0; b < n; b++) {
-        const sm::NlTree& t = trees[b];
-        std::copy(t.s_cu.begin(), t.s_cu.end(), cu.begin() + (size_t)b * nu);
-        std::copy(t.s_cd.begin(), t.s_cd.end(), cd.begin() + (size_t)b * nd);
-    }
-    std::vector<int> up_off(nu + 1, 0), dn_off(nd + 1, 0);
-    auto offsets = [n](std::vector<int>& cnt, std::vector<int>& off, int nr) {
-        int o = 0;
-        for (int r = 0; r < nr; r++) {
-            off[r] = o;
-            for (int b = 0; b < n; b++) {
-                const int x = cnt[(size_t)b * nr + r];
-                cnt[(size_t)b * nr + r] = o;   // pair b's first slot in round r
-                o += x;
-            }
-        }
-        off[nr] = o;
-    };
-    offsets(cu, up_off, nu);
-    offsets(cd, dn_off, nd);
-    // device tables: ints [4][cap * npix]: chain_start, chain_len, order_up, order_down
-    int* tabs = c->nl_tabs_h.data();
-    int* cs = tabs;
-    int* cl = tabs + slot;
-    int* ord_up = tabs + 2 * slot;
-    int* ord_dn = tabs + 3 * slot;
-    const bool tabled = parallel([&](int b) {
-        const sm::NlTree& t = trees[b];
-        const int r0 = b * (int)np, c0 = coff[b];
-        int* pu = &cu[(size_t)b * nu];
-        int* pd = &cd[(size_t)b * nd];
-        for (size_t k = 0; k < t.chain_len.size(); k++) {
-            const int g = c0 + (int)k;
-            cs[g] = t.chain_start[k] + r0;
-            cl[g] = t.chain_len[k];
-            ord_up[pu[t.up_level[k]]++] = g;
-            ord_dn[pd[t.down_level[k]]++] = g;
-        }
-    });
-    if (!tabled) return fail(c, SM_ENOMEM, "NL: path tables could not be written");
-    phase("records");
-    int* I = c->nl_ints;
-    int* rec_d = c->nl_rec + sm::NL_REC_PAD * 4;
-    for (int k = 0; k < 4; k++)   // the tables' used heads only
-        HIP_TRY(c, hipMemcpyAsync(I + k * slot, tabs + k * slot, (size_t)nchain * 4, hipMemcpyHostToDevice, c->st));
-    for (int b = 0; b < n; b++) {
-        HIP_TRY(c, hipMemcpyAsync(rec_d + (size_t)b * np * 4, trees[b].s_rec.data(), np * 16, hipMemcpyHostToDevice, c->st));
-        HIP_TRY(c, hipMemcpyAsync(c->nl_wsum + (size_t)b * np, trees[b].s_wsum.data(), np * 4, hipMemcpyHostToDevice, c->st));
-    }
-    HIP_TRY(c, hipEventRecord(c->nl_ev_up, c->st));
-    phase("upload");
+    HIP_TRY(c, hipStreamSynchronize(c->nl_st));   // the round offsets (the records are then in place)
+    const int* up_off = c->nl_offs_h;
+    const int* dn_off = c->nl_offs_h + sm::NL_LEVELS + 1;
+    if (c->nl_offs_h[NOFF - 1] != 0)
+        return fail(c, SM_EINVAL, "NL: spanning tree walk failed (flags " + std::to_string(c->nl_offs_h[NOFF - 1]) + ")");
     sm::NlArgs a{};
     a.chain_start = I;
     a.chain_len = I + slot;
@@ -714,21 +604,21 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     a.table = c->nl_table;
     a.val = c->nl_val;
     a.vm = B.vm0;
-    a.wsum = c->nl_wsum;
+    a.oup = c->nl_oup;
+    a.ofin = c->nl_ofin;
     a.W = W;
     a.solve_all = solve_all;
     a.scale = w;
-    // the cost volume (the weight sums came from the host): up rounds, then down rounds; per
-    // voxel: cost in, up sum out; up sum in, final out, float out (+ the light children's sums,
-    // about one per node)
+    // the cost volume and the ones: up rounds, then down rounds; per voxel: cost in, up sum out;
+    // up sum in, final out, float out (+ the light children's sums, about one per node)
     const double bytes = (double)n * c->nvol * (4 + 8 + 8 + 8 + 8 + 4);
     s = timed(c, "nl_filter", bytes, [&] {
-        for (int r = 0; r <= max_up; r++) sm::launch_nl_round(a, true, up_off[r], up_off[r + 1], D, c->st);
-        for (int r = 0; r <= max_dn; r++) sm::launch_nl_round(a, false, dn_off[r], dn_off[r + 1], D, c->st);
+        for (int r = 0; r < sm::NL_LEVELS; r++) sm::launch_nl_round(a, true, up_off[r], up_off[r + 1], D, c->st);
+        for (int r = 0; r < sm::NL_LEVELS; r++) sm::launch_nl_round(a, false, dn_off[r], dn_off[r + 1], D, c->st);
     });
-    phase("launch");
-    t_prev_end = t_last;
-    return s;
+    if (s) return s;
+    HIP_TRY(c, hipEventRecord(c->nl_ev_set[set], c->st));
+    return SM_OK;
 }
 
 #ifndef SM_FUSE_SOLVE_ALL
@@ -1055,17 +945,21 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         const size_t ne = (size_t)p->rows * (p->cols - 1) + (size_t)(p->rows - 1) * p->cols;
         if ((s = dalloc(c, &c->nl_med, cap * c->npix * 3))) return s;
         if ((s = dalloc(c, &c->nl_ew, cap * ne))) return s;
-        if ((s = dalloc(c, &c->nl_ints, cap * c->npix * 4))) return s;
-        if ((s = dalloc(c, &c->nl_rec, (cap * c->npix + 2 * sm::NL_REC_PAD) * 4))) return s;
-        HIP_TRY(c, hipMemset(c->nl_rec, 0, (cap * c->npix + 2 * sm::NL_REC_PAD) * 16));
+        if ((s = dalloc(c, &c->nl_ints, 2 * cap * c->npix * 4))) return s;
+        if ((s = dalloc(c, &c->nl_rec, 2 * (cap * c->npix + 2 * sm::NL_REC_PAD) * 4))) return s;
+        HIP_TRY(c, hipMemset(c->nl_rec, 0, 2 * (cap * c->npix + 2 * sm::NL_REC_PAD) * 16));
         if ((s = dalloc(c, &c->nl_table, 256))) return s;
         if ((s = dalloc(c, &c->nl_val, cap * c->nvol))) return s;
-        if ((s = dalloc(c, &c->nl_wsum, cap * c->npix))) return s;
+        if ((s = dalloc(c, &c->nl_oup, cap * c->npix))) return s;
+        if ((s = dalloc(c, &c->nl_ofin, cap * c->npix))) return s;
+        if ((s = dalloc(c, &c->nl_walk, sm::nl_walk_scratch_bytes(p->rows, p->cols, cap)))) return s;
+        if ((s = dalloc(c, &c->nl_offs, 2 * (sm::NL_LEVELS + 1) + 1))) return s;
+        HIP_TRY(c, hipHostMalloc((void**)&c->nl_offs_h, (2 * (sm::NL_LEVELS + 1) + 1) * sizeof(int), hipHostMallocDefault));
         if ((s = dalloc(c, &c->nl_par, cap * c->npix))) return s;
         if ((s = dalloc(c, &c->nl_best, cap * c->npix))) return s;
         if ((s = dalloc(c, &c->nl_mst, sm::nl_mst_scratch_bytes(p->rows, p->cols, cap)))) return s;
         if ((s = dalloc(c, &c->nl_adj, cap * c->npix))) return s;
-        double* table = c->nl_table_h;
+        double table[256];
         const double sg = p->nl_sigma < 0.01 ? 0.01 : p->nl_sigma;   // update_table (qx_tree_filter.cpp:23-24)
         for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));
         HIP_TRY(c, hipMemcpy(c->nl_table, table, 256 * sizeof(double), hipMemcpyHostToDevice));

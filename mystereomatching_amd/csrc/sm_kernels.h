@@ -145,10 +145,19 @@ struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids =
     float* vm;                  // [nodes][D] costs in, normalised aggregated costs out
     int solve_all;              // 1: vm out is SolveAll's `0 + w * v` (cpp:2189-2201), w = scale
     float scale;
-    const float* wsum;          // [nodes] the filtered ones (host, nl_weight_sums)
+    double* oup;                // [nodes] the ones volume's up sums (qx_tree_filter on ones)
+    double* ofin;               // [nodes] its final sums: the normaliser fin(1)
     int W;
 };
 constexpr int NL_REC_PAD = 64;  // zero records after the last path (blocked reads past a path's end)
+constexpr int NL_LEVELS = 32;   // round tables of the GPU tree walk (light depth <= log2(H W) < 32)
+// The tree walk on the GPU (sm_nl_walk.hip): from the neighbour words adj [n H W] of the spanning
+// trees, the path records rec [n H W] (bottom -> top per path), chain_start / chain_len per path
+// (indexed by the path top's preorder position), the paths of every up / down round (order_up,
+// order_down) and offs [2 (NL_LEVELS + 1) + 1]: up round offsets, down round offsets, error flags.
+size_t nl_walk_scratch_bytes(int H, int W, int n);
+void launch_nl_walk(const uint32_t* adj, int H, int W, int n, uint8_t* scratch, int4* rec, int* chain_start, int* chain_len,
+                    int* order_up, int* order_down, int* offs, hipStream_t st);
 void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8_t* ew, int H, int W, int n, hipStream_t st);
 void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_t st);
 // minimum spanning trees of n pairs' edge weights (sm_nl_mst.hip): par / best [n H W] and

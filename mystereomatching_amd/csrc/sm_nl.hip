@@ -3,13 +3,13 @@
 //
 //   edges      ctmf 3x3 median of each channel with clamped borders (NL/ctmf.c, called with r = 1
 //              by qx_mst_kruskals_image::mst), weight = max channel |difference| of 4-neighbours
-//   tree       GPU spanning trees (sm_nl_mst.hip), host breadth-first orientation + heavy paths
-//              (sm_nl_tree.cpp)
+//   tree       GPU spanning trees (sm_nl_mst.hip), rooted at pixel 0 and cut into heavy paths on
+//              the GPU (sm_nl_walk.hip)
 //   filter     qx_tree_filter::filter (NL/qx_tree_filter.cpp:61-117) in double, w = exp(-c / 25.5):
 //                up(x)  = C(x) + sum_j up(child_j) * w(child_j)           children in list order
 //                fin(x) = w(x) * (fin(parent) - w(x) * up(x)) + up(x),    fin(root) = up(root)
 //   NL()       vm = (float)fin(C) / (float)fin(1)   (the ones volume, cpp:4899-4910; fin(1) depends
-//              only on the tree and is filtered on the host with the tree, sm_nl_tree.cpp)
+//              only on the tree and is filtered here too, as one more channel of the same walk)
 //
 // gfx950 mapping: one wave per (heavy path, 64-disparity chunk), lane = disparity, walking the path
 // node by node; the child on the same path arrives in a register, the other children (their paths
@@ -124,6 +124,7 @@ struct NlUpBlock {
     int4 r[K];
     float cost[K];
     double wh[K], lm[K][4];
+    double lo[K][4];   // the ones channel's off-path children (uniform across the wave)
 };
 
 // issue the block's loads (uniform branches; nothing here waits for them)
@@ -138,12 +139,16 @@ __device__ __forceinline__ void nl_up_load(NlUpBlock<K>& B, const NlArgs& a, con
         const int nc = r.y & 7, hv = ((r.y >> 3) & 7) - 1;
         B.cost[k] = 0.0f;
 #pragma unroll
-        for (int j = 0; j < 4; j++) B.lm[k][j] = 0.0;
+        for (int j = 0; j < 4; j++) B.lm[k][j] = B.lo[k][j] = 0.0;
         if (b + k >= len) continue;                     // no loads past the path
         B.cost[k] = a.vm[(size_t)r.x * P + d];
 #pragma unroll
         for (int j = 0; j < 4; j++)
-            if (j < nc && j != hv) B.lm[k][j] = a.val[(size_t)nl_child(r.x, r.y, j, a.W) * P + d];
+            if (j < nc && j != hv) {
+                const int ch = nl_child(r.x, r.y, j, a.W);
+                B.lm[k][j] = a.val[(size_t)ch * P + d];
+                B.lo[k][j] = a.oup[ch];
+            }
     }
 }
 
@@ -156,27 +161,38 @@ __device__ __forceinline__ void nl_up_weigh(NlUpBlock<K>& B, const double* __res
         const int hv = ((r.y >> 3) & 7) - 1;
         B.wh[k] = hv >= 0 ? table[(r.z >> (8 * hv)) & 255] : 0.0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) B.lm[k][j] = B.lm[k][j] * table[(r.z >> (8 * j)) & 255];
+        for (int j = 0; j < 4; j++) {
+            const double t = table[(r.z >> (8 * j)) & 255];
+            B.lm[k][j] = B.lm[k][j] * t;
+            B.lo[k][j] = B.lo[k][j] * t;
+        }
     }
 }
 
+// (the ones channel: up(1) = 1 + sum_j up_1(child_j) * w(child_j), the same order; every wave
+// of the path computes it, the first lane of chunk 0 stores it)
 template <int K>
 __device__ __forceinline__ void nl_up_compute(const NlUpBlock<K>& B, const NlArgs& a, int b, int len, int P, int d,
-                                              double& carry) {
+                                              double& carry, double& carry_o) {
 #pragma unroll
     for (int k = 0; k < K; k++) {
         if (b + k >= len) break;
         const int4 r = B.r[k];
         const int nc = r.y & 7, hv = ((r.y >> 3) & 7) - 1;
         double v = (double)B.cost[k];
+        double vo = 1.0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             if (j >= nc) break;
             const double m = (j == hv) ? carry * B.wh[k] : B.lm[k][j];
+            const double mo = (j == hv) ? carry_o * B.wh[k] : B.lo[k][j];
             v = v + m;
+            vo = vo + mo;
         }
         a.val[(size_t)r.x * P + d] = v;
+        if (d == 0) a.oup[r.x] = vo;
         carry = v;
+        carry_o = vo;
     }
 }
 
@@ -193,25 +209,25 @@ __global__ __launch_bounds__(64 * SM_NL_WAVES) void k_nl_up(const NlArgs a, cons
     if (d >= P) return;
     const int4* __restrict__ R = rec + a.chain_start[ci];
     const int len = a.chain_len[ci];
-    double carry = 0.0;
+    double carry = 0.0, carry_o = 0.0;
 #if SM_NL_PIPE
     NlUpBlock<K> X, Y;
     nl_up_load(X, a, R, 0, len, P, d);
     for (int b = 0; b < len; b += 2 * K) {
         nl_up_load(Y, a, R, b + K, len, P, d);
         nl_up_weigh(X, table);
-        nl_up_compute(X, a, b, len, P, d, carry);
+        nl_up_compute(X, a, b, len, P, d, carry, carry_o);
         if (b + K >= len) break;
         nl_up_load(X, a, R, b + 2 * K, len, P, d);
         nl_up_weigh(Y, table);
-        nl_up_compute(Y, a, b + K, len, P, d, carry);
+        nl_up_compute(Y, a, b + K, len, P, d, carry, carry_o);
     }
 #else
     for (int b = 0; b < len; b += K) {
         NlUpBlock<K> X;
         nl_up_load(X, a, R, b, len, P, d);
         nl_up_weigh(X, table);
-        nl_up_compute(X, a, b, len, P, d, carry);
+        nl_up_compute(X, a, b, len, P, d, carry, carry_o);
     }
 #endif
 }
@@ -223,7 +239,7 @@ template <int K>
 struct NlDownBlock {
     int4 r[K];
     double up[K];
-    float ws[K];
+    double uo[K];      // the ones channel's up sum (uniform across the wave)
 };
 
 template <int K>
@@ -235,16 +251,16 @@ __device__ __forceinline__ void nl_down_load(NlDownBlock<K>& B, const NlArgs& a,
     for (int k = 0; k < K; k++) {
         const int4 r = B.r[k];
         B.up[k] = 0.0;
-        B.ws[k] = 1.0f;
+        B.uo[k] = 1.0;
         if (b - k < 0) continue;                        // no loads before the path
         B.up[k] = a.val[(size_t)r.x * P + d];
-        B.ws[k] = a.wsum[r.x];
+        B.uo[k] = a.oup[r.x];
     }
 }
 
 template <int K>
 __device__ __forceinline__ void nl_down_compute(const NlDownBlock<K>& B, const NlArgs& a, const double* __restrict__ table,
-                                                int b, int P, int d, double& carry) {
+                                                int b, int P, int d, double& carry, double& carry_o) {
     double w[K];
 #pragma unroll
     for (int k = 0; k < K; k++) w[k] = table[(B.r[k].y >> 16) & 255];
@@ -252,18 +268,25 @@ __device__ __forceinline__ void nl_down_compute(const NlDownBlock<K>& B, const N
     for (int k = 0; k < K; k++) {
         if (b - k < 0) break;
         const int4 r = B.r[k];
-        double fin;
+        double fin, fo;
         if (r.w == r.x) {
             fin = B.up[k];                              // the root
+            fo = B.uo[k];
         } else {
             const double m = w[k] * B.up[k];
             const double q = carry - m;
             const double s = w[k] * q;
             fin = s + B.up[k];
+            const double mo = w[k] * B.uo[k];
+            const double qo = carry_o - mo;
+            const double so = w[k] * qo;
+            fo = so + B.uo[k];
         }
         a.val[(size_t)r.x * P + d] = fin;
+        if (d == 0) a.ofin[r.x] = fo;
         carry = fin;
-        float out = (float)fin / B.ws[k];
+        carry_o = fo;
+        float out = (float)fin / (float)fo;
         if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
             float sum = 0.f;
             sum += a.scale * out;
@@ -287,21 +310,22 @@ __global__ __launch_bounds__(64 * SM_NL_WAVES) void k_nl_down(const NlArgs a, co
     const int4 top = R[len - 1];
     // the top's parent is on a path finished in an earlier round (or the top is the root)
     double carry = top.w == top.x ? 0.0 : a.val[(size_t)top.w * P + d];
+    double carry_o = top.w == top.x ? 0.0 : a.ofin[top.w];
 #if SM_NL_PIPE
     NlDownBlock<K> X, Y;
     nl_down_load(X, a, R, len - 1, P, d);
     for (int b = len - 1; b >= 0; b -= 2 * K) {
         nl_down_load(Y, a, R, b - K, P, d);
-        nl_down_compute(X, a, table, b, P, d, carry);
+        nl_down_compute(X, a, table, b, P, d, carry, carry_o);
         if (b - K < 0) break;
         nl_down_load(X, a, R, b - 2 * K, P, d);
-        nl_down_compute(Y, a, table, b - K, P, d, carry);
+        nl_down_compute(Y, a, table, b - K, P, d, carry, carry_o);
     }
 #else
     for (int b = len - 1; b >= 0; b -= K) {
         NlDownBlock<K> X;
         nl_down_load(X, a, R, b, P, d);
-        nl_down_compute(X, a, table, b, P, d, carry);
+        nl_down_compute(X, a, table, b, P, d, carry, carry_o);
     }
 #endif
 }

@@ -330,6 +330,250 @@ __global__ __launch_bounds__(64 * SM_NL_WAVES) void k_nl_down(const NlArgs a, co
 #endif
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Producer / consumer rounds.  The last up rounds and the first down rounds hold a few long
+// paths (Teddy: the root's heavy path has ~3000 nodes), and there a wave walking its path waits
+// on every block's records and then on the block's data loads (~0.3-0.4 us per node).  In these
+// rounds a workgroup of 1 + PC_P waves owns one (path, 64-disparity chunk): producer wave p loads
+// the nodes of ring slot c (c = p mod PC_P: PC_C nodes' records, costs or up sums, the light
+// children's sums and the weights), keeps the loads in flight for two steps and then writes the
+// slot -- weighted products ready -- into LDS; the consumer wave runs the node chain out of LDS
+// three steps after the slot's loads were issued.  One barrier per step of PC_C nodes; the
+// arithmetic and its order are the block kernels' above (bit-exact).
+#ifndef SM_NL_PC_UNITS
+#define SM_NL_PC_UNITS 512   // rounds of fewer (path, chunk) units use the producer/consumer kernels (0: never)
+#endif
+constexpr int PC_C = 16;     // nodes per ring slot
+constexpr int PC_R = 4;      // ring slots (a slot is written 2 steps after its loads, read 1 step later)
+constexpr int PC_P = 3;      // producer waves
+
+struct PcUpSlot {
+    int4 rec[PC_C];
+    double wh[PC_C];         // the heavy child's weight (0: none)
+    double lo[PC_C][4];      // the ones channel's light products by child position (0: heavy / none)
+    float cost[PC_C][64];
+    double lm[PC_C][4][64];  // light products (lane = disparity) by child position (0: heavy / none)
+};
+struct PcDnSlot {
+    int4 rec[PC_C];
+    double w[PC_C];          // the node's own weight
+    double uo[PC_C];         // the ones channel's up sum
+    double up[PC_C][64];
+};
+
+__device__ __forceinline__ double rdlane_f64(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l), hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
+// Consumers run a slot's PC_C nodes as straight-line code (the LDS reads of later nodes issue
+// ahead of the chain): absent and heavy children hold +0 in the light arrays, and adding +0 leaves
+// every sum unchanged (sums are >= +0, never -0), so the child loop needs no branches; the heavy
+// child's term is selected at its position in the child order.
+__global__ __launch_bounds__(64 * (1 + PC_P), 1) void k_nl_up_pc(const NlArgs a, const int4* __restrict__ rec,
+                                                                  const double* __restrict__ table, int lo, int nunits, int P) {
+    extern __shared__ __align__(16) unsigned char pc_smem[];
+    PcUpSlot* S = (PcUpSlot*)pc_smem;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int nchunks = (P + 63) >> 6;
+    const int u = blockIdx.x;
+    if (u >= nunits) return;
+    const int ci = a.order_up[lo + u / nchunks];
+    const int d = (u % nchunks) * 64 + lane;
+    const bool dok = d < P;
+    const int4* __restrict__ R = rec + a.chain_start[ci];
+    const int len = a.chain_len[ci];
+    const int nst = (len + PC_C - 1) / PC_C;
+    double carry = 0.0, carry_o = 0.0;
+    // producer state: records of the chunk being loaded (lane t < PC_C: node t) and of the next one
+    int4 rc = make_int4(0, 0, 0, 0), rn = make_int4(0, 0, 0, 0);
+    float xc[PC_C];
+    double xm[PC_C][4];
+    double xo = 0.0, xw = 0.0;   // lane t: child position t % 4 of node t / 4: its ones up sum, weight
+    double xh = 0.0;             // lane t < PC_C: node t's heavy-child weight
+    const int p = wv - 1;
+    if (wv > 0 && p < nst && lane < PC_C) rc = R[p * PC_C + lane];
+    for (int s = 0; s < nst + 3; s++) {
+        if (wv == 0) {
+            const int c = s - 3;
+            if (c >= 0) {
+                const PcUpSlot& B = S[c % PC_R];
+#pragma unroll
+                for (int k = 0; k < PC_C; k++) {
+                    const bool ok = c * PC_C + k < len;
+                    const int4 r = B.rec[k];
+                    const int x = __builtin_amdgcn_readfirstlane(r.x), meta = __builtin_amdgcn_readfirstlane(r.y);
+                    const int hv = ((meta >> 3) & 7) - 1;
+                    const double h = carry * B.wh[k], ho = carry_o * B.wh[k];
+                    double v = (double)B.cost[k][lane];
+                    double vo = 1.0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        v = v + (j == hv ? h : B.lm[k][j][lane]);
+                        vo = vo + (j == hv ? ho : B.lo[k][j]);
+                    }
+                    if (ok) {
+                        if (dok) a.val[(size_t)x * P + d] = v;
+                        if (d == 0) a.oup[x] = vo;
+                        carry = v;
+                        carry_o = vo;
+                    }
+                }
+            }
+        } else {
+            // write the slot whose loads were issued two steps ago
+            const int cw = s - 2;
+            if (cw >= 0 && cw < nst && cw % PC_P == p) {
+                PcUpSlot& B = S[cw % PC_R];
+                if (lane < PC_C) {
+                    B.rec[lane] = rc;
+                    B.wh[lane] = xh;
+                }
+                B.lo[lane >> 2][lane & 3] = xo * xw;
+#pragma unroll
+                for (int k = 0; k < PC_C; k++) {
+                    B.cost[k][lane] = xc[k];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) B.lm[k][j][lane] = xm[k][j] * rdlane_f64(xw, 4 * k + j);
+                }
+                rc = rn;   // the records of this producer's next chunk (cw + PC_P)
+            }
+            // issue the loads of chunk s (its records were loaded a producer cycle earlier)
+            if (s < nst && s % PC_P == p) {
+                if (s + PC_P < nst && lane < PC_C) rn = R[(s + PC_P) * PC_C + lane];
+#pragma unroll
+                for (int k = 0; k < PC_C; k++) {
+                    const int x = __builtin_amdgcn_readlane(rc.x, k), meta = __builtin_amdgcn_readlane(rc.y, k);
+                    const int nc = meta & 7, hv = ((meta >> 3) & 7) - 1;
+                    xc[k] = 0.0f;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) xm[k][j] = 0.0;
+                    if (s * PC_C + k >= len) continue;
+                    if (dok) xc[k] = a.vm[(size_t)x * P + d];
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (j < nc && j != hv && dok) xm[k][j] = a.val[(size_t)nl_child(x, meta, j, a.W) * P + d];
+                }
+                // lane t: child position t % 4 of node t / 4 (weights of every child; the ones sum
+                // of the light ones)
+                const int kt = lane >> 2, jt = lane & 3;
+                const int xk = __shfl(rc.x, kt), mk = __shfl(rc.y, kt), wk = __shfl(rc.z, kt);
+                const int nck = mk & 7, hvk = ((mk >> 3) & 7) - 1;
+                const bool here = s * PC_C + kt < len && jt < nck;
+                xw = here ? table[(wk >> (8 * jt)) & 255] : 0.0;
+                xo = (here && jt != hvk) ? a.oup[nl_child(xk, mk, jt, a.W)] : 0.0;
+                xh = 0.0;
+                if (lane < PC_C && s * PC_C + lane < len) {
+                    const int hvl = ((rc.y >> 3) & 7) - 1;
+                    if (hvl >= 0) xh = table[(rc.z >> (8 * hvl)) & 255];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64 * (1 + PC_P), 1) void k_nl_down_pc(const NlArgs a, const int4* __restrict__ rec,
+                                                                    const double* __restrict__ table, int lo, int nunits, int P) {
+    extern __shared__ __align__(16) unsigned char pc_smem[];
+    PcDnSlot* S = (PcDnSlot*)pc_smem;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int nchunks = (P + 63) >> 6;
+    const int u = blockIdx.x;
+    if (u >= nunits) return;
+    const int ci = a.order_down[lo + u / nchunks];
+    const int d = (u % nchunks) * 64 + lane;
+    const bool dok = d < P;
+    const int4* __restrict__ R = rec + a.chain_start[ci];
+    const int len = a.chain_len[ci];
+    const int nst = (len + PC_C - 1) / PC_C;
+    double carry = 0.0, carry_o = 0.0;
+    if (wv == 0) {
+        // the top's parent is on a path finished in an earlier round (or the top is the root)
+        const int4 top = R[len - 1];
+        if (top.w != top.x) {
+            carry = dok ? a.val[(size_t)top.w * P + d] : 0.0;
+            carry_o = a.ofin[top.w];
+        }
+    }
+    int4 rc = make_int4(0, 0, 0, 0), rn = make_int4(0, 0, 0, 0);
+    double xu[PC_C];
+    double xo = 0.0, xw = 0.0;   // lane t < PC_C: node t's ones up sum and own weight
+    const int p = wv - 1;
+    // chunk c holds path positions len - 1 - c PC_C - k, k = 0 .. PC_C - 1 (top -> bottom)
+    if (wv > 0 && p < nst && lane < PC_C) rc = R[len - 1 - p * PC_C - lane];
+    for (int s = 0; s < nst + 3; s++) {
+        if (wv == 0) {
+            const int c = s - 3;
+            if (c >= 0) {
+                const PcDnSlot& B = S[c % PC_R];
+#pragma unroll
+                for (int k = 0; k < PC_C; k++) {
+                    const bool ok = c * PC_C + k < len;
+                    const int4 r = B.rec[k];
+                    const int x = __builtin_amdgcn_readfirstlane(r.x), par = __builtin_amdgcn_readfirstlane(r.w);
+                    const double up = B.up[k][lane], uo = B.uo[k], w = B.w[k];
+                    const double m = w * up;
+                    const double q = carry - m;
+                    const double sv = w * q;
+                    const double mo = w * uo;
+                    const double qo = carry_o - mo;
+                    const double so = w * qo;
+                    const double fin = par == x ? up : sv + up;   // the root keeps its up sum
+                    const double fo = par == x ? uo : so + uo;
+                    float out = (float)fin / (float)fo;
+                    if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
+                        float sum = 0.f;
+                        sum += a.scale * out;
+                        out = sum;
+                    }
+                    if (ok) {
+                        if (d == 0) a.ofin[x] = fo;
+                        if (dok) {
+                            a.val[(size_t)x * P + d] = fin;
+                            a.vm[(size_t)x * P + d] = out;
+                        }
+                        carry = fin;
+                        carry_o = fo;
+                    }
+                }
+            }
+        } else {
+            const int cw = s - 2;
+            if (cw >= 0 && cw < nst && cw % PC_P == p) {
+                PcDnSlot& B = S[cw % PC_R];
+                if (lane < PC_C) {
+                    B.rec[lane] = rc;
+                    B.uo[lane] = xo;
+                    B.w[lane] = xw;
+                }
+#pragma unroll
+                for (int k = 0; k < PC_C; k++) B.up[k][lane] = xu[k];
+                rc = rn;
+            }
+            if (s < nst && s % PC_P == p) {
+                if (s + PC_P < nst && lane < PC_C) rn = R[len - 1 - (s + PC_P) * PC_C - lane];
+#pragma unroll
+                for (int k = 0; k < PC_C; k++) {
+                    const int x = __builtin_amdgcn_readlane(rc.x, k);
+                    xu[k] = 0.0;
+                    if (s * PC_C + k >= len) continue;
+                    if (dok) xu[k] = a.val[(size_t)x * P + d];
+                }
+                xo = 0.0;
+                xw = 0.0;
+                if (lane < PC_C && s * PC_C + lane < len) {
+                    xo = a.oup[rc.x];
+                    xw = table[(rc.y >> 16) & 255];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8_t* ew, int H, int W, int n, hipStream_t st) {
@@ -342,6 +586,19 @@ void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8
 void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_t st) {
     if (hi <= lo) return;
     const int nchunks = (P + 63) / 64, nunits = (hi - lo) * nchunks;
+    if (nunits < SM_NL_PC_UNITS) {
+        static bool attr = false;   // LDS above the 64 KiB default
+        if (!attr) {
+            hipFuncSetAttribute((const void*)k_nl_up_pc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_R * sizeof(PcUpSlot)));
+            hipFuncSetAttribute((const void*)k_nl_down_pc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_R * sizeof(PcDnSlot)));
+            attr = true;
+        }
+        if (up)
+            hipLaunchKernelGGL(k_nl_up_pc, dim3(nunits), dim3(64 * (1 + PC_P)), PC_R * sizeof(PcUpSlot), st, a, a.rec, a.table, lo, nunits, P);
+        else
+            hipLaunchKernelGGL(k_nl_down_pc, dim3(nunits), dim3(64 * (1 + PC_P)), PC_R * sizeof(PcDnSlot), st, a, a.rec, a.table, lo, nunits, P);
+        return;
+    }
     const dim3 grid((unsigned)((nunits + SM_NL_WAVES - 1) / SM_NL_WAVES)), block(64 * SM_NL_WAVES);
     constexpr int K = SM_NL_BLOCK;
     if (up)

@@ -147,6 +147,7 @@ struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids =
     float scale;
     double* oup;                // [nodes] the ones volume's up sums (qx_tree_filter on ones)
     double* ofin;               // [nodes] its final sums: the normaliser fin(1)
+    long nodes;                 // n H W
     int W;
 };
 constexpr int NL_REC_PAD = 64;  // zero records after the last path (blocked reads past a path's end)

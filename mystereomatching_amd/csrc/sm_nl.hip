@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sm_device.h"
 #include "sm_kernels.h"
 
@@ -335,44 +337,168 @@ __global__ __launch_bounds__(64 * SM_NL_WAVES) void k_nl_down(const NlArgs a, co
 // Producer / consumer rounds.  The last up rounds and the first down rounds hold a few long
 // paths (Teddy: the root's heavy path has ~3000 nodes), and there a wave walking its path waits
 // on every block's records and then on the block's data loads (~0.3-0.4 us per node).  In these
-// rounds a workgroup of 1 + PC_P waves owns one (path, 64-disparity chunk): producer wave p loads
-// the nodes of ring slot c (c = p mod PC_P: PC_C nodes' records, costs or up sums, the light
-// children's sums and the weights), keeps the loads in flight for two steps and then writes the
-// slot -- weighted products ready -- into LDS; the consumer wave runs the node chain out of LDS
-// three steps after the slot's loads were issued.  One barrier per step of PC_C nodes; the
+// rounds a workgroup of 1 + PC_P PC_C / PC_H waves owns one (path, 64-disparity chunk): producer group p
+// (PC_C / PC_H waves, PC_H nodes each) loads the nodes of chunk c (c = p mod PC_P: PC_C nodes'
+// records, costs or up sums, the light children's sums and the weights), keeps the loads in flight
+// for PC_P - 1 steps and then writes one of two LDS slots -- weighted and pre-summed; the consumer
+// wave runs the node chain out of that slot in the next step.  One barrier per step of PC_C nodes; the
 // arithmetic and its order are the block kernels' above (bit-exact).
 #ifndef SM_NL_PC_UNITS
 #define SM_NL_PC_UNITS 512   // rounds of fewer (path, chunk) units use the producer/consumer kernels (0: never)
 #endif
-constexpr int PC_C = 16;     // nodes per ring slot
-constexpr int PC_R = 4;      // ring slots (a slot is written 2 steps after its loads, read 1 step later)
-constexpr int PC_P = 3;      // producer waves
+#ifndef SM_NL_PC_C
+#define SM_NL_PC_C 8         // nodes per chunk (ring slot)
+#endif
+constexpr int PC_C = SM_NL_PC_C;
+#ifndef SM_NL_PC_P
+#define SM_NL_PC_P 3         // producer groups: a chunk's loads are issued PC_P - 1 steps before its write
+#endif
+constexpr int PC_P = SM_NL_PC_P;
+constexpr int PC_R = 2;      // ring slots: a slot is read the step after its write, while the next one is written
+#ifndef SM_NL_PC_H
+#define SM_NL_PC_H 2         // nodes per producer wave (PC_C / PC_H producer waves per group share a chunk)
+#endif
+constexpr int PC_H = SM_NL_PC_H;
+#ifndef SM_NL_PC_PROBE
+#define SM_NL_PC_PROBE 0     // timing probes only (wrong results): 1 producers skip the data loads, 2 the consumer skips its stores
+#endif
+constexpr int PC_NH = PC_C / PC_H;
+constexpr int PC_WAVES = 1 + PC_NH * PC_P;
+static_assert(PC_WAVES <= 16 && PC_C % PC_H == 0, "a workgroup holds at most 1024 threads");
 
 struct PcUpSlot {
     int4 rec[PC_C];
+    double4 lu[PC_C][64];    // per lane (disparity): {pre, post1, post2, post3} (see below)
+    double4 ou[PC_C];        // the ones channel: {pre, post1, post2, post3}
     double wh[PC_C];         // the heavy child's weight (0: none)
-    double lo[PC_C][4];      // the ones channel's light products by child position (0: heavy / none)
-    float cost[PC_C][64];
-    double lm[PC_C][4][64];  // light products (lane = disparity) by child position (0: heavy / none)
 };
 struct PcDnSlot {
     int4 rec[PC_C];
-    double w[PC_C];          // the node's own weight
+    double w[PC_C];          // the node's own weight (0 for the root: fin = 0 (carry - 0) + up = up)
     double uo[PC_C];         // the ones channel's up sum
     double up[PC_C][64];
 };
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double rdlane_f64(double v, int l) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l), hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
     return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
 }
 
-// Consumers run a slot's PC_C nodes as straight-line code (the LDS reads of later nodes issue
-// ahead of the chain): absent and heavy children hold +0 in the light arrays, and adding +0 leaves
-// every sum unchanged (sums are >= +0, never -0), so the child loop needs no branches; the heavy
-// child's term is selected at its position in the child order.
-__global__ __launch_bounds__(64 * (1 + PC_P), 1) void k_nl_up_pc(const NlArgs a, const int4* __restrict__ rec,
+// The up sum of a node is ((cost + m_0) + m_1) + ... in child order, the heavy child's term
+// m_hv = carry * w_hv the only one on the chain.  The producer adds the terms before it (pre =
+// ((cost + m_0) + ...) + m_(hv-1)) and lines up the ones after it (post1..3, +0 where absent:
+// adding +0 leaves every sum unchanged, sums are >= +0), so the consumer's chain is always
+// (((pre + carry w_hv) + post1) + post2) + post3 -- the reference's additions in the reference's
+// order, no selects or branches (a node without children has w_hv = 0, and pre + 0 = pre).
+// Each wave type runs its own step loop (barriers only have to match in number): producer PP
+// handles chunks PP, PP + PC_P, ...; its body for chunk c spans steps c .. c + PC_P - 1 -- issue,
+// PC_P - 2 idle steps, write -- as straight-line code, so the compiler's wait for the loads sits at
+// the write (PC_P - 1 barriers after the issue) and nowhere earlier.
+// producer wave w (0-based) = group w % PC_P, half w / PC_P: a compile-time (group, half) pair
+template <int W, typename F>
+__device__ __forceinline__ void pc_dispatch(int w, F&& f) {
+    if constexpr (W < PC_P * PC_NH) {
+        if (w == W) f(std::integral_constant<int, W % PC_P>{}, std::integral_constant<int, W / PC_P>{});
+        else pc_dispatch<W + 1>(w, f);
+    }
+}
+
+struct PcCtx {
+    const int4* R;
+    int len, nst, d, lane;
+    bool dok;
+};
+
+template <int PP, int HF>
+__device__ __forceinline__ void nl_up_producer(PcUpSlot* S, const NlArgs& a, const double* __restrict__ table, const PcCtx& q, int P) {
+    constexpr int K0 = HF * PC_H;   // this producer's nodes of a chunk: K0 .. K0 + PC_H - 1
+    const int lane = q.lane, d = q.d, len = q.len, nst = q.nst;
+    const bool dok = q.dok;
+    int step = 0;
+    for (; step < PP; step++) __syncthreads();
+    int4 rc = make_int4(0, 0, 0, 0);
+    if (PP < nst && lane < PC_C) rc = q.R[PP * PC_C + lane];
+    for (int c = PP; c < nst; c += PC_P) {
+        // step c: issue the loads, then the records of this producer's next chunk (issued last:
+        // the next chunk's first readlane then waits for nothing younger)
+        float xc[PC_H];
+        double xm[PC_H][4];
+#pragma unroll
+        for (int kk = 0; kk < PC_H; kk++) {
+            const int k = K0 + kk;
+            const int x = __builtin_amdgcn_readlane(rc.x, k), meta = __builtin_amdgcn_readlane(rc.y, k);
+            const int nc = meta & 7, hv = ((meta >> 3) & 7) - 1;
+            xc[kk] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 4; j++) xm[kk][j] = 0.0;
+            if (c * PC_C + k >= len || (SM_NL_PC_PROBE & 1)) continue;
+            if (dok) xc[kk] = a.vm[(size_t)x * P + d];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (j < nc && j != hv && dok) xm[kk][j] = a.val[(size_t)nl_child(x, meta, j, a.W) * P + d];
+        }
+        // lane t < 4 PC_H: child position t % 4 of node K0 + t / 4 (weights of every child, the
+        // ones sum of the light ones)
+        const int kt = K0 + ((lane >> 2) & (PC_H - 1)), jt = lane & 3;   // (PC_H <= 16)
+        const int xk = __shfl(rc.x, kt), mk = __shfl(rc.y, kt), wk = __shfl(rc.z, kt);
+        const int nck = mk & 7, hvk = ((mk >> 3) & 7) - 1;
+        const bool here = lane < 4 * PC_H && c * PC_C + kt < len && jt < nck;
+        const double xw = here ? table[(wk >> (8 * jt)) & 255] : 0.0;
+        const double xo = (here && jt != hvk && !(SM_NL_PC_PROBE & 1)) ? a.oup[nl_child(xk, mk, jt, a.W)] : 0.0;
+        int4 rn = make_int4(0, 0, 0, 0);
+        if (c + PC_P < nst && lane < PC_C) rn = q.R[(c + PC_P) * PC_C + lane];
+        for (int i = 0; i < PC_P - 1; i++) __syncthreads();   // steps c .. c + PC_P - 2: the loads stay in flight
+        // step c + PC_P - 1: write the slot's nodes K0 .. K0 + PC_H - 1
+        PcUpSlot& B = S[c % PC_R];
+        if (lane >= K0 && lane < K0 + PC_H) B.rec[lane] = rc;
+        // the ones channel, lane-parallel: lane kk < PC_H sums node K0 + kk's four terms
+        {
+            const double mo_t = xo * xw;   // lane t: the ones term of position t % 4 of node K0 + t / 4
+            const int kk = lane & (PC_H - 1);
+            const int hvl = ((__shfl(rc.y, K0 + kk) >> 3) & 7) - 1;
+            double t4[4], w4[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                t4[j] = __shfl(mo_t, 4 * kk + j);
+                w4[j] = __shfl(xw, 4 * kk + j);
+            }
+            double pre = 1.0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) pre = pre + (j < hvl ? t4[j] : 0.0);
+            const double p1 = hvl == 0 ? t4[1] : (hvl == 1 ? t4[2] : (hvl == 2 ? t4[3] : 0.0));
+            const double p2 = hvl == 0 ? t4[2] : (hvl == 1 ? t4[3] : 0.0);
+            const double p3 = hvl == 0 ? t4[3] : 0.0;
+            const double wh = hvl == 0 ? w4[0] : (hvl == 1 ? w4[1] : (hvl == 2 ? w4[2] : (hvl == 3 ? w4[3] : 0.0)));
+            if (lane < PC_H) {
+                B.ou[K0 + kk] = make_double4(pre, p1, p2, p3);
+                B.wh[K0 + kk] = wh;
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < PC_H; kk++) {
+            const int k = K0 + kk;
+            const int hv = ((__builtin_amdgcn_readlane(rc.y, k) >> 3) & 7) - 1;
+            double t4[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) t4[j] = xm[kk][j] * rdlane_f64(xw, 4 * kk + j);
+            double pre = (double)xc[kk];
+#pragma unroll
+            for (int j = 0; j < 4; j++) pre = pre + (j < hv ? t4[j] : 0.0);
+            const double p1 = hv == 0 ? t4[1] : (hv == 1 ? t4[2] : (hv == 2 ? t4[3] : 0.0));
+            const double p2 = hv == 0 ? t4[2] : (hv == 1 ? t4[3] : 0.0);
+            const double p3 = hv == 0 ? t4[3] : 0.0;
+            B.lu[k][lane] = make_double4(pre, p1, p2, p3);
+        }
+        __syncthreads();
+        step += PC_P;
+        rc = rn;
+    }
+    for (; step < nst + PC_P; step++) __syncthreads();
+}
+
+__global__ __launch_bounds__(64 * PC_WAVES, 1) void k_nl_up_pc(const NlArgs a, const int4* __restrict__ rec,
                                                                   const double* __restrict__ table, int lo, int nunits, int P) {
     extern __shared__ __align__(16) unsigned char pc_smem[];
     PcUpSlot* S = (PcUpSlot*)pc_smem;
@@ -381,101 +507,95 @@ __global__ __launch_bounds__(64 * (1 + PC_P), 1) void k_nl_up_pc(const NlArgs a,
     const int u = blockIdx.x;
     if (u >= nunits) return;
     const int ci = a.order_up[lo + u / nchunks];
-    const int d = (u % nchunks) * 64 + lane;
-    const bool dok = d < P;
-    const int4* __restrict__ R = rec + a.chain_start[ci];
-    const int len = a.chain_len[ci];
-    const int nst = (len + PC_C - 1) / PC_C;
+    PcCtx q;
+    q.lane = lane;
+    q.d = (u % nchunks) * 64 + lane;
+    q.dok = q.d < P;
+    q.R = rec + a.chain_start[ci];
+    q.len = a.chain_len[ci];
+    q.nst = (q.len + PC_C - 1) / PC_C;
+    if (wv > 0) {
+        pc_dispatch<0>(wv - 1, [&](auto pp, auto hf) { nl_up_producer<decltype(pp)::value, decltype(hf)::value>(S, a, table, q, P); });
+        return;
+    }
+    __builtin_amdgcn_s_setprio(3);   // the chain: first at its SIMD
+    const int len = q.len;
+    // lanes past P store out of range (dropped) instead of under an exec mask
+    const __amdgpu_buffer_rsrc_t val_r = buf_rsrc(a.val), oup_r = buf_rsrc(a.oup);
+    const uint32_t dof = q.dok ? (uint32_t)q.d * 8u : 0x80000000u;
     double carry = 0.0, carry_o = 0.0;
-    // producer state: records of the chunk being loaded (lane t < PC_C: node t) and of the next one
-    int4 rc = make_int4(0, 0, 0, 0), rn = make_int4(0, 0, 0, 0);
-    float xc[PC_C];
-    double xm[PC_C][4];
-    double xo = 0.0, xw = 0.0;   // lane t: child position t % 4 of node t / 4: its ones up sum, weight
-    double xh = 0.0;             // lane t < PC_C: node t's heavy-child weight
-    const int p = wv - 1;
-    if (wv > 0 && p < nst && lane < PC_C) rc = R[p * PC_C + lane];
-    for (int s = 0; s < nst + 3; s++) {
-        if (wv == 0) {
-            const int c = s - 3;
-            if (c >= 0) {
-                const PcUpSlot& B = S[c % PC_R];
+    auto node = [&](const PcUpSlot& B, int k) {
+        const int x = __builtin_amdgcn_readfirstlane(B.rec[k].x);
+        const double4 L = B.lu[k][lane];
+        const double4 O = B.ou[k];
+        const double wh = B.wh[k];
+        const double v = (((L.x + carry * wh) + L.y) + L.z) + L.w;
+        const double vo = (((O.x + carry_o * wh) + O.y) + O.z) + O.w;
+        const uint32_t row = (uint32_t)x * (uint32_t)P * 8u;   // (volume < 4 GiB: see launch)
+        if (!(SM_NL_PC_PROBE & 2)) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), val_r, dof, row, 0);
+        if (lane == 0 && q.d == 0) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, vo), oup_r, 0, (uint32_t)x * 8u, 0);
+        carry = v;
+        carry_o = vo;
+    };
+    for (int s = 0; s < q.nst + PC_P; s++) {
+        const int c = s - PC_P;
+        if (c >= 0) {
+            const PcUpSlot& B = S[c % PC_R];
+            if ((c + 1) * PC_C <= len) {   // a full slot: straight-line
 #pragma unroll
-                for (int k = 0; k < PC_C; k++) {
-                    const bool ok = c * PC_C + k < len;
-                    const int4 r = B.rec[k];
-                    const int x = __builtin_amdgcn_readfirstlane(r.x), meta = __builtin_amdgcn_readfirstlane(r.y);
-                    const int hv = ((meta >> 3) & 7) - 1;
-                    const double h = carry * B.wh[k], ho = carry_o * B.wh[k];
-                    double v = (double)B.cost[k][lane];
-                    double vo = 1.0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        v = v + (j == hv ? h : B.lm[k][j][lane]);
-                        vo = vo + (j == hv ? ho : B.lo[k][j]);
-                    }
-                    if (ok) {
-                        if (dok) a.val[(size_t)x * P + d] = v;
-                        if (d == 0) a.oup[x] = vo;
-                        carry = v;
-                        carry_o = vo;
-                    }
-                }
-            }
-        } else {
-            // write the slot whose loads were issued two steps ago
-            const int cw = s - 2;
-            if (cw >= 0 && cw < nst && cw % PC_P == p) {
-                PcUpSlot& B = S[cw % PC_R];
-                if (lane < PC_C) {
-                    B.rec[lane] = rc;
-                    B.wh[lane] = xh;
-                }
-                B.lo[lane >> 2][lane & 3] = xo * xw;
-#pragma unroll
-                for (int k = 0; k < PC_C; k++) {
-                    B.cost[k][lane] = xc[k];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) B.lm[k][j][lane] = xm[k][j] * rdlane_f64(xw, 4 * k + j);
-                }
-                rc = rn;   // the records of this producer's next chunk (cw + PC_P)
-            }
-            // issue the loads of chunk s (its records were loaded a producer cycle earlier)
-            if (s < nst && s % PC_P == p) {
-                if (s + PC_P < nst && lane < PC_C) rn = R[(s + PC_P) * PC_C + lane];
-#pragma unroll
-                for (int k = 0; k < PC_C; k++) {
-                    const int x = __builtin_amdgcn_readlane(rc.x, k), meta = __builtin_amdgcn_readlane(rc.y, k);
-                    const int nc = meta & 7, hv = ((meta >> 3) & 7) - 1;
-                    xc[k] = 0.0f;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) xm[k][j] = 0.0;
-                    if (s * PC_C + k >= len) continue;
-                    if (dok) xc[k] = a.vm[(size_t)x * P + d];
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        if (j < nc && j != hv && dok) xm[k][j] = a.val[(size_t)nl_child(x, meta, j, a.W) * P + d];
-                }
-                // lane t: child position t % 4 of node t / 4 (weights of every child; the ones sum
-                // of the light ones)
-                const int kt = lane >> 2, jt = lane & 3;
-                const int xk = __shfl(rc.x, kt), mk = __shfl(rc.y, kt), wk = __shfl(rc.z, kt);
-                const int nck = mk & 7, hvk = ((mk >> 3) & 7) - 1;
-                const bool here = s * PC_C + kt < len && jt < nck;
-                xw = here ? table[(wk >> (8 * jt)) & 255] : 0.0;
-                xo = (here && jt != hvk) ? a.oup[nl_child(xk, mk, jt, a.W)] : 0.0;
-                xh = 0.0;
-                if (lane < PC_C && s * PC_C + lane < len) {
-                    const int hvl = ((rc.y >> 3) & 7) - 1;
-                    if (hvl >= 0) xh = table[(rc.z >> (8 * hvl)) & 255];
-                }
+                for (int k = 0; k < PC_C; k++) node(B, k);
+            } else {
+                for (int k = 0; k < len - c * PC_C; k++) node(B, k);
             }
         }
         __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(64 * (1 + PC_P), 1) void k_nl_down_pc(const NlArgs a, const int4* __restrict__ rec,
+template <int PP, int HF>
+__device__ __forceinline__ void nl_down_producer(PcDnSlot* S, const NlArgs& a, const double* __restrict__ table, const PcCtx& q, int P) {
+    constexpr int K0 = HF * PC_H;
+    const int lane = q.lane, d = q.d, len = q.len, nst = q.nst;
+    const bool dok = q.dok;
+    int step = 0;
+    for (; step < PP; step++) __syncthreads();
+    // chunk c holds path positions len - 1 - c PC_C - k, k = 0 .. PC_C - 1 (top -> bottom)
+    int4 rc = make_int4(0, 0, 0, 0);
+    if (PP < nst && lane < PC_C) rc = q.R[len - 1 - PP * PC_C - lane];
+    for (int c = PP; c < nst; c += PC_P) {
+        double xu[PC_H];
+#pragma unroll
+        for (int kk = 0; kk < PC_H; kk++) {
+            const int k = K0 + kk;
+            const int x = __builtin_amdgcn_readlane(rc.x, k);
+            xu[kk] = 0.0;
+            if (c * PC_C + k >= len || (SM_NL_PC_PROBE & 1)) continue;
+            if (dok) xu[kk] = a.val[(size_t)x * P + d];
+        }
+        double xo = 0.0, xw = 0.0;   // lane k in [K0, K0 + PC_H): node k's ones up sum and own weight (0: root)
+        if (lane >= K0 && lane < K0 + PC_H && c * PC_C + lane < len) {
+            xo = a.oup[rc.x];
+            xw = rc.w == rc.x ? 0.0 : table[(rc.y >> 16) & 255];
+        }
+        int4 rn = make_int4(0, 0, 0, 0);
+        if (c + PC_P < nst && lane < PC_C) rn = q.R[len - 1 - (c + PC_P) * PC_C - lane];
+        for (int i = 0; i < PC_P - 1; i++) __syncthreads();
+        PcDnSlot& B = S[c % PC_R];
+        if (lane >= K0 && lane < K0 + PC_H) {
+            B.rec[lane] = rc;
+            B.uo[lane] = xo;
+            B.w[lane] = xw;
+        }
+#pragma unroll
+        for (int kk = 0; kk < PC_H; kk++) B.up[K0 + kk][lane] = xu[kk];
+        __syncthreads();
+        step += PC_P;
+        rc = rn;
+    }
+    for (; step < nst + PC_P; step++) __syncthreads();
+}
+
+__global__ __launch_bounds__(64 * PC_WAVES, 1) void k_nl_down_pc(const NlArgs a, const int4* __restrict__ rec,
                                                                     const double* __restrict__ table, int lo, int nunits, int P) {
     extern __shared__ __align__(16) unsigned char pc_smem[];
     PcDnSlot* S = (PcDnSlot*)pc_smem;
@@ -484,90 +604,58 @@ __global__ __launch_bounds__(64 * (1 + PC_P), 1) void k_nl_down_pc(const NlArgs 
     const int u = blockIdx.x;
     if (u >= nunits) return;
     const int ci = a.order_down[lo + u / nchunks];
-    const int d = (u % nchunks) * 64 + lane;
-    const bool dok = d < P;
-    const int4* __restrict__ R = rec + a.chain_start[ci];
-    const int len = a.chain_len[ci];
-    const int nst = (len + PC_C - 1) / PC_C;
+    PcCtx q;
+    q.lane = lane;
+    q.d = (u % nchunks) * 64 + lane;
+    q.dok = q.d < P;
+    q.R = rec + a.chain_start[ci];
+    q.len = a.chain_len[ci];
+    q.nst = (q.len + PC_C - 1) / PC_C;
+    if (wv > 0) {
+        pc_dispatch<0>(wv - 1, [&](auto pp, auto hf) { nl_down_producer<decltype(pp)::value, decltype(hf)::value>(S, a, table, q, P); });
+        return;
+    }
+    __builtin_amdgcn_s_setprio(3);
+    const int len = q.len;
+    const __amdgpu_buffer_rsrc_t val_r = buf_rsrc(a.val), vm_r = buf_rsrc(a.vm), ofin_r = buf_rsrc(a.ofin);
+    const uint32_t dof8 = q.dok ? (uint32_t)q.d * 8u : 0x80000000u, dof4 = q.dok ? (uint32_t)q.d * 4u : 0x80000000u;
     double carry = 0.0, carry_o = 0.0;
-    if (wv == 0) {
+    {
         // the top's parent is on a path finished in an earlier round (or the top is the root)
-        const int4 top = R[len - 1];
+        const int4 top = q.R[len - 1];
         if (top.w != top.x) {
-            carry = dok ? a.val[(size_t)top.w * P + d] : 0.0;
+            carry = q.dok ? a.val[(size_t)top.w * P + q.d] : 0.0;
             carry_o = a.ofin[top.w];
         }
     }
-    int4 rc = make_int4(0, 0, 0, 0), rn = make_int4(0, 0, 0, 0);
-    double xu[PC_C];
-    double xo = 0.0, xw = 0.0;   // lane t < PC_C: node t's ones up sum and own weight
-    const int p = wv - 1;
-    // chunk c holds path positions len - 1 - c PC_C - k, k = 0 .. PC_C - 1 (top -> bottom)
-    if (wv > 0 && p < nst && lane < PC_C) rc = R[len - 1 - p * PC_C - lane];
-    for (int s = 0; s < nst + 3; s++) {
-        if (wv == 0) {
-            const int c = s - 3;
-            if (c >= 0) {
-                const PcDnSlot& B = S[c % PC_R];
+    auto node = [&](const PcDnSlot& B, int k) {
+        const int x = __builtin_amdgcn_readfirstlane(B.rec[k].x);
+        const double up = B.up[k][lane], uo = B.uo[k], w = B.w[k];
+        // (the root has w = 0: fin = 0 (carry - 0 up) + up = up, exactly)
+        const double fin = w * (carry - w * up) + up;
+        const double fo = w * (carry_o - w * uo) + uo;
+        float out = (float)fin / (float)fo;
+        if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
+            float sum = 0.f;
+            sum += a.scale * out;
+            out = sum;
+        }
+        const uint32_t row = (uint32_t)x * (uint32_t)P;
+        if (!(SM_NL_PC_PROBE & 2)) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fin), val_r, dof8, row * 8u, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), vm_r, dof4, row * 4u, 0);
+        if (lane == 0 && q.d == 0) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fo), ofin_r, 0, (uint32_t)x * 8u, 0);
+        carry = fin;
+        carry_o = fo;
+    };
+    for (int s = 0; s < q.nst + PC_P; s++) {
+        const int c = s - PC_P;
+        if (c >= 0) {
+            const PcDnSlot& B = S[c % PC_R];
+            if ((c + 1) * PC_C <= len) {
 #pragma unroll
-                for (int k = 0; k < PC_C; k++) {
-                    const bool ok = c * PC_C + k < len;
-                    const int4 r = B.rec[k];
-                    const int x = __builtin_amdgcn_readfirstlane(r.x), par = __builtin_amdgcn_readfirstlane(r.w);
-                    const double up = B.up[k][lane], uo = B.uo[k], w = B.w[k];
-                    const double m = w * up;
-                    const double q = carry - m;
-                    const double sv = w * q;
-                    const double mo = w * uo;
-                    const double qo = carry_o - mo;
-                    const double so = w * qo;
-                    const double fin = par == x ? up : sv + up;   // the root keeps its up sum
-                    const double fo = par == x ? uo : so + uo;
-                    float out = (float)fin / (float)fo;
-                    if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
-                        float sum = 0.f;
-                        sum += a.scale * out;
-                        out = sum;
-                    }
-                    if (ok) {
-                        if (d == 0) a.ofin[x] = fo;
-                        if (dok) {
-                            a.val[(size_t)x * P + d] = fin;
-                            a.vm[(size_t)x * P + d] = out;
-                        }
-                        carry = fin;
-                        carry_o = fo;
-                    }
-                }
-            }
-        } else {
-            const int cw = s - 2;
-            if (cw >= 0 && cw < nst && cw % PC_P == p) {
-                PcDnSlot& B = S[cw % PC_R];
-                if (lane < PC_C) {
-                    B.rec[lane] = rc;
-                    B.uo[lane] = xo;
-                    B.w[lane] = xw;
-                }
-#pragma unroll
-                for (int k = 0; k < PC_C; k++) B.up[k][lane] = xu[k];
-                rc = rn;
-            }
-            if (s < nst && s % PC_P == p) {
-                if (s + PC_P < nst && lane < PC_C) rn = R[len - 1 - (s + PC_P) * PC_C - lane];
-#pragma unroll
-                for (int k = 0; k < PC_C; k++) {
-                    const int x = __builtin_amdgcn_readlane(rc.x, k);
-                    xu[k] = 0.0;
-                    if (s * PC_C + k >= len) continue;
-                    if (dok) xu[k] = a.val[(size_t)x * P + d];
-                }
-                xo = 0.0;
-                xw = 0.0;
-                if (lane < PC_C && s * PC_C + lane < len) {
-                    xo = a.oup[rc.x];
-                    xw = table[(rc.y >> 16) & 255];
-                }
+                for (int k = 0; k < PC_C; k++) node(B, k);
+            } else {
+                for (int k = 0; k < len - c * PC_C; k++) node(B, k);
             }
         }
         __syncthreads();
@@ -586,7 +674,9 @@ void launch_nl_edges(const uint8_t* bgr, size_t pair_stride, uint8_t* med, uint8
 void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_t st) {
     if (hi <= lo) return;
     const int nchunks = (P + 63) / 64, nunits = (hi - lo) * nchunks;
-    if (nunits < SM_NL_PC_UNITS) {
+    // (the producer/consumer stores use 32-bit byte offsets into val: volumes below 4 GiB)
+    const bool small = (double)a.nodes * P * 8 < 4294967296.0;
+    if (nunits < SM_NL_PC_UNITS && small) {
         static bool attr = false;   // LDS above the 64 KiB default
         if (!attr) {
             hipFuncSetAttribute((const void*)k_nl_up_pc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_R * sizeof(PcUpSlot)));
@@ -594,9 +684,9 @@ void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_
             attr = true;
         }
         if (up)
-            hipLaunchKernelGGL(k_nl_up_pc, dim3(nunits), dim3(64 * (1 + PC_P)), PC_R * sizeof(PcUpSlot), st, a, a.rec, a.table, lo, nunits, P);
+            hipLaunchKernelGGL(k_nl_up_pc, dim3(nunits), dim3(64 * PC_WAVES), PC_R * sizeof(PcUpSlot), st, a, a.rec, a.table, lo, nunits, P);
         else
-            hipLaunchKernelGGL(k_nl_down_pc, dim3(nunits), dim3(64 * (1 + PC_P)), PC_R * sizeof(PcDnSlot), st, a, a.rec, a.table, lo, nunits, P);
+            hipLaunchKernelGGL(k_nl_down_pc, dim3(nunits), dim3(64 * PC_WAVES), PC_R * sizeof(PcDnSlot), st, a, a.rec, a.table, lo, nunits, P);
         return;
     }
     const dim3 grid((unsigned)((nunits + SM_NL_WAVES - 1) / SM_NL_WAVES)), block(64 * SM_NL_WAVES);

@@ -364,7 +364,7 @@ constexpr int PC_H = SM_NL_PC_H;
 #endif
 constexpr int PC_NH = PC_C / PC_H;
 constexpr int PC_WAVES = 1 + PC_NH * PC_P;
-static_assert(PC_WAVES <= 16 && PC_C % PC_H == 0, "a workgroup holds at most 1024 threads");
+static_assert(PC_WAVES + 2 <= 16 && PC_C % PC_H == 0, "a workgroup holds at most 1024 threads");
 
 struct PcUpSlot {
     int4 rec[PC_C];
@@ -377,6 +377,14 @@ struct PcDnSlot {
     double w[PC_C];          // the node's own weight (0 for the root: fin = 0 (carry - 0) + up = up)
     double uo[PC_C];         // the ones channel's up sum
     double up[PC_C][64];
+};
+// Down rounds: the consumer leaves each node's final sums here; PC_SW store waves divide, scale
+// and store them the step after (the division and the three stores are off the chain).
+constexpr int PC_SW = 2;
+struct PcDnOut {
+    double fin[PC_C][64];
+    double fo[PC_C];
+    int x[PC_C];
 };
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -592,10 +600,10 @@ __device__ __forceinline__ void nl_down_producer(PcDnSlot* S, const NlArgs& a, c
         step += PC_P;
         rc = rn;
     }
-    for (; step < nst + PC_P; step++) __syncthreads();
+    for (; step < nst + PC_P + 1; step++) __syncthreads();   // (+1: the store waves' last step)
 }
 
-__global__ __launch_bounds__(64 * PC_WAVES, 1) void k_nl_down_pc(const NlArgs a, const int4* __restrict__ rec,
+__global__ __launch_bounds__(64 * (PC_WAVES + PC_SW), 1) void k_nl_down_pc(const NlArgs a, const int4* __restrict__ rec,
                                                                     const double* __restrict__ table, int lo, int nunits, int P) {
     extern __shared__ __align__(16) unsigned char pc_smem[];
     PcDnSlot* S = (PcDnSlot*)pc_smem;
@@ -611,14 +619,45 @@ __global__ __launch_bounds__(64 * PC_WAVES, 1) void k_nl_down_pc(const NlArgs a,
     q.R = rec + a.chain_start[ci];
     q.len = a.chain_len[ci];
     q.nst = (q.len + PC_C - 1) / PC_C;
+    PcDnOut* O = (PcDnOut*)(pc_smem + PC_R * sizeof(PcDnSlot));
+    const int len = q.len;
+    if (wv >= PC_WAVES) {
+        // store wave: nodes [sw PC_C / PC_SW, (sw + 1) PC_C / PC_SW) of the chunk consumed last step
+        constexpr int NPW = PC_C / PC_SW;
+        const int k0 = (wv - PC_WAVES) * NPW;
+        const __amdgpu_buffer_rsrc_t val_r = buf_rsrc(a.val), vm_r = buf_rsrc(a.vm), ofin_r = buf_rsrc(a.ofin);
+        const uint32_t dof8 = q.dok ? (uint32_t)q.d * 8u : 0x80000000u, dof4 = q.dok ? (uint32_t)q.d * 4u : 0x80000000u;
+        for (int s = 0; s < q.nst + PC_P + 1; s++) {
+            const int cc = s - PC_P - 1;
+            if (cc >= 0) {
+                const PcDnOut& B = O[cc % 2];
+#pragma unroll
+                for (int kk = 0; kk < NPW; kk++) {
+                    const int k = k0 + kk;
+                    if (cc * PC_C + k >= len) break;
+                    const double fin = B.fin[k][lane], fo = B.fo[k];
+                    const int x = __builtin_amdgcn_readfirstlane(B.x[k]);
+                    float out = (float)fin / (float)fo;
+                    if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
+                        float sum = 0.f;
+                        sum += a.scale * out;
+                        out = sum;
+                    }
+                    const uint32_t row = (uint32_t)x * (uint32_t)P;
+                    if (!(SM_NL_PC_PROBE & 2)) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fin), val_r, dof8, row * 8u, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), vm_r, dof4, row * 4u, 0);
+                    if (lane == 0 && q.d == 0) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fo), ofin_r, 0, (uint32_t)x * 8u, 0);
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
     if (wv > 0) {
         pc_dispatch<0>(wv - 1, [&](auto pp, auto hf) { nl_down_producer<decltype(pp)::value, decltype(hf)::value>(S, a, table, q, P); });
         return;
     }
     __builtin_amdgcn_s_setprio(3);
-    const int len = q.len;
-    const __amdgpu_buffer_rsrc_t val_r = buf_rsrc(a.val), vm_r = buf_rsrc(a.vm), ofin_r = buf_rsrc(a.ofin);
-    const uint32_t dof8 = q.dok ? (uint32_t)q.d * 8u : 0x80000000u, dof4 = q.dok ? (uint32_t)q.d * 4u : 0x80000000u;
     double carry = 0.0, carry_o = 0.0;
     {
         // the top's parent is on a path finished in an earlier round (or the top is the root)
@@ -628,34 +667,29 @@ __global__ __launch_bounds__(64 * PC_WAVES, 1) void k_nl_down_pc(const NlArgs a,
             carry_o = a.ofin[top.w];
         }
     }
-    auto node = [&](const PcDnSlot& B, int k) {
-        const int x = __builtin_amdgcn_readfirstlane(B.rec[k].x);
+    auto node = [&](const PcDnSlot& B, PcDnOut& OB, int k) {
         const double up = B.up[k][lane], uo = B.uo[k], w = B.w[k];
         // (the root has w = 0: fin = 0 (carry - 0 up) + up = up, exactly)
         const double fin = w * (carry - w * up) + up;
         const double fo = w * (carry_o - w * uo) + uo;
-        float out = (float)fin / (float)fo;
-        if (a.solve_all) {   // SolveAll fused (sm_run): its `sum = 0; sum += w * v`
-            float sum = 0.f;
-            sum += a.scale * out;
-            out = sum;
+        OB.fin[k][lane] = fin;
+        if (lane == 0) {
+            OB.fo[k] = fo;
+            OB.x[k] = B.rec[k].x;
         }
-        const uint32_t row = (uint32_t)x * (uint32_t)P;
-        if (!(SM_NL_PC_PROBE & 2)) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fin), val_r, dof8, row * 8u, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), vm_r, dof4, row * 4u, 0);
-        if (lane == 0 && q.d == 0) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fo), ofin_r, 0, (uint32_t)x * 8u, 0);
         carry = fin;
         carry_o = fo;
     };
-    for (int s = 0; s < q.nst + PC_P; s++) {
+    for (int s = 0; s < q.nst + PC_P + 1; s++) {
         const int c = s - PC_P;
-        if (c >= 0) {
+        if (c >= 0 && c < q.nst) {
             const PcDnSlot& B = S[c % PC_R];
+            PcDnOut& OB = O[c % 2];
             if ((c + 1) * PC_C <= len) {
 #pragma unroll
-                for (int k = 0; k < PC_C; k++) node(B, k);
+                for (int k = 0; k < PC_C; k++) node(B, OB, k);
             } else {
-                for (int k = 0; k < len - c * PC_C; k++) node(B, k);
+                for (int k = 0; k < len - c * PC_C; k++) node(B, OB, k);
             }
         }
         __syncthreads();
@@ -680,13 +714,13 @@ void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_
         static bool attr = false;   // LDS above the 64 KiB default
         if (!attr) {
             hipFuncSetAttribute((const void*)k_nl_up_pc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_R * sizeof(PcUpSlot)));
-            hipFuncSetAttribute((const void*)k_nl_down_pc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_R * sizeof(PcDnSlot)));
+            hipFuncSetAttribute((const void*)k_nl_down_pc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(PC_R * sizeof(PcDnSlot) + 2 * sizeof(PcDnOut)));
             attr = true;
         }
         if (up)
             hipLaunchKernelGGL(k_nl_up_pc, dim3(nunits), dim3(64 * PC_WAVES), PC_R * sizeof(PcUpSlot), st, a, a.rec, a.table, lo, nunits, P);
         else
-            hipLaunchKernelGGL(k_nl_down_pc, dim3(nunits), dim3(64 * PC_WAVES), PC_R * sizeof(PcDnSlot), st, a, a.rec, a.table, lo, nunits, P);
+            hipLaunchKernelGGL(k_nl_down_pc, dim3(nunits), dim3(64 * (PC_WAVES + PC_SW)), PC_R * sizeof(PcDnSlot) + 2 * sizeof(PcDnOut), st, a, a.rec, a.table, lo, nunits, P);
         return;
     }
     const dim3 grid((unsigned)((nunits + SM_NL_WAVES - 1) / SM_NL_WAVES)), block(64 * SM_NL_WAVES);

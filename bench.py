@@ -297,20 +297,30 @@ def main():
                              f"{t_cpu:.1f} s; GPU maps checked bit-exact against it", "host": host}
         else:
             # a whole pair would take minutes and tens of GB on one core: time the restatement on
-            # the first rows of pair 0 (full width, full D; its cost is linear in H*W*D) and report
-            # that rate.  Timing only: a crop's CBCA/SGM columns end early, so no map comparison
-            # (parity at this size: tests/test_gpu_fullres.py; the oracle itself: every smaller size).
+            # the first rows of pair 0 as an image of their own (full width, full D; its cost is
+            # linear in H*W*D) and report that rate (parity at the full size: the fixture check
+            # above and tests/test_gpu_large_fixtures.py).
             hc = max(8, min(H, CPU_FULL_PAIR_MAX // (W * D)))
             pair = {k: np.ascontiguousarray(batch[k][0][:hc]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
             cfg = O.config(hc, W, md, sgm_paths=paths, do_refine=int(args.refine), optimization=2 if args.opt == "so" else 1,
                            aggregation={"CBCA": 1, "GF": 2, "NL": 3}[args.agg])
             t = time.perf_counter()
-            O.run_ex(pair, cfg)
+            r = O.run_ex(pair, cfg)
             t_cpu = time.perf_counter() - t
+            # the crop is an image of its own: the GPU runs it too (outside the timed region) and
+            # its map must equal the restatement's
+            sbc = StereoBatch(md, hc, W, 1, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt,
+                              aggregation=args.agg, fuse_norm_scan={"auto": -1, "on": 1, "off": 0}[args.fuse_norm_scan])
+            sbc.upload(pair["lbgr"][None], pair["rbgr"][None], pair["lgray"][None], pair["rgray"][None])
+            crop_ok = bool(np.array_equal(sbc.run(0.3)[0], r["disp"]))
+            del sbc
+            if not crop_ok:
+                raise SystemExit(f"bench: GPU disparity of the {W}x{hc} crop differs from the CPU restatement")
             cpu = {"value": round(hc * W * D / t_cpu / 1e6, 3), "unit": "Mdisp/s", "cores": 1, "kind": "port",
-                   "sample": f"rows 0-{hc - 1} of bench pair 0 ({W}x{hc} D={D}, {hc * W * D / 1e6:.0f} M disparities) "
-                             f"through oracle/sm_oracle.c, 1 thread, {t_cpu:.1f} s; rate extrapolated linearly "
-                             f"to the {W}x{H} pairs; timing only (no map comparison on a crop)", "host": host}
+                   "sample": f"rows 0-{hc - 1} of bench pair 0 as a {W}x{hc} image (D={D}, {hc * W * D / 1e6:.0f} M "
+                             f"disparities) through oracle/sm_oracle.c, 1 thread, {t_cpu:.1f} s; rate extrapolated "
+                             f"linearly to the {W}x{H} pairs; the GPU's map of the same crop checked bit-exact against it",
+                   "host": host}
 
     if rank == 0:
         out = {

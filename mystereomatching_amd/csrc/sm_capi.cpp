@@ -563,11 +563,6 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     int* rec_d = c->nl_rec + ((size_t)set * (slot + 2 * sm::NL_REC_PAD) + sm::NL_REC_PAD) * 4;
     constexpr int NOFF = 2 * (sm::NL_LEVELS + 1) + 1;
     sm_status s;
-    static const bool serial_front = getenv("SM_NL_SERIAL_FRONT") != nullptr;   // diagnostics: no overlap
-    if (serial_front) {
-        HIP_TRY(c, hipEventRecord(c->nl_ev_set[set ^ 1], c->st));
-        HIP_TRY(c, hipStreamWaitEvent(c->nl_st, c->nl_ev_set[set ^ 1], 0));
-    }
     {
         struct Swap {   // the front's launches (and their profiling events) go to nl_st
             sm_ctx* c;

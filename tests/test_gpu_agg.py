@@ -57,6 +57,20 @@ def test_aggregated_volume_bits(oracle, agg, H, W, md, idx):
     np.testing.assert_array_equal(bits(got), bits(want))
 
 
+@pytest.mark.parametrize("H,W,md,idx", [(3, 3, 4, 560), (3, 90, 15, 561), (90, 3, 15, 562), (4, 257, 63, 563),
+                                        (130, 5, 70, 564)])
+def test_nl_thin_images(oracle, H, W, md, idx):
+    """NL on the thinnest images ctmf allows (3 rows or columns) and long single paths: the GPU
+    tree walk (Euler tour ranking, heavy-first preorder, path tables) and both filter kernels
+    (block rounds and producer / consumer rounds, partial last chunks) against the restatement."""
+    pair = S.make_pair(H, W, md + 1, idx)
+    cfg = ocfg(oracle, H, W, md)
+    vm = oracle.cost_volume(pair, cfg)
+    want = oracle.nl_aggregate(vm, pair["lbgr"], cfg)
+    got = _agg_volume(pair, H, W, md, "NL")
+    np.testing.assert_array_equal(bits(got), bits(want))
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("H,W,md,idx", [(24, 30, 7, 540), (40, 61, 63, 541), (19, 23, 255, 542), (9, 12, 20, 543),
                                         (11, 9, 64, 544), (33, 70, 130, 545)])

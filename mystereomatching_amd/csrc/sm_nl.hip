@@ -31,6 +31,15 @@
 #ifndef SM_NL_PIPE
 #define SM_NL_PIPE 1    // issue the next block's loads before this block's arithmetic (tuning)
 #endif
+#ifndef SM_NL_BLOCK_SHORT
+#define SM_NL_BLOCK_SHORT 2      // ... in rounds of at least SM_NL_SHORT_UNITS (path, chunk) units
+#endif
+#ifndef SM_NL_SHORT_UNITS
+#define SM_NL_SHORT_UNITS 65536
+#endif
+#ifndef SM_NL_SHORT_UNITS_DN
+#define SM_NL_SHORT_UNITS_DN 65536
+#endif
 #ifndef SM_NL_WAVES
 #define SM_NL_WAVES 1   // waves (independent paths) per workgroup (tuning)
 #endif
@@ -725,6 +734,15 @@ void launch_nl_round(const NlArgs& a, bool up, int lo, int hi, int P, hipStream_
     }
     const dim3 grid((unsigned)((nunits + SM_NL_WAVES - 1) / SM_NL_WAVES)), block(64 * SM_NL_WAVES);
     constexpr int K = SM_NL_BLOCK;
+    // rounds of very many (short) paths: smaller blocks, fewer registers, more waves in flight
+    if (nunits >= (up ? SM_NL_SHORT_UNITS : SM_NL_SHORT_UNITS_DN)) {
+        constexpr int KS = SM_NL_BLOCK_SHORT;
+        if (up)
+            hipLaunchKernelGGL((k_nl_up<KS>), grid, block, 0, st, a, a.rec, a.table, lo, nunits, P);
+        else
+            hipLaunchKernelGGL((k_nl_down<KS>), grid, block, 0, st, a, a.rec, a.table, lo, nunits, P);
+        return;
+    }
     if (up)
         hipLaunchKernelGGL((k_nl_up<K>), grid, block, 0, st, a, a.rec, a.table, lo, nunits, P);
     else

@@ -166,6 +166,24 @@ def test_teddy_size_maps(oracle, agg):
     np.testing.assert_array_equal(got, want)
 
 
+def test_nl_teddy_batch_all_round_kernels(oracle):
+    """Two Teddy-size pairs in one batch: the first up / down rounds then hold >= 64 K (path, chunk)
+    units and run the 2-node block kernel, the middle rounds the 4-node one and the long-path
+    rounds the producer / consumer workgroups -- all three filter kernels, both maps bit-exact."""
+    H, W, md, n = 375, 450, 63, 2
+    batch = S.make_batch(n, H, W, md + 1, first_index=20)
+    sb = StereoBatch(md, H, W, n, device=0, aggregation=AGG["NL"])
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        got = sb.run(0.3)
+    finally:
+        sb.close()
+    cfg = ocfg(oracle, H, W, md, aggregation=AGG["NL"])
+    for i in range(n):
+        pair = {k: batch[k][i] for k in KEYS}
+        np.testing.assert_array_equal(got[i], oracle.run(pair, cfg)["disp"])
+
+
 @pytest.mark.parametrize("agg", ["GF", "NL"])
 @pytest.mark.parametrize("sub_batch,num_streams", [(2, 2), (1, 3), (2, 1)])
 def test_sub_batches_and_streams(oracle, agg, sub_batch, num_streams):

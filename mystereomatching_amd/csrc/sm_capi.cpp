@@ -216,6 +216,9 @@ sm_status validate(const sm_params& p, std::string& why) {
         if (!(p.nl_sigma > 0)) return bad("nl_sigma must be > 0");
         // ctmf's 3x3 median asserts width >= 3 and height >= 3 (NL/ctmf.c:211-212)
         if (p.rows < 3 || p.cols < 3) return bad("aggregation NL needs rows, cols >= 3 (ctmf median)");
+        // the GPU tree walk indexes the batch's tour arcs (4 per pixel) with 32-bit ints
+        if (4.0 * (double)p.rows * (double)p.cols * (double)(p.batch_capacity > 0 ? p.batch_capacity : 1) >= 2147483647.0)
+            return bad("aggregation NL: rows * cols * batch_capacity must stay below 2^29");
     }
     if (p.optimization < 0 || p.optimization > 2) return bad("unknown optimization");
     if (p.census_rv < 0 || p.census_ru < 0 || census_len(p) > 128) return bad("census code longer than 128 bits");

@@ -145,7 +145,8 @@ def test_run_batch_multi_argument_checks():
                                       (dict(aggregation=3, rows=2, cols=2), b"NL"), (dict(aggregation=3, rows=2), b"NL"),
                                       (dict(aggregation=3, cols=2), b"NL"), (dict(aggregation=2, gf_eps=0.0), b"gf_eps"),
                                       (dict(aggregation=2, gf_mode=2), b"gf_mode"),
-                                      (dict(aggregation=3, nl_sigma=0.0), b"nl_sigma")])
+                                      (dict(aggregation=3, nl_sigma=0.0), b"nl_sigma"),
+                                      (dict(aggregation=3, rows=8192, cols=8192, batch_capacity=8), b"2^29")])
 def test_alternative_aggregator_domain(over, msg):
     lib = _capi.load()
     p = _capi.default_params(15, 32, 32)

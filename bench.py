@@ -117,7 +117,8 @@ def parse():
                          "batch on the host; each step broadcasts the header, scatters the pairs (RCCL), runs "
                          "them and gathers the int16 maps back (mystereomatching_amd.batch.DistributedBatchRunner)")
     ap.add_argument("--agg", default="CBCA", choices=["CBCA", "GF", "NL"],
-                    help='aggregation selector (h:52): "CBCA" (default), "GF" guided filter (cpp:4492-4516, MY_GUIDE form), '
+                    help='aggregation selector (h:52): "CBCA" (default), "GF" guided filter (cpp:4492-4516, the shipped '
+                         'ximgproc::guidedFilter form; sm_params.gf_mode = 1 for MY_GUIDE), '
                          '"NL" non-local MST filter (cpp:4892-4917)')
     ap.add_argument("--opt", default="sgm", choices=["sgm", "so"],
                     help='optimization selector (h:53): "sgm" (default) or "so" scan-line DP (cpp:6272-6394)')

@@ -127,8 +127,6 @@ typedef struct sm_params {
     /* alternative aggregators */
     float gf_eps;                /* gf_eps[0] = 0.0001 (h:298; radius gf_r[0] = 9, h:297) */
     int32_t gf_mode;             /* sm_gf_mode: SM_GF_XIMGPROC (default, the shipped build) or SM_GF_MY_GUIDE */
-    int32_t sgm_2pass;           /* 1 (default): 4-path SGM with D = 64 / 128 / 256 as two 2-D wavefront passes
-                                  * (L0 + L2, then L1 + L3 + sum + WTA; identical results); 0: four path sweeps */
     double nl_sigma;             /* NLCCA sigma = 0.1 (NL/NLCCA.cpp:33): weights exp(-c / (255 sigma)) */
 } sm_params;
 
@@ -160,7 +158,9 @@ SM_API sm_status sm_pyr_down(int32_t hip_device, const uint8_t* src, int32_t row
 SM_API sm_status sm_pyr_down_f32(int32_t hip_device, const float* src, int32_t rows, int32_t cols, float* dst);
 /* refine() on DP[0] (needs do_refine = 1 at sm_create and a preceding sm_disp_optimize). */
 SM_API sm_status sm_refine(sm_ctx* ctx, int16_t* disp_out);
-SM_API sm_status sm_get_disp(sm_ctx* ctx, int32_t view, int16_t* dst);  /* DP[view], H*W int16 */
+SM_API sm_status sm_get_disp(sm_ctx* ctx, int32_t view, int16_t* dst);  /* DP[view], H*W int16; DP[1] exists
+                                                                        * with do_refine or optimization "so"
+                                                                        * (so runs on both views, cpp:1093) */
 /* Overwrite DP[view] (the reference's DP is a public member, h:2724); after sm_disp_optimize. */
 SM_API sm_status sm_set_disp(sm_ctx* ctx, int32_t view, const int16_t* src);
 SM_API sm_status sm_get_volume(sm_ctx* ctx, int32_t view, float* dst);   /* H*W*D floats */

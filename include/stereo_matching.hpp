@@ -42,6 +42,7 @@
 #include <iostream>
 #include <iterator>
 #include <memory>
+#include <new>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -136,6 +137,11 @@ class Mat {
 
 namespace detail {
 
+// Largest image imread accepts (pixels): header sizes above it, or whose products would overflow,
+// are rejected before anything is allocated (a crafted header must not wrap a buffer size).
+constexpr uint64_t kMaxImagePixels = 1ull << 28;
+inline bool size_ok(int64_t w, int64_t h) { return w >= 1 && h >= 1 && (uint64_t)w * (uint64_t)h <= kMaxImagePixels; }
+
 // Decoded 8-bit pixels: w x h, cin = 1 (gray) or 3 (R, G, B), row-major.
 struct Pixels {
     int w = 0, h = 0, cin = 0;
@@ -145,7 +151,7 @@ struct Pixels {
 inline bool read_pnm(std::ifstream& f, Pixels& out) {
     std::string magic;
     int w = 0, h = 0, maxv = 0;
-    if (!(f >> magic >> w >> h >> maxv) || (magic != "P6" && magic != "P5") || maxv != 255 || w < 1 || h < 1)
+    if (!(f >> magic >> w >> h >> maxv) || (magic != "P6" && magic != "P5") || maxv != 255 || !size_ok(w, h))
         return false;
     f.get();
     out.w = w, out.h = h, out.cin = magic == "P6" ? 3 : 1;
@@ -162,7 +168,8 @@ inline uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t
 inline bool read_png(const std::vector<uint8_t>& file, Pixels& out) {
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0d, 0x0a, 0x1a, 0x0a};
     if (file.size() < 8 || std::memcmp(file.data(), sig, 8) != 0) return false;
-    int w = 0, h = 0, depth = 0, ctype = -1, interlace = 0;
+    int64_t w = 0, h = 0;
+    int depth = 0, ctype = -1, interlace = 0;
     std::vector<uint8_t> idat, plte;
     for (size_t pos = 8; pos + 12 <= file.size();) {
         const uint32_t len = be32(&file[pos]);
@@ -170,7 +177,7 @@ inline bool read_png(const std::vector<uint8_t>& file, Pixels& out) {
         const uint8_t* type = &file[pos + 4];
         const uint8_t* data = &file[pos + 8];
         if (!std::memcmp(type, "IHDR", 4) && len >= 13) {
-            w = (int)be32(data), h = (int)be32(data + 4), depth = data[8], ctype = data[9], interlace = data[12];
+            w = be32(data), h = be32(data + 4), depth = data[8], ctype = data[9], interlace = data[12];
         } else if (!std::memcmp(type, "PLTE", 4)) {
             plte.assign(data, data + len);
         } else if (!std::memcmp(type, "IDAT", 4)) {
@@ -183,10 +190,14 @@ inline bool read_png(const std::vector<uint8_t>& file, Pixels& out) {
     // samples per pixel by colour type: 0 gray, 2 RGB, 3 palette index, 4 gray + alpha, 6 RGBA
     const int spp = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
     const bool depth_ok = depth == 8 || depth == 16 || ((ctype == 0 || ctype == 3) && (depth == 1 || depth == 2 || depth == 4));
-    if (w < 1 || h < 1 || spp == 0 || !depth_ok || interlace != 0 || (ctype == 3 && (plte.empty() || depth == 16)))
+    // (w * h <= 2^28 keeps every size below in 64-bit range: stride <= 8 w + 1)
+    if (!size_ok(w, h) || spp == 0 || !depth_ok || interlace != 0 || (ctype == 3 && (plte.empty() || depth == 16)))
         return false;
     const size_t bpp = std::max<size_t>(1, (size_t)spp * depth / 8);     // filter byte distance
     const size_t stride = ((size_t)w * spp * depth + 7) / 8;             // bytes per scanline
+    // zlib's deflate expands at most ~1032:1: an IDAT far too short for the header's size is
+    // rejected before the scanline buffer is allocated
+    if ((uint64_t)h * (stride + 1) > (uint64_t)idat.size() * 1100 + 4096) return false;
     std::vector<uint8_t> raw(h * (stride + 1));
     uLongf rlen = (uLongf)raw.size();
     if (uncompress(raw.data(), &rlen, idat.data(), (uLong)idat.size()) != Z_OK || rlen != raw.size()) return false;
@@ -215,7 +226,7 @@ inline bool read_png(const std::vector<uint8_t>& file, Pixels& out) {
             cur[i] = (uint8_t)x;
         }
     }
-    out.w = w, out.h = h, out.cin = (ctype == 0 || ctype == 4) ? 1 : 3;
+    out.w = (int)w, out.h = (int)h, out.cin = (ctype == 0 || ctype == 4) ? 1 : 3;
     out.px.assign((size_t)w * h * out.cin, 0);
     for (int y = 0; y < h; y++) {
         const uint8_t* row = &img[(size_t)y * stride];
@@ -247,12 +258,7 @@ inline bool read_png(const std::vector<uint8_t>& file, Pixels& out) {
 }
 #endif
 
-}  // namespace detail
-
-// cv::imread for PNG (when zlib is available) and binary PNM (P6 RGB / P5 gray, maxval 255).
-// flags 1: 3-channel BGR; flags 0: gray ((R*9798 + G*19235 + B*3735 + 16384) >> 15, libpng's
-// rgb_to_gray).  Empty Mat on failure (main_.cpp:108 tests empty()).
-inline Mat imread(const std::string& path, int flags = 1) {
+inline Mat imread_impl(const std::string& path, int flags) {
     std::ifstream f(path, std::ios::binary);
     if (!f) return Mat();
     detail::Pixels d;
@@ -278,6 +284,20 @@ inline Mat imread(const std::string& path, int flags = 1) {
         }
     }
     return m;
+}
+}  // namespace detail
+
+// cv::imread for PNG (when zlib is available) and binary PNM (P6 RGB / P5 gray, maxval 255).
+// flags 1: 3-channel BGR; flags 0: gray ((R*9798 + G*19235 + B*3735 + 16384) >> 15, libpng's
+// rgb_to_gray).  Empty Mat on failure (main_.cpp:108 tests empty()).
+inline Mat imread(const std::string& path, int flags = 1) {
+    try {
+        return detail::imread_impl(path, flags);
+    } catch (const std::bad_alloc&) {   // an image too large for this host: empty Mat, as documented
+        return Mat();
+    } catch (const std::length_error&) {
+        return Mat();
+    }
 }
 
 // cv::pyrDown (main_.cpp:145-154) on the GPU: u8 with 1 or 3 channels (the inputs, masks) or
@@ -366,10 +386,10 @@ class StereoMatching {
     StereoMatching& operator=(const StereoMatching&) = delete;
 
     void costCalculate() { check(sm_cost_calculate(ctx_), "costCalculate"); }
-    void dispOptimize() {  // DP[0] (and DP[1] when Do_refine), cpp:1046-1136
+    void dispOptimize() {  // DP[0] (and DP[1] when Do_refine, or with "so": cpp:1093), cpp:1046-1136
         DP[0].create(h_, w_, CV_16S);
         check(sm_disp_optimize(ctx_, DP[0].ptr<int16_t>()), "dispOptimize");
-        if (refine_on_) {
+        if (refine_on_ || (optimization == "so" && Do_LRConsis)) {
             DP[1].create(h_, w_, CV_16S);
             check(sm_get_disp(ctx_, 1, DP[1].ptr<int16_t>()), "DP[1]");
         }

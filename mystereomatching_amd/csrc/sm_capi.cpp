@@ -54,8 +54,6 @@ struct sm_ctx {
     float* vm0 = nullptr;       // [cap][npix][D]
     float* vm1 = nullptr;       // [cap][npix][D] (right view, optional)
     float* acc = nullptr;       // [cap][npix][D]
-    float* l2v = nullptr;       // [cap][npix][D] SGM path 2 (two-pass SGM, sm_sgm2.hip)
-    uint32_t* sgm2_sync = nullptr;  // two-pass SGM: ticket, abort flag, per-strip progress
     int16_t* disp = nullptr;    // [cap][npix] DP[0]
     int16_t* disp1 = nullptr;   // [cap][npix] DP[1] (do_refine)
     int16_t* disp_tmp = nullptr;// [cap][npix] refine ping-pong (do_refine)
@@ -183,8 +181,14 @@ bool needs_census(const sm_params& p) { return p.cost_method != SM_COST_AD; }
 bool needs_arms(const sm_params& p) {
     return p.cost_method == SM_COST_CENSUS_GRAD || p.aggregation == SM_AGG_CBCA || p.do_refine;  // + regionVote (cpp:1393-1396)
 }
-bool right_view(const sm_params& p) { return p.compute_right_view || p.do_refine; }
+// "so" runs on both views (num = Do_LRConsis ? 2 : 1, cpp:1093, Do_LRConsis = 1, h:72), so DP[1]
+// = so(vm[1]) needs the right cost volume even without Do_refine
+bool right_view(const sm_params& p) { return p.compute_right_view || p.do_refine || p.optimization == SM_OPT_SO; }
 int n_views(const sm_params& p) { return p.do_refine ? 2 : 1; }   // imgNum = Do_refine && Do_LRConsis ? 2 : 1
+// views dispOptimize runs on: sgm / WTA num = Do_refine && Do_LRConsis ? 2 : 1 (cpp:1054, 1110);
+// so num = Do_LRConsis ? 2 : 1 (cpp:1093) -- on vm[1] as costCalculate left it (CBCA and
+// SolveAll touch vm[1] only with Do_refine, cpp:5592, 2178)
+int opt_views(const sm_params& p) { return p.optimization == SM_OPT_SO ? 2 : n_views(p); }
 
 int cbca_lag(const sm_params& p) { return p.arm_l_out > p.arm_min_l ? p.arm_l_out : p.arm_min_l; }
 
@@ -226,7 +230,6 @@ sm_status validate(const sm_params& p, std::string& why) {
         return bad("arm lengths must be in [0, 84]");
     if (p.cbca_iterations < 0 || p.cbca_iterations > 64) return bad("cbca_iterations must be in [0, 64]");
     if (p.sgm_paths < 1 || p.sgm_paths > 8) return bad("sgm_paths must be in [1, 8]");
-    if (p.sgm_2pass < 0 || p.sgm_2pass > 1) return bad("sgm_2pass must be 0 or 1");
     if (p.sgm_redu_coeff == 0) return bad("sgm_redu_coeff must be non-zero");
     if (p.batch_capacity < 1) return bad("batch_capacity must be >= 1");
     if (p.sub_batch < 0 || p.num_streams < 0 || p.num_streams > 4) return bad("sub_batch >= 0 and num_streams in [0, 4] required");
@@ -281,7 +284,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 void free_all(sm_ctx* c) {
     void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
-                    c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->l2v, c->sgm2_sync, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
+                    c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
                     c->nl_table, c->nl_val, c->nl_oup, c->nl_ofin, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->nl_walk,
                     c->nl_offs, c->luts};
     for (void* q : ptrs)
@@ -643,35 +646,7 @@ sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
     float* vm = view == 0 ? B.vm0 : B.vm1;
     int16_t* disp = view == 0 ? B.disp : B.disp1;
     const char* sfx = view == 0 ? "" : "_r";
-    if (p.optimization == SM_OPT_SGM && c->l2v) {
-        // two 2-D wavefront passes (sm_sgm2.hip): L0 and L2, then L1 and L3 with the path sum and WTA
-        sm::Sgm2Args a{};
-        a.vm = vm;
-        a.acc = B.acc;
-        a.l2v = c->l2v + (size_t)(B.vm0 - c->vm0);
-        a.disp = disp;
-        a.flags = view == 0 ? B.flags : B.flags1;
-        a.sync = c->sgm2_sync;
-        a.H = p.rows;
-        a.W = p.cols;
-        a.D = p.num_disparities;
-        a.n = n;
-        a.p1 = p.sgm_p1;
-        a.p2 = p.sgm_p2;
-        a.redu = p.sgm_redu_coeff;
-        a.keep_final = p.keep_final_volume;
-        a.signed_costs = p.aggregation == SM_AGG_GF;
-        hipError_t e = hipSuccess;
-        sm_status s = timed(c, (std::string("sgm2_pass_a") + sfx).c_str(), (double)n * c->nvol * 12.0,
-                            [&] { e = sm::launch_sgm2_pass(a, false, c->st); });
-        if (s) return s;
-        if (e != hipSuccess) return hip_fail(c, e, "sgm2 pass A");
-        s = timed(c, (std::string("sgm2_pass_b_wta") + sfx).c_str(),
-                  (double)n * c->nvol * (12.0 + (p.keep_final_volume ? 4.0 : 0)) + (double)n * c->npix * 2,
-                  [&] { e = sm::launch_sgm2_pass(a, true, c->st); });
-        if (s) return s;
-        if (e != hipSuccess) return hip_fail(c, e, "sgm2 pass B");
-    } else if (p.optimization == SM_OPT_SGM) {
+    if (p.optimization == SM_OPT_SGM) {
         static const int RV[8] = {+1, -1, 0, 0, +1, +1, -1, -1};  // cpp:6207
         static const int RU[8] = {0, 0, +1, -1, -1, +1, +1, -1};  // cpp:6208
         static const char* NAMES[8] = {"sgm_path0", "sgm_path1", "sgm_path2", "sgm_path3",
@@ -786,17 +761,6 @@ sm_status upload(sm_ctx* c, int n, const uint8_t* lbgr, const uint8_t* rbgr, siz
     return SM_OK;
 }
 
-// The two-pass SGM's bounded waits raise a device flag instead of hanging (sm_sgm2.hip); read
-// after the stream has drained, reported once, then cleared.
-sm_status sgm2_abort_check(sm_ctx* c) {
-    if (!c->sgm2_sync) return SM_OK;
-    uint32_t ab = 0;
-    HIP_TRY(c, hipMemcpy(&ab, c->sgm2_sync + 1, 4, hipMemcpyDeviceToHost));
-    if (!ab) return SM_OK;
-    HIP_TRY(c, hipMemset(c->sgm2_sync + 1, 0, 4));
-    return fail(c, SM_EHIP, "two-pass SGM: a strip waited too long for its predecessor (maps of this run are invalid)");
-}
-
 sm_status check(sm_ctx* c) {
     if (!c) return SM_EINVAL;
     hipError_t e = hipSetDevice(c->device);
@@ -857,7 +821,6 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->fuse_norm_scan = -1;   // auto: fused for volumes >= 256 MiB per pair
     p->gf_eps = 0.0001f;        // gf_eps[0] = 1e-4 (h:298; guidedFilter / guideFilterCore_matlab, cpp:4509-4513)
     p->gf_mode = SM_GF_XIMGPROC;  // `//#define MY_GUIDE` (h:38): the shipped build calls ximgproc::guidedFilter
-    p->sgm_2pass = 0;             // (until measured on the GPU)
     p->nl_sigma = 0.1;          // NLCCA::aggreCV (NL/NLCCA.cpp:33)
 }
 
@@ -917,11 +880,6 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->vm1, cap * c->nvol + vpad))) return s;
     if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
         if ((s = dalloc(c, &c->acc, cap * c->nvol + vpad))) return s;
-    if (p->optimization == SM_OPT_SGM && p->sgm_2pass && sm::sgm2_supported(p->num_disparities, p->sgm_paths, p->cols)) {
-        if ((s = dalloc(c, &c->l2v, cap * c->nvol + vpad))) return s;
-        if ((s = dalloc(c, &c->sgm2_sync, sm::sgm2_sync_words(p->rows, (int)cap)))) return s;
-        HIP_TRY(c, hipMemset(c->sgm2_sync, 0, sm::sgm2_sync_words(p->rows, (int)cap) * 4));
-    }
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
     if ((s = dalloc(c, &c->dummy, 64))) return s;
     if ((s = dalloc(c, &c->flags, cap * c->npix))) return s;
@@ -929,9 +887,10 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->so_trace, cap * c->nvol))) return s;
         if ((s = dalloc(c, &c->so_cidx, cap * c->npix))) return s;
     }
+    if (p->do_refine || p->optimization == SM_OPT_SO)
+        if ((s = dalloc(c, &c->disp1, cap * c->npix))) return s;
     if (p->do_refine) {
         if ((s = dalloc(c, &c->flags1, cap * c->npix))) return s;
-        if ((s = dalloc(c, &c->disp1, cap * c->npix))) return s;
         if ((s = dalloc(c, &c->disp_tmp, cap * c->npix))) return s;
     }
     if ((s = dalloc(c, &c->px, 3 * cap * 2 * c->npix))) return s;
@@ -1164,7 +1123,7 @@ sm_status sm_disp_optimize(sm_ctx* c, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
     if (c->stage < 2 || c->stage > 3) return fail(c, SM_ESTATE, "sm_disp_optimize must follow sm_cost_calculate / sm_solve_all");
-    for (int v = 0; v < n_views(c->p); v++)   // num = Do_refine && Do_LRConsis ? 2 : 1 (cpp:1054, 1110)
+    for (int v = 0; v < opt_views(c->p); v++)   // num (cpp:1054, 1093, 1110)
         if ((s = run_optimize(c, c->n_loaded, v, at(c, 0)))) return s;
     c->stage = 4;
     if (disp_out) return sm_download_disp(c, 1, disp_out);
@@ -1188,10 +1147,10 @@ sm_status sm_get_disp(sm_ctx* c, int32_t view, int16_t* dst) {
     if (!dst || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
     if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
     const int16_t* src = view == 0 ? c->disp : c->disp1;
-    if (!src) return fail(c, SM_EINVAL, "DP[1] is only computed with do_refine = 1");
+    if (!src) return fail(c, SM_EINVAL, "DP[1] is only computed with do_refine = 1 or optimization so");
     HIP_TRY(c, hipMemcpyAsync(dst, src, c->npix * 2, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
-    return sgm2_abort_check(c);
+    return SM_OK;
 }
 
 sm_status sm_set_disp(sm_ctx* c, int32_t view, const int16_t* src) {
@@ -1200,7 +1159,7 @@ sm_status sm_set_disp(sm_ctx* c, int32_t view, const int16_t* src) {
     if (!src || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
     if (c->stage < 4) return fail(c, SM_ESTATE, "sm_set_disp must follow sm_disp_optimize");
     int16_t* dst = view == 0 ? c->disp : c->disp1;
-    if (!dst) return fail(c, SM_EINVAL, "DP[1] is only allocated with do_refine = 1");
+    if (!dst) return fail(c, SM_EINVAL, "DP[1] is only allocated with do_refine = 1 or optimization so");
     HIP_TRY(c, hipMemcpyAsync(dst, src, c->npix * 2, hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     c->stage = 4;   // refine() may run (again) on the new maps
@@ -1302,7 +1261,7 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
             s_out = hip_fail(c, e, "hipEventRecord (group CBCA done)");
             break;
         }
-        for (int v = 0; v < n_views(c->p) && !s_out; v++) s_out = run_optimize(c, m2, v, B);
+        for (int v = 0; v < opt_views(c->p) && !s_out; v++) s_out = run_optimize(c, m2, v, B);
         if (s_out) break;
         if (c->p.do_refine && (s_out = run_refine(c, m2, B))) break;
     }
@@ -1331,7 +1290,7 @@ sm_status sm_download_disp(sm_ctx* c, int32_t n, int16_t* disp_out) {
     if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
     HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDefault, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
-    return sgm2_abort_check(c);
+    return SM_OK;
 }
 
 sm_status sm_run_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr, const uint8_t* lgray,
@@ -1381,7 +1340,7 @@ sm_status sm_synchronize(sm_ctx* c) {
     sm_status s = check(c);
     if (s) return s;
     HIP_TRY(c, hipStreamSynchronize(c->st));
-    return sgm2_abort_check(c);
+    return SM_OK;
 }
 
 void* sm_stream(sm_ctx* c) { return c ? (void*)c->st : nullptr; }

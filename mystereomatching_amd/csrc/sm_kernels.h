@@ -78,21 +78,6 @@ struct SgmArgs {
     int n;                      // pairs in the launch
 };
 
-struct Sgm2Args {               // 4-path SGM in two 2-D wavefront passes (sm_sgm2.hip)
-    float* vm;                  // [n][H][W][D] C (the final sum too when keep_final)
-    float* acc;                 // [n][H][W][D] pass A: 0 + L0; pass B: the strips' exchange rows
-    float* l2v;                 // [n][H][W][D] pass A: L2
-    int16_t* disp;              // [n][H][W]
-    const uint8_t* flags;       // [n][H][W] penalty bits per direction
-    uint32_t* sync;             // sgm2_sync_words(H, n): ticket, abort flag, per-strip progress
-    int H, W, D, n;
-    float p1, p2;
-    int redu, keep_final, signed_costs;
-};
-bool sgm2_supported(int D, int paths, int W);
-size_t sgm2_sync_words(int H, int n);
-hipError_t launch_sgm2_pass(const Sgm2Args& a, bool pass_b, hipStream_t st);
-
 struct GfPix {                  // guided filter, p-independent terms of one pixel (sm_gf.hip)
     double cof[9];              // the nine cofactor expressions of guideFilterCore_matlab (cpp:5060-5078)
     double idet;                // 1 / DET

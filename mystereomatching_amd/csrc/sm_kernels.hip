@@ -160,16 +160,13 @@ constexpr uint32_t PREP_OUT = 0xffffffffu;   // fused regions: a pixel outside t
 #ifndef SM_PREP_WALK
 #define SM_PREP_WALK 1    // arm-walk steps whose LDS reads are issued together (tuning)
 #endif
-#ifndef SM_PREP_PROBE
-#define SM_PREP_PROBE 0   // timing probes: 1 = no arms, 2 = no census, 3 = neither (results wrong)
-#endif
 // census code (genCensusCode_NC_Sur, h:867-934) and x/y gradients of one pixel; g = the pixel in
 // the block's gray tile (row stride gw, REFLECT_101 halo of max(rv, 1) rows / max(ru, 1) columns)
 template <int TRV, int TRU, int TRING>
 __device__ __forceinline__ void prep_census_grad(const PrepArgs& a, const uint8_t* g, int gw, int rv, int ru, int ring,
                                                  int u, int v, size_t o) {
     const int H = a.H, W = a.W;
-    if (TRV >= 0 && a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
+    if (TRV >= 0 && a.do_census) {
         // compile-time geometry: every bit's position is a constant, so the bits go into four
         // 32-bit accumulators (acc = 2 acc + bit: a compare and an add-with-carry per bit)
         // instead of a 64-bit shift register; the words are then assembled exactly as the
@@ -194,7 +191,7 @@ __device__ __forceinline__ void prep_census_grad(const PrepArgs& a, const uint8_
         const uint64_t w0 = nb0 > 32 ? ((uint64_t)acc[0] << (nb0 - 32)) | acc[1] : acc[0];
         const uint64_t w1 = nb1 > 32 ? ((uint64_t)acc[2] << (nb1 - 32)) | acc[3] : acc[2];
         a.code[o] = make_ulonglong2(w0, w1);
-    } else if (a.do_census && SM_PREP_PROBE != 2 && SM_PREP_PROBE != 3) {
+    } else if (a.do_census) {
         const int c = g[0];
         uint64_t w[2] = {0, 0};
         uint64_t cs = 0;
@@ -508,7 +505,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         const uint32_t* pc = P + (size_t)v * W + u;
         // cross arms (calHorVerDis 7-arg, cpp:2959-3050), direction order L, R, U, D; the walks
         // read the packed image (lanes = consecutive pixels, so every step is one coalesced load)
-        if (a.do_arms && SM_PREP_PROBE != 1 && SM_PREP_PROBE != 3) {
+        if (a.do_arms) {
             uint32_t packed = 0;
             // strip walks: centre words and the two thresholds' guard-bit operands
             const uint32_t* hc = FUSED ? PHr + (yy + 1) * fhc + (x + Lo + 1) : hs + yy * hsw + (x + Lo);
@@ -679,7 +676,7 @@ __global__ __launch_bounds__(256) void k_prep_h(const PrepArgs a) {
     const int hv = max(rv, 1), hu = max(ru, 1);
     const int gw = PH_TW + 2 * hu, gh = PH_TH + 2 * hv;
     uint8_t* gt = prep_raw;
-    const bool words = a.do_arms && SM_PREP_PROBE != 1 && SM_PREP_PROBE != 3;
+    const bool words = a.do_arms;
     const bool flags = a.do_flags && (view == 0 || a.flags1);
     if (a.do_census || a.do_grad) {
         const uint8_t* G = a.gray + img * npix;
@@ -935,9 +932,6 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 // the adaptive weights the weights are 1, and 1 * x + 1 * y == x + y exactly.  lamG == 1 (the
 // default) skips the division, since -G / 1 == -G.
 // ---------------------------------------------------------------------------------------
-#ifndef SM_COST_PROBE
-#define SM_COST_PROBE 0
-#endif
 #ifndef SM_COST_STORE_AUX
 #define SM_COST_STORE_AUX 2   // buffer store cache policy: slc = non-temporal (see SM_ST_AUX, sm_device.h)
 #endif
@@ -1180,11 +1174,7 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 const int ci = oor ? icd : min((int)pc, icd);
                 const float e0 = luta[ci];                // expf(-C / lamCen)
                 const float xg = LAM1 ? -g : -g / a.lam2;
-#if SM_COST_PROBE == 1
-                const float ex = xg * 1e-3f;                 // timing probe: no exponential
-#else
                 const float ex = expf_glibc_core(xg, etab); // expf(-G / lamG)
-#endif
                 const float e1 = xg >= -17.5f ? ex : 0.f;
                 const float t = 2.0f - e0;
                 res = t - e1;
@@ -1202,9 +1192,6 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                     res = t - e1;
                 }
             }
-#if SM_COST_PROBE == 2
-            res = (float)mi;                             // timing probe: stores only
-#endif
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, voff, soff,
                                                   SM_COST_STORE_AUX);
         };

@@ -368,9 +368,6 @@ constexpr int PC_R = 2;      // ring slots: a slot is read the step after its wr
 #define SM_NL_PC_H 2         // nodes per producer wave (PC_C / PC_H producer waves per group share a chunk)
 #endif
 constexpr int PC_H = SM_NL_PC_H;
-#ifndef SM_NL_PC_PROBE
-#define SM_NL_PC_PROBE 0     // timing probes only (wrong results): 1 producers skip the data loads, 2 the consumer skips its stores
-#endif
 constexpr int PC_NH = PC_C / PC_H;
 constexpr int PC_WAVES = 1 + PC_NH * PC_P;
 static_assert(PC_WAVES + 2 <= 16 && PC_C % PC_H == 0, "a workgroup holds at most 1024 threads");
@@ -450,7 +447,7 @@ __device__ __forceinline__ void nl_up_producer(PcUpSlot* S, const NlArgs& a, con
             xc[kk] = 0.0f;
 #pragma unroll
             for (int j = 0; j < 4; j++) xm[kk][j] = 0.0;
-            if (c * PC_C + k >= len || (SM_NL_PC_PROBE & 1)) continue;
+            if (c * PC_C + k >= len) continue;
             if (dok) xc[kk] = a.vm[(size_t)x * P + d];
 #pragma unroll
             for (int j = 0; j < 4; j++)
@@ -463,7 +460,7 @@ __device__ __forceinline__ void nl_up_producer(PcUpSlot* S, const NlArgs& a, con
         const int nck = mk & 7, hvk = ((mk >> 3) & 7) - 1;
         const bool here = lane < 4 * PC_H && c * PC_C + kt < len && jt < nck;
         const double xw = here ? table[(wk >> (8 * jt)) & 255] : 0.0;
-        const double xo = (here && jt != hvk && !(SM_NL_PC_PROBE & 1)) ? a.oup[nl_child(xk, mk, jt, a.W)] : 0.0;
+        const double xo = (here && jt != hvk) ? a.oup[nl_child(xk, mk, jt, a.W)] : 0.0;
         int4 rn = make_int4(0, 0, 0, 0);
         if (c + PC_P < nst && lane < PC_C) rn = q.R[(c + PC_P) * PC_C + lane];
         for (int i = 0; i < PC_P - 1; i++) __syncthreads();   // steps c .. c + PC_P - 2: the loads stay in flight
@@ -549,7 +546,7 @@ __global__ __launch_bounds__(64 * PC_WAVES, 1) void k_nl_up_pc(const NlArgs a, c
         const double v = (((L.x + carry * wh) + L.y) + L.z) + L.w;
         const double vo = (((O.x + carry_o * wh) + O.y) + O.z) + O.w;
         const uint32_t row = (uint32_t)x * (uint32_t)P * 8u;   // (volume < 4 GiB: see launch)
-        if (!(SM_NL_PC_PROBE & 2)) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), val_r, dof, row, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), val_r, dof, row, 0);
         if (lane == 0 && q.d == 0) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, vo), oup_r, 0, (uint32_t)x * 8u, 0);
         carry = v;
         carry_o = vo;
@@ -586,7 +583,7 @@ __device__ __forceinline__ void nl_down_producer(PcDnSlot* S, const NlArgs& a, c
             const int k = K0 + kk;
             const int x = __builtin_amdgcn_readlane(rc.x, k);
             xu[kk] = 0.0;
-            if (c * PC_C + k >= len || (SM_NL_PC_PROBE & 1)) continue;
+            if (c * PC_C + k >= len) continue;
             if (dok) xu[kk] = a.val[(size_t)x * P + d];
         }
         double xo = 0.0, xw = 0.0;   // lane k in [K0, K0 + PC_H): node k's ones up sum and own weight (0: root)
@@ -653,7 +650,7 @@ __global__ __launch_bounds__(64 * (PC_WAVES + PC_SW), 1) void k_nl_down_pc(const
                         out = sum;
                     }
                     const uint32_t row = (uint32_t)x * (uint32_t)P;
-                    if (!(SM_NL_PC_PROBE & 2)) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fin), val_r, dof8, row * 8u, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fin), val_r, dof8, row * 8u, 0);
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), vm_r, dof4, row * 4u, 0);
                     if (lane == 0 && q.d == 0) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, fo), ofin_r, 0, (uint32_t)x * 8u, 0);
                 }

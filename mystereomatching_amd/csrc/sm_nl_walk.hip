@@ -136,6 +136,11 @@ __global__ __launch_bounds__(256) void k_walk_sub(WalkBufs w, int np, int nn) {
     if (!start_node((uint32_t)(g - base))) return;
     int cur = w.succ[4 * g], len = 1;
     while (cur >= 0 && !is_start(cur, base)) {
+        if (len > 4 * np) {   // a list that is no tour (a cycle without a start): stop, flag it
+            atomicOr(w.err, 8);
+            cur = -1;
+            break;
+        }
         cur = w.succ[cur];
         len++;
     }
@@ -166,7 +171,11 @@ __global__ __launch_bounds__(256) void k_walk_rank(WalkBufs w, const int* __rest
     if (g == base && r != 0) atomicOr(w.err, 2);   // the tour from pixel 0 misses arcs
     w.rank[4 * g] = r;
     int cur = w.succ[4 * g];
-    while (cur >= 0 && !is_start(cur, base)) {
+    for (int steps = 0; cur >= 0 && !is_start(cur, base); steps++) {
+        if (steps > 4 * np) {
+            atomicOr(w.err, 8);
+            break;
+        }
         w.rank[cur] = ++r;
         cur = w.succ[cur];
     }
@@ -174,6 +183,7 @@ __global__ __launch_bounds__(256) void k_walk_rank(WalkBufs w, const int* __rest
 
 // parent direction, entering rank, subtree size
 __global__ __launch_bounds__(256) void k_walk_node1(const uint32_t* __restrict__ adj, WalkBufs w, int np, int W, long nn) {
+    if (*w.err) return;   // not a spanning tree's tour (flags read by the host): indices below are invalid
     const long g = (long)blockIdx.x * 256 + threadIdx.x;
     if (g >= nn) return;
     const long b = (long)((int)g / np);   // (node ids < 2^31: 32-bit division)
@@ -204,6 +214,7 @@ __global__ __launch_bounds__(256) void k_walk_node1(const uint32_t* __restrict__
 
 // children, heavy child, record words; the children's preorder offsets into the tour
 __global__ __launch_bounds__(256) void k_walk_node2(const uint32_t* __restrict__ adj, WalkBufs w, int np, int W, long nn) {
+    if (*w.err) return;   // not a spanning tree's tour (flags read by the host): indices below are invalid
     const long g = (long)blockIdx.x * 256 + threadIdx.x;
     if (g >= nn) return;
     const long b = (long)((int)g / np);   // (node ids < 2^31: 32-bit division)
@@ -258,6 +269,7 @@ __global__ __launch_bounds__(256) void k_walk_node2(const uint32_t* __restrict__
 }
 
 __global__ __launch_bounds__(256) void k_walk_node3(WalkBufs w, int np, long nn) {
+    if (*w.err) return;   // not a spanning tree's tour (flags read by the host): indices below are invalid
     const long g = (long)blockIdx.x * 256 + threadIdx.x;
     if (g >= nn) return;
     const long b = (long)((int)g / np);   // (node ids < 2^31: 32-bit division)
@@ -275,6 +287,7 @@ __global__ __launch_bounds__(256) void k_walk_node3(WalkBufs w, int np, long nn)
 // records (bottom -> top per path), path tables per top position
 __global__ __launch_bounds__(256) void k_walk_node4(WalkBufs w, int4* __restrict__ rec, int* __restrict__ cstart, int* __restrict__ clen,
                                                     int np, int W, long nn) {
+    if (*w.err) return;   // not a spanning tree's tour (flags read by the host): indices below are invalid
     const long g = (long)blockIdx.x * 256 + threadIdx.x;
     if (g >= nn) return;
     const long b = (long)((int)g / np);   // (node ids < 2^31: 32-bit division)
@@ -296,6 +309,7 @@ __global__ __launch_bounds__(256) void k_walk_node4(WalkBufs w, int4* __restrict
 }
 
 __global__ __launch_bounds__(256) void k_walk_ul(WalkBufs w, long nn, int d) {
+    if (*w.err) return;   // not a spanning tree's tour (flags read by the host): indices below are invalid
     const long pos = (long)blockIdx.x * 256 + threadIdx.x;
     if (pos >= nn) return;
     const int pt = w.ptop[pos];
@@ -304,6 +318,7 @@ __global__ __launch_bounds__(256) void k_walk_ul(WalkBufs w, long nn, int d) {
 
 // per-block histograms in LDS, one global atomic per nonzero bin and block
 __global__ __launch_bounds__(256) void k_walk_hist(WalkBufs w, long nn) {
+    if (*w.err) return;   // (uniform over the block: before any barrier)
     __shared__ int h[2 * NL_LEVELS];
     if (threadIdx.x < 2 * NL_LEVELS) h[threadIdx.x] = 0;
     __syncthreads();
@@ -335,6 +350,7 @@ __global__ void k_walk_offs(WalkBufs w, int* __restrict__ offs) {
 // counting-sort scatter: a block counts its tops per bin in LDS, reserves each bin's range with
 // one global atomic, and places its tops (any order within a round is valid)
 __global__ __launch_bounds__(256) void k_walk_scatter(WalkBufs w, int* __restrict__ oup, int* __restrict__ odn, long nn) {
+    if (*w.err) return;   // (uniform over the block: before any barrier)
     __shared__ int h[2 * NL_LEVELS];
     if (threadIdx.x < 2 * NL_LEVELS) h[threadIdx.x] = 0;
     __syncthreads();

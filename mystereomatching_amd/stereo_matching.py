@@ -158,11 +158,12 @@ class StereoMatching:
         _capi.check(self._lib, self._ctx, self._lib.sm_cost_calculate(self._ctx), "costCalculate")
 
     def dispOptimize(self):
-        """SGM (or WTA only) -> DP[0], and DP[1] when Do_refine (cpp:1046-1136)."""
+        """SGM (or WTA only) -> DP[0], and DP[1] when Do_refine; "so" -> DP[0] and DP[1]
+        (num = Do_LRConsis ? 2 : 1, cpp:1093) (cpp:1046-1136)."""
         dp = np.empty((self.h_, self.w_), np.int16)
         _capi.check(self._lib, self._ctx, self._lib.sm_disp_optimize(self._ctx, _capi.ptr(dp)), "dispOptimize")
         self.DP[0] = dp
-        if self._refine_on:
+        if self._refine_on or (self.optimization == "so" and self.Do_LRConsis):
             d1 = np.empty((self.h_, self.w_), np.int16)
             _capi.check(self._lib, self._ctx, self._lib.sm_get_disp(self._ctx, 1, _capi.ptr(d1)), "DP[1]")
             self.DP[1] = d1
@@ -321,6 +322,12 @@ class StereoBatch:
         else:
             dst = _capi.ptr(out)
         _capi.check(self._lib, self._ctx, self._lib.sm_download_disp(self._ctx, self.n, dst), "download")
+        return out
+
+    def get_disp(self, view: int = 0) -> np.ndarray:
+        """DP[view] of the first pair (sm_get_disp): DP[1] exists with do_refine or optimization "so"."""
+        out = np.empty((self.shape[0], self.shape[1]), np.int16)
+        _capi.check(self._lib, self._ctx, self._lib.sm_get_disp(self._ctx, view, _capi.ptr(out)), "get_disp")
         return out
 
     def synchronize(self):

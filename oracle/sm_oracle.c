@@ -782,6 +782,11 @@ int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR, co
     const smo_dumps* d = dd ? dd : &none;
     const int refine = c->do_refine;
     const int views = refine ? 2 : 1;
+    /* "so" runs on both views whenever Do_LRConsis (= 1, h:72): num = Do_LRConsis ? 2 : 1
+     * (cpp:1093), so DP[1] = so(vm[1]) also without Do_refine -- on the raw right cost volume,
+     * since CBCA (cpp:5592) and SolveAll (cpp:2178) touch vm[1] only with Do_refine */
+    const int so_views = c->optimization == 2 ? 2 : views;
+    const int right = refine || so_views == 2;
     const size_t npix = (size_t)c->H * c->W, nvol = npix * c->D;
     double t0 = now_ms(), t;
     double ms[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -791,11 +796,11 @@ int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR, co
     int rc = -1;
     vm[0] = (float*)malloc(nvol * 4);
     if (!vm[0]) goto done;
-    if (refine && !(vm[1] = (float*)malloc(nvol * 4))) goto done;
+    if (right && !(vm[1] = (float*)malloc(nvol * 4))) goto done;
     smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 0, vm[0]);
-    if (refine) smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 1, vm[1]);
+    if (right) smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 1, vm[1]);
     else if (d->vol_right) smo_cost_volume(c, bgrL, bgrR, grayL, grayR, 1, d->vol_right);
-    if (refine && d->vol_right) memcpy(d->vol_right, vm[1], nvol * 4);
+    if (right && d->vol_right) memcpy(d->vol_right, vm[1], nvol * 4);
     if (d->vol_cost) memcpy(d->vol_cost, vm[0], nvol * 4);
     t = now_ms(); ms[0] = t - t0; t0 = t;
     if (c->aggregation == 1 || refine) {
@@ -817,16 +822,16 @@ int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR, co
     if (c->solve_all)
         for (int i = 0; i < views; i++) smo_solve_all(c, vm[i]);               /* img_n (cpp:2178) */
     t = now_ms(); ms[2] = t - t0; t0 = t;
-    if (refine && !(dp1 = (int16_t*)malloc(npix * 2))) goto done;
+    if (right && !(dp1 = (int16_t*)malloc(npix * 2))) goto done;
     if (c->optimization == 1)
         for (int i = 0; i < views; i++) smo_sgm(c, vm[i], i == 0 ? bgrL : bgrR);  /* cpp:1053-1060 */
     if (c->optimization == 2)   /* "so": DP directly, I_c[0] for both views (cpp:1091-1105) */
-        for (int i = 0; i < views; i++) smo_so(c, vm[i], i == 0 ? disp : dp1, bgrL);
+        for (int i = 0; i < so_views; i++) smo_so(c, vm[i], i == 0 ? disp : dp1, bgrL);
     if (d->vol_final) memcpy(d->vol_final, vm[0], nvol * 4);
     t = now_ms(); ms[3] = t - t0; t0 = t;
     if (c->optimization != 2) smo_wta(c, vm[0], disp);
-    if (refine) {
-        if (c->optimization != 2) smo_wta(c, vm[1], dp1);                      /* cpp:1110-1127 */
+    if (refine && c->optimization != 2) smo_wta(c, vm[1], dp1);               /* cpp:1110-1127 */
+    if (dp1) {
         if (d->disp_left_raw) memcpy(d->disp_left_raw, disp, npix * 2);
         if (d->disp_right) memcpy(d->disp_right, dp1, npix * 2);
     }

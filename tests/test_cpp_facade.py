@@ -187,6 +187,38 @@ int main(int argc, char** argv) {
 """
 
 
+def _png_with_header(w, h, depth=8, ctype=2, idat=b""):
+    import struct
+    import zlib
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)
+    return b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", idat) + chunk(b"IEND", b"")
+
+
+def test_imread_png_rejects_oversized_headers(tmp_path):
+    """Crafted IHDR sizes (round-3 ADVICE): sizes whose products wrap 32 / 64-bit buffer sizes,
+    sizes above the 2^28-pixel cap, and a header far larger than its compressed data must give an
+    empty Mat (imread's failure result, main_.cpp:108), never a short buffer or an exception."""
+    import zlib
+    src = tmp_path / "png_check.cpp"
+    src.write_text(PNG_CHECK)
+    exe = str(tmp_path / "png_check")
+    _compile(str(src), exe, link=False)
+    small = zlib.compress(bytes(4 * (1 + 3 * 4)))
+    cases = [(0xFFFFFFFF, 0xFFFFFFFF, 8, 2), (0x80000000, 2, 8, 2), (0x10000, 0x10000, 8, 2),
+             (0x7FFFFFFF, 3, 16, 6), (1 << 15, 1 << 14, 8, 0), (20000, 13000, 16, 6), (1, 0, 8, 2)]
+    files = []
+    for i, (w, h, depth, ctype) in enumerate(cases):
+        f = tmp_path / f"bad{i}.png"
+        f.write_bytes(_png_with_header(w, h, depth, ctype, small))
+        files.append(str(f))
+    r = subprocess.run([exe] + files, capture_output=True, timeout=60)
+    assert r.returncode == 0, r.stderr[:300]
+    assert r.stdout.decode().split() == sum((["E", str(i + 1)] for i in range(len(cases))), [])
+
+
 def test_imread_png(tmp_path):
     """smamd::imread on PNG files written by PIL: RGB, RGBA, gray, 16-bit gray, 1/4-bit gray and
     palette images, several filter choices -- BGR for flags 1 and libpng's rgb_to_gray for flags 0,

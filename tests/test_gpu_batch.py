@@ -1,4 +1,6 @@
 """GPU: device-resident batch entry points and the batch runner's product compute path."""
+import contextlib
+
 import numpy as np
 import pytest
 
@@ -103,10 +105,9 @@ def test_runner_numpy_fn_gets_host_arrays(oracle):
     np.testing.assert_array_equal(got, _oracle_maps(oracle, batch, H, W, md))
 
 
-def test_runner_rccl_world_one(oracle):
-    """DistributedBatchRunner over an initialised `nccl` (RCCL) process group of size 1: header
-    broadcast, scatter and gather run as RCCL collectives on device tensors, as on the 8-GPU node
-    (configs[4]); the maps must equal the oracle's."""
+@contextlib.contextmanager
+def _rccl_world_one():
+    """An initialised `nccl` (RCCL) process group of size 1 on device 0 (127.0.0.1 rendezvous)."""
     import socket
     import torch
     import torch.distributed as dist
@@ -114,18 +115,60 @@ def test_runner_rccl_world_one(oracle):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    H, W, md, n = 30, 52, 15, 3
-    batch = S.make_batch(n, H, W, md + 1, first_index=440)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
-    fn = hip_compute_fn(md, H, W, n, device=0)
     try:
-        runner = DistributedBatchRunner(fn)
-        assert runner.collective and runner.device.type == "cuda"
-        want = _oracle_maps(oracle, batch, H, W, md)
-        for _ in range(2):
-            np.testing.assert_array_equal(runner.run(batch, max_disp=md, reg_lambda=0.3), want)
+        yield
     finally:
-        fn.close()
         dist.destroy_process_group()
+
+
+def test_runner_rccl_world_one(oracle):
+    """DistributedBatchRunner over an initialised `nccl` (RCCL) process group of size 1: header
+    broadcast, scatter and gather run as RCCL collectives on device tensors, as on the 8-GPU node
+    (configs[4]); the maps must equal the oracle's."""
+    H, W, md, n = 30, 52, 15, 3
+    batch = S.make_batch(n, H, W, md + 1, first_index=440)
+    with _rccl_world_one():
+        fn = hip_compute_fn(md, H, W, n, device=0)
+        try:
+            runner = DistributedBatchRunner(fn)
+            assert runner.collective and runner.device.type == "cuda"
+            want = _oracle_maps(oracle, batch, H, W, md)
+            for _ in range(2):
+                np.testing.assert_array_equal(runner.run(batch, max_disp=md, reg_lambda=0.3), want)
+        finally:
+            fn.close()
+
+
+def test_runner_rccl_hd1080_rank_shard():
+    """configs[4] on one rank: one rank's share of the 64-pair batch (8 synthetic pairs of
+    1920 x 1080, D = 256) through DistributedBatchRunner over RCCL (broadcast, scatter of the
+    images as device tensors, the whole hot path per pair, gather of the int16 maps), i.e.
+    main_.cpp:135-163 per pair.  Pair 0 must equal the oracle fixture large_hd1080_d256 bit for
+    bit, and all 8 maps must equal a plain StereoBatch.run of the same pairs."""
+    import hashlib
+    import os
+    H, W, md, n = 1080, 1920, 255, 8
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large_hd1080_d256.npz"))
+    assert (int(z["H"]), int(z["W"]), int(z["max_disp"]), int(z["index"])) == (H, W, md, 0)
+    batch = S.make_batch(n, H, W, md + 1, first_index=0)
+    for k in KEYS:
+        assert hashlib.sha256(np.ascontiguousarray(batch[k][0]).tobytes()).hexdigest() == str(z["sha_" + k])
+    with _rccl_world_one():
+        fn = hip_compute_fn(md, H, W, n, device=0)
+        try:
+            runner = DistributedBatchRunner(fn)
+            assert runner.collective and runner.device.type == "cuda"
+            got = runner.run(batch, max_disp=md, reg_lambda=0.3)
+        finally:
+            fn.close()
+    assert got.shape == (n, H, W)
+    np.testing.assert_array_equal(got[0], z["disp"])
+    sb = StereoBatch(md, H, W, n, device=0)
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        np.testing.assert_array_equal(got, sb.run(0.3))
+    finally:
+        sb.close()

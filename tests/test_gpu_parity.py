@@ -80,7 +80,8 @@ def test_cost_volume_and_stages(oracle, cost):
 
 
 @pytest.mark.parametrize("rv,ru,ring,cost,md", [(1, 1, 0, 1, 23), (2, 3, 1, 0, 99), (3, 4, 0, 2, 23),
-                                                 (4, 4, 1, 0, 23), (4, 5, 1, 0, 70), (4, 5, 1, 2, 99)])
+                                                 (4, 4, 1, 0, 23), (4, 5, 1, 0, 70), (4, 5, 1, 2, 99),
+                                                 (2, 2, 0, 0, 23), (2, 2, 0, 1, 70), (2, 2, 0, 2, 130)])
 def test_census_windows(oracle, rv, ru, ring, cost, md):
     """Census widths of 1-4 32-bit words (cost-kernel record layouts), D <= 64 and D > 64, both views."""
     H, W = 23, 97
@@ -151,6 +152,71 @@ def test_right_view_volume(oracle):
     finally:
         lib.sm_destroy(ctx)
     np.testing.assert_array_equal(bits(got), bits(ref))
+
+
+@pytest.mark.parametrize("cost,md,paths", [("censusGrad", 63, 4), ("Census", 40, 8), ("ADCensus", 100, 4)])
+def test_census_5x5_maps(oracle, cost, md, paths):
+    """north_star's 5 x 5 census (census_rv = census_ru = 2, no ring bits: the generic census
+    path, not the unrolled 7 x 9 + ring default): census codes of both views and the final maps
+    through the whole pipeline, against the oracle."""
+    H, W = 47, 133
+    pair = S.make_pair(H, W, md + 1, 880 + md)
+    cfg = oracle.config(H, W, md, cost=cost, census_rv=2, census_ru=2, census_ring=0, sgm_paths=paths)
+    ref = oracle.run(pair, cfg, dumps=True)
+    sb = StereoBatch(md, H, W, 1, cost_method=cost, census_rv=2, census_ru=2, census_ring=0, sgm_paths=paths,
+                     keep_final_volume=1)
+    try:
+        sb.upload(*(pair[k][None] for k in ("lbgr", "rbgr", "lgray", "rgray")))
+        np.testing.assert_array_equal(sb.run(0.3)[0], ref["disp"])
+        got = np.empty((H, W, md + 1), np.float32)
+        lib = _capi.load()
+        _capi.check(lib, sb._ctx, lib.sm_get_volume(sb._ctx, 0, _capi.ptr(got)))
+        np.testing.assert_array_equal(bits(got), bits(ref["final"]))
+        for view, g in ((0, "lgray"), (1, "rgray")):
+            codes = np.zeros((H, W, 2), np.uint64)
+            _capi.check(lib, sb._ctx, lib.sm_get_census(sb._ctx, view, _capi.ptr(codes)))
+            want = oracle.census(pair[g], cfg)
+            np.testing.assert_array_equal(codes[..., :want.shape[2]], want)
+    finally:
+        sb.close()
+
+
+def test_contexts_with_different_cost_constants(oracle):
+    """Contexts on one device keep their own exponent tables (round-2 ADVICE: no __constant__ LUT
+    shared across contexts): censusGrad with lamCen 13 and 5, ADCensus with lamCen 30 / lamAD 10
+    and with 11 / 4, created together and run interleaved; each context's raw cost volume
+    (gen_vm_from2vm_exp, cpp:3566-3590) and final map must equal the oracle's for ITS constants."""
+    H, W, md = 33, 71, 31
+    pair = S.make_pair(H, W, md + 1, 905)
+    cases = [("censusGrad", dict(lam_cen=13.0)), ("censusGrad", dict(lam_cen=5.0)),
+             ("ADCensus", dict(lam_cen_adc=30.0, lam_ad=10.0)), ("ADCensus", dict(lam_cen_adc=11.0, lam_ad=4.0))]
+    lib = _capi.load()
+    ctxs = []
+    try:
+        for cost, kw in cases:   # raw volumes: aggregation and SGM off (WTA keeps vm)
+            ctxs.append(StereoBatch(md, H, W, 1, cost_method=cost, aggregation=0, optimization=0, **kw))
+            ctxs.append(StereoBatch(md, H, W, 1, cost_method=cost, **kw))
+        for sb in ctxs:
+            sb.upload(*(pair[k][None] for k in ("lbgr", "rbgr", "lgray", "rgray")))
+        for rnd in range(2):   # interleaved: a table left behind by another context would show
+            for i, sb in enumerate(ctxs):
+                cost, kw = cases[i // 2]
+                if i % 2 == 0:
+                    sb.run(0.3)
+                    got = np.empty((H, W, md + 1), np.float32)
+                    _capi.check(lib, sb._ctx, lib.sm_get_volume(sb._ctx, 0, _capi.ptr(got)))
+                    # sm_run applies SolveAll's scale to the unaggregated volume: compare with the
+                    # oracle's final volume of the same WTA-only pipeline
+                    cfg = oracle.config(H, W, md, cost=cost, aggregation=0, optimization=0, **kw)
+                    ref = oracle.run(pair, cfg, dumps=True)
+                    np.testing.assert_array_equal(bits(got), bits(ref["final"]), err_msg=f"{cost} {kw}")
+                    np.testing.assert_array_equal(sb.download()[0], ref["disp"])
+                else:
+                    cfg = oracle.config(H, W, md, cost=cost, **kw)
+                    np.testing.assert_array_equal(sb.run(0.3)[0], oracle.run(pair, cfg)["disp"], err_msg=f"{cost} {kw}")
+    finally:
+        for sb in ctxs:
+            sb.close()
 
 
 def test_census_and_arms(oracle):

@@ -49,6 +49,34 @@ def test_so_other_costs_batch(oracle, cost, agg):
         np.testing.assert_array_equal(out[i], oracle.run(p, cfg)["disp"], err_msg=f"pair {i}")
 
 
+@pytest.mark.parametrize("cost,H,W,md", [("censusGrad", 29, 83, 31), ("ADCensus", 18, 140, 127)])
+def test_so_right_view_without_refine(oracle, cost, H, W, md):
+    """so runs on both views whenever Do_LRConsis (num = Do_LRConsis ? 2 : 1, cpp:1093), also
+    with Do_refine off: DP[1] = so(vm[1]) on the raw right cost volume (CBCA, cpp:5592, and
+    SolveAll, cpp:2178, touch vm[1] only with Do_refine), with the left colours (cpp:1098)."""
+    pair = S.make_pair(H, W, md + 1, 700 + md)
+    StereoMatching.costcalculation, StereoMatching.aggregation, StereoMatching.optimization = cost, "CBCA", "so"
+    try:
+        prm = StereoMatching.Parameters(md, H, W)
+        sm = StereoMatching(pair["lbgr"], pair["rbgr"], pair["lgray"], pair["rgray"], None, None, None, None, prm)
+        sm.costCalculate()
+        SolveAll([sm], 1, 0.3)
+        sm.dispOptimize()
+    finally:
+        StereoMatching.optimization = "sgm"
+    ref = oracle.run_ex(pair, oracle.config(H, W, md, cost=cost, optimization=2), dumps=("disp_right",))
+    np.testing.assert_array_equal(sm.DP[0], ref["disp"])
+    np.testing.assert_array_equal(sm.DP[1], ref["disp_right"])
+    # the batch path leaves DP[1] in the context too
+    b = StereoBatch(md, H, W, 1, optimization="so", cost_method=cost)
+    try:
+        b.upload(*(pair[k][None] for k in ("lbgr", "rbgr", "lgray", "rgray")))
+        np.testing.assert_array_equal(b.run()[0], ref["disp"])
+        np.testing.assert_array_equal(b.get_disp(1), ref["disp_right"])
+    finally:
+        b.close()
+
+
 def test_so_with_refine(oracle):
     H, W, md = 40, 66, 23
     pair = S.make_pair(H, W, md + 1, 77)

@@ -204,3 +204,9 @@ def test_so_bitexact(oracle, H, W, D, idx):
     r = oracle.run_ex(p, cfgr, dumps=("agg_right", "disp_right"))
     _, ref_d1 = pyref.so(pyref.solve_all(r["agg_right"]), p["lbgr"])
     np.testing.assert_array_equal(r["disp_right"], ref_d1)
+    # without refine "so" still runs on both views (num = Do_LRConsis ? 2 : 1, cpp:1093): DP[1]
+    # from the raw right cost volume (CBCA and SolveAll touch vm[1] only with Do_refine)
+    n = oracle.run_ex(p, cfg, dumps=("right", "disp_right"))
+    np.testing.assert_array_equal(n["disp"], got["disp"])
+    _, ref_n1 = pyref.so(n["right"], p["lbgr"])
+    np.testing.assert_array_equal(n["disp_right"], ref_n1)

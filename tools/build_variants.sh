@@ -17,7 +17,7 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc $FLAGS $defs -c $SRC.$EXT -o build/var/${SRC}__$name.o &
 done
 wait
-OBJS="build/sm_kernels.o build/sm_cbca.o build/sm_sgm.o build/sm_sgm2.o build/sm_refine.o build/sm_pyramid.o build/sm_so.o build/sm_gf.o build/sm_gf_cv.o build/sm_nl.o build/sm_nl_mst.o build/sm_nl_walk.o build/sm_capi.o"
+OBJS="build/sm_kernels.o build/sm_cbca.o build/sm_sgm.o build/sm_refine.o build/sm_pyramid.o build/sm_so.o build/sm_gf.o build/sm_gf_cv.o build/sm_nl.o build/sm_nl_mst.o build/sm_nl_walk.o build/sm_capi.o"
 for o in build/var/${SRC}__*.o; do
   name=${o#build/var/${SRC}__}; name=${name%.o}
   objs=${OBJS/build\/$SRC.o/$o}

@@ -43,6 +43,7 @@ struct sm_ctx {
     std::string err;
     int cap = 1;
     size_t npix = 0, nvol = 0;
+    size_t vtail = 0;           // floats of tail pad after each volume's cap * nvol
     uint8_t* bgr = nullptr;     // [cap][2][npix][3]
     uint8_t* gray = nullptr;    // [cap][2][npix]
     ulonglong2* code = nullptr; // [cap][2][npix]
@@ -191,6 +192,28 @@ int n_views(const sm_params& p) { return p.do_refine ? 2 : 1; }   // imgNum = Do
 int opt_views(const sm_params& p) { return p.optimization == SM_OPT_SO ? 2 : n_views(p); }
 
 int cbca_lag(const sm_params& p) { return p.arm_l_out > p.arm_min_l ? p.arm_l_out : p.arm_min_l; }
+
+// Every dividend of iteration k's normalisation (genfinalVm_cbca, cpp:3969-3992) is 0 or
+// >= 2^-110, so the area division needs no check for tiny dividends (sm_device.h div_area)?
+// Costs are 0 or >= 2^f0: censusGrad / ADCensus fl(fl(2 - e0) - e1) with e0, e1 in [0, 1] is 0
+// or >= 2^-24 (fl(2 - e0) = 1 gives 1 - e1 >= 2^-24 unless e1 = 1, else >= 1 + 2^-23 - 1);
+// Census costs are integers; AD costs are 0 or >= min(1/3, trunc).  A prefix sum of values 0 or
+// >= 2^f is 0 or >= 2^f, and a difference of two such sums is 0, the larger sum, or >= ulp(2^f)
+// = 2^(f - 23); so iteration k's scan outputs are 0 or >= 2^(f_k - 23), its normalisation's
+// dividends 0 or >= 2^(f_k - 46), and its quotients (areas < 2^15) 0 or >= 2^(f_k - 61) = f_{k+1}.
+bool cbca_div_safe(const sm_params& p, int k) {
+    int f0;
+    if (p.cost_method == SM_COST_CENSUS_GRAD || p.cost_method == SM_COST_AD_CENSUS) {
+        f0 = -24;
+    } else if (p.cost_method == SM_COST_CENSUS) {
+        f0 = 0;
+    } else {   // AD: min(s / 3, trunc)
+        if (p.ad_trunc_ad == 0.0f) return true;   // every cost is 0
+        const float m = std::min(1.0f / 3.0f, p.ad_trunc_ad);
+        f0 = std::ilogb(m);
+    }
+    return f0 - 61 * k - 46 >= -110;
+}
 
 bool nonneg(float x) { return x >= 0 && !std::signbit(x); }   // >= +0 (rejects NaN and -0.0)
 
@@ -455,11 +478,12 @@ sm_status run_cbca(sm_ctx* c, int n, int view, bool fuse_scale, float w, const B
     a.W = p.cols;
     a.D = p.num_disparities;
     a.lag = cbca_lag(p);
-    a.vm_end = (view == 0 ? c->vm0 : c->vm1) + (size_t)c->cap * c->nvol;
+    a.vm_end = (view == 0 ? c->vm0 : c->vm1) + (size_t)c->cap * c->nvol + c->vtail;   // incl. the tail pad
     a.arms_end = (const uint32_t*)(c->arms + c->arms_bytes);
     a.scale = w;
     a.apply_scale = 0;
     a.num_cu = c->num_cu;
+    a.arm_pad_rows = 2 * cbca_lag(p);
     const double bytes = (double)n * c->nvol * 8.0;
     // profile names: "cbca_h_scan" etc. for vm[0], "cbca_h_scan_r" etc. for vm[1]
     std::string sfx = view == 0 ? "" : "_r";
@@ -468,6 +492,7 @@ sm_status run_cbca(sm_ctx* c, int n, int view, bool fuse_scale, float w, const B
     if (s) return s;
     for (int k = 0; k < N; k++) {
         const bool dir_h = (k % 2 == 1);  // direction of iteration k's second pass
+        a.div_safe = cbca_div_safe(p, k) ? 1 : 0;   // this step's normalisation is iteration k's
         if (k + 1 < N && c->fuse_norm_scan) {
             s = timed(c, nm(dir_h ? "cbca_h_norm_scan" : "cbca_v_norm_scan"), bytes,
                       [&] { sm::launch_cbca(a, dir_h, sm::CB_NORM_SCAN, n, c->st); });
@@ -868,13 +893,18 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->gx, cap * 2 * c->npix))) return s;
     if ((s = dalloc(c, &c->gy, cap * 2 * c->npix))) return s;
     {
+        // front pad: V sweeps read rows i - lag >= -2 lag; tail pad: the fast V sweep's loads run
+        // up to 2 lag + 3 T rows past the last plane's end (sm_cbca.hip NsV)
         const size_t pad = ((size_t)2 * cbca_lag(*p) * p->cols * 4 + 255) / 256 * 256;
+        const size_t tail = (size_t)(2 * cbca_lag(*p) + 64) * p->cols * 4;
         c->arms_bytes = cap * 2 * 2 * c->npix * 4;
-        if ((s = dalloc(c, &c->arms_alloc, pad + c->arms_bytes))) return s;
+        if ((s = dalloc(c, &c->arms_alloc, pad + c->arms_bytes + tail))) return s;
         c->arms = c->arms_alloc + pad;
     }
-    // volumes carry a 4 KiB tail: vectorised SGM lanes past D read (never write) into it
-    const size_t vpad = 1024;
+    // volumes carry a tail: vectorised SGM lanes past D read (never write) into it, and the fast V
+    // sweep's tiles that straddle the last rows read up to CBCA_VM_TAIL_ROWS rows past them
+    const size_t vpad = 1024 + (size_t)sm::CBCA_VM_TAIL_ROWS * p->cols * p->num_disparities;
+    c->vtail = vpad;
     if ((s = dalloc(c, &c->vm0, cap * c->nvol + vpad))) return s;
     if (right_view(*p))
         if ((s = dalloc(c, &c->vm1, cap * c->nvol + vpad))) return s;

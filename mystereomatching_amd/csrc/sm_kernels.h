@@ -61,8 +61,13 @@ struct CbcaArgs {
     int apply_scale;
     float scale;                // SolveAll weight (fused into the last normalising pass)
     int view;                   // 0: vm[0] (left reference), 1: vm[1] (right reference, Do_refine)
-    int num_cu;                 // compute units of the device (persistent V sweeps)
+    int num_cu;                 // compute units of the device
+    int arm_pad_rows;           // rows of front pad before the arm planes (2 lag; the allocation also
+                                // has >= 2 lag + 64 rows of tail pad, and the volumes >= 8 rows)
+    int div_safe;               // 1: every dividend of this launch's normalisation is 0 or >= 2^-110
+                                // (proven by the host, cbca_div_safe): the area division needs no check
 };
+constexpr int CBCA_VM_TAIL_ROWS = 8;   // volume tail pad in rows of W * D floats (fast V sweeps)
 
 struct SgmArgs {
     float* vm;                  // [n][H][W][D] aggregated costs (also the final volume if keep_final)

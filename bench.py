@@ -5,6 +5,9 @@ torch.distributed.run, one rank per GPU.  A step = one pass of the whole hot pat
 (cost volume -> CBCA x2 -> SolveAll -> 4-path SGM -> WTA) over one batch of synthetic pairs
 already resident in HBM.  Pairs shard across ranks with no data-path collective (weak scaling:
 each rank owns its own batch); RCCL is used only for the barrier and the max-over-ranks time.
+With N > 1 the line also carries "e2e_batch": a few steps of the product batching path
+(DistributedBatchRunner: rank 0's host batch scattered over RCCL, maps gathered back), timed after
+the resident measurement.
 
 Default workload = BASELINE.json configs[3], the largest single-GPU config and the one north_star's
 targets are quoted on: Middlebury-2014 full resolution 3000x2000, D = 256, censusGrad + CBCA(2) +
@@ -112,6 +115,8 @@ def parse():
     ap.add_argument("--fuse-norm-scan", choices=["auto", "on", "off"], default="auto",
                     help="CBCA: fuse iteration k's normalising sweep with iteration k+1's scan (sm_params.fuse_norm_scan; "
                          "auto = for volumes >= 256 MiB per pair)")
+    ap.add_argument("--no-e2e-batch", action="store_true",
+                    help="N > 1: skip the DistributedBatchRunner steps reported as e2e_batch next to the resident line")
     ap.add_argument("--e2e", action="store_true",
                     help="time the product multi-GPU path instead of resident batches: rank 0 holds the global "
                          "batch on the host; each step broadcasts the header, scatters the pairs (RCCL), runs "
@@ -185,13 +190,15 @@ def main():
             dist.barrier()
 
     # A step ends with the maps on the host (t up to "disp_out ready"): the int16 maps
-    # of the batch are copied into page-locked host memory and the copy is waited for.
+    # of the batch are copied into page-locked host memory on the context's copy stream
+    # (sm_download_disp_async), overlapping the next step's cost / aggregation work; the next
+    # step's map-writing kernels wait for the copy, and the timed region ends after the last copy.
     host_maps = torch.empty((B, H, W), dtype=torch.int16, pin_memory=True).numpy() if not args.no_d2h else None
 
     def step():
         sb.run(0.3, download=False)
         if host_maps is not None:
-            sb.download(host_maps)
+            sb.download_async(host_maps)
 
     for _ in range(args.warmup):
         step()
@@ -323,6 +330,13 @@ def main():
                              f"linearly to the {W}x{H} pairs; the GPU's map of the same crop checked bit-exact against it",
                    "host": host}
 
+    # N > 1: the product batching path as well (configs[4]'s RCCL scatter / gather), timed after
+    # the resident-batch line and reported beside it -- never instead of it
+    e2e = None
+    if world > 1 and not args.no_e2e_batch:
+        sb.close()
+        e2e = _e2e_batch(args, world, rank, local, dist, backend, batch, H, W, md, paths, B)
+
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mdisp/s", "n_gpus": world,
@@ -333,17 +347,65 @@ def main():
                        "sgm_paths": paths, "aggregation": args.agg, "optimization": args.opt, "refine": bool(args.refine),
                        "parallelism": f"dp{world} (independent pairs, no data-path collective)",
                        "timed_region": "inputs resident in HBM -> maps in HBM (D2H excluded, --no-d2h)" if args.no_d2h
-                       else "inputs resident in HBM -> int16 maps in pinned host memory (D2H included)"},
+                       else "inputs resident in HBM -> int16 maps in pinned host memory (D2H included, each "
+                            "step's copy overlapping the next step's compute; the last copy inside the region)"},
             "bad_2.0_nonocc_pct": round(100 * bad2, 3), "bad_1.0_nonocc_pct": round(100 * bad1, 3),
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "kernels": kern_out,
             "ms_per_step_instrumented": None if ms_prof is None else round(ms_prof, 4),
         }
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if e2e is not None:
+            out["e2e_batch"] = e2e
         print(json.dumps(out))
     sb.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _e2e_batch(args, world, rank, local, dist, backend, batch, H, W, md, paths, B, steps=3):
+    """A few steps of mystereomatching_amd.batch.DistributedBatchRunner: rank 0 holds a global
+    batch of B x world pairs on the host (its own B pairs, repeated), broadcasts the header,
+    scatters the pairs over RCCL, every rank runs its block, the int16 maps are gathered back.
+    Errors are reported in the JSON object, never raised (the resident line stands on its own)."""
+    import torch
+    from mystereomatching_amd.batch import DistributedBatchRunner, hip_compute_fn
+    D = md + 1
+    fn = None
+    try:
+        glob = {k: np.ascontiguousarray(np.concatenate([batch[k]] * world)) for k in ("lbgr", "rbgr", "lgray", "rgray")} \
+            if rank == 0 else None
+        fn = hip_compute_fn(md, H, W, B, local, sgm_paths=paths)
+        runner = DistributedBatchRunner(fn)
+        maps = runner.run(glob, md, 0.3)   # warm-up
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            maps = runner.run(glob, md, 0.3)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        ok = None
+        if rank == 0:
+            ok = bool(all(np.array_equal(maps[r * B], maps[0]) for r in range(world)))
+            fx = fixture_check(args.workload, False, "sgm", maps[0]) if not args.no_parity and args.agg == "CBCA" \
+                and args.opt == "sgm" and not args.refine else None
+            if fx is not None:
+                ok = ok and fx["bit_exact"]
+        return {"value": round(world * B * H * W * D * steps / el / 1e6, 2), "unit": "Mdisp/s",
+                "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "global_batch": world * B,
+                "path": f"DistributedBatchRunner ({backend}): header broadcast, scatter of host pairs from rank 0, "
+                        "compute, gather of the int16 maps to rank 0 host memory",
+                "maps_ok": ok}
+    except Exception as e:   # noqa: BLE001 -- reported, not raised
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    finally:
+        if fn is not None:
+            fn.close()
 
 
 def run_e2e(args, world, rank, local, dist, backend):

@@ -176,6 +176,11 @@ SM_API sm_status sm_upload_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, co
  * NULL to leave the maps on the device (read them with sm_download_disp). */
 SM_API sm_status sm_run(sm_ctx* ctx, int32_t n, float reg_lambda, int16_t* disp_out);
 SM_API sm_status sm_download_disp(sm_ctx* ctx, int32_t n, int16_t* disp_out);
+/* The same copy, enqueued on the ctx's copy stream behind the work queued so far, returning at
+ * once: the next sm_run's disparity-writing kernels wait for it, so the copy overlaps the next
+ * run's cost / aggregation work.  disp_out must be page-locked host memory (or device memory) and
+ * stays in flight until sm_synchronize. */
+SM_API sm_status sm_download_disp_async(sm_ctx* ctx, int32_t n, int16_t* disp_out);
 SM_API sm_status sm_run_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
                               const uint8_t* lgray, const uint8_t* rgray, float reg_lambda,
                               int16_t* disp_out);

@@ -103,6 +103,9 @@ struct sm_ctx {
     int sub_batch = 0;          // sm_params.sub_batch: run sm_run in groups of k pairs (0 = all)
     int nstreams = 1;           // sm_params.num_streams: groups alternate over s streams (see sm_run)
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
+    hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
+    hipEvent_t ev_run = nullptr, ev_copy = nullptr;     // run done (c->st) / async copy done (cst)
+    bool copy_pending = false;  // an async copy may still read the maps
     std::vector<hipEvent_t> xev;                        // stagger / join events
     // profiling
     bool prof = false;
@@ -334,6 +337,14 @@ void free_all(sm_ctx* c) {
     for (auto e : c->free_events) hipEventDestroy(e);
     for (auto e : c->xev) hipEventDestroy(e);
     c->xev.clear();
+    if (c->cst) {
+        hipStreamSynchronize(c->cst);
+        hipStreamDestroy(c->cst);
+        c->cst = nullptr;
+    }
+    if (c->ev_run) hipEventDestroy(c->ev_run);
+    if (c->ev_copy) hipEventDestroy(c->ev_copy);
+    c->ev_run = c->ev_copy = nullptr;
     for (auto& x : c->xst)
         if (x) {
             hipStreamDestroy(x);
@@ -786,6 +797,12 @@ sm_status upload(sm_ctx* c, int n, const uint8_t* lbgr, const uint8_t* rbgr, siz
     return SM_OK;
 }
 
+// the maps are about to be written: an asynchronous copy of the previous maps must be done
+sm_status wait_copy(sm_ctx* c) {
+    if (c->copy_pending) HIP_TRY(c, hipStreamWaitEvent(c->st, c->ev_copy, 0));
+    return SM_OK;
+}
+
 sm_status check(sm_ctx* c) {
     if (!c) return SM_EINVAL;
     hipError_t e = hipSetDevice(c->device);
@@ -900,6 +917,10 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         c->arms_bytes = cap * 2 * 2 * c->npix * 4;
         if ((s = dalloc(c, &c->arms_alloc, pad + c->arms_bytes + tail))) return s;
         c->arms = c->arms_alloc + pad;
+        // the pads hold zero arms (never written later): rows the sweeps read outside the planes
+        // then give zero-length windows, so every window slot stays inside the rings
+        HIP_TRY(c, hipMemset(c->arms_alloc, 0, pad));
+        HIP_TRY(c, hipMemset(c->arms + c->arms_bytes, 0, tail));
     }
     // volumes carry a tail: vectorised SGM lanes past D read (never write) into it, and the fast V
     // sweep's tiles that straddle the last rows read up to CBCA_VM_TAIL_ROWS rows past them
@@ -1153,6 +1174,7 @@ sm_status sm_disp_optimize(sm_ctx* c, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
     if (c->stage < 2 || c->stage > 3) return fail(c, SM_ESTATE, "sm_disp_optimize must follow sm_cost_calculate / sm_solve_all");
+    if ((s = wait_copy(c))) return s;
     for (int v = 0; v < opt_views(c->p); v++)   // num (cpp:1054, 1093, 1110)
         if ((s = run_optimize(c, c->n_loaded, v, at(c, 0)))) return s;
     c->stage = 4;
@@ -1165,6 +1187,7 @@ sm_status sm_refine(sm_ctx* c, int16_t* disp_out) {
     if (s) return s;
     if (!c->p.do_refine) return fail(c, SM_ESTATE, "sm_refine needs do_refine = 1 at sm_create (DP[1] is not computed otherwise)");
     if (c->stage != 4) return fail(c, SM_ESTATE, "sm_refine must follow sm_disp_optimize");
+    if ((s = wait_copy(c))) return s;
     if ((s = run_refine(c, c->n_loaded, at(c, 0)))) return s;
     c->stage = 5;
     if (disp_out) return sm_download_disp(c, 1, disp_out);
@@ -1188,6 +1211,7 @@ sm_status sm_set_disp(sm_ctx* c, int32_t view, const int16_t* src) {
     if (s) return s;
     if (!src || view < 0 || view > 1) return fail(c, SM_EINVAL, "bad arguments");
     if (c->stage < 4) return fail(c, SM_ESTATE, "sm_set_disp must follow sm_disp_optimize");
+    if ((s = wait_copy(c))) return s;
     int16_t* dst = view == 0 ? c->disp : c->disp1;
     if (!dst) return fail(c, SM_EINVAL, "DP[1] is only allocated with do_refine = 1 or optimization so");
     HIP_TRY(c, hipMemcpyAsync(dst, src, c->npix * 2, hipMemcpyHostToDevice, c->st));
@@ -1287,6 +1311,12 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
                 s_out = run_scale(c, m2, v, w, B);      // (GF and NL's vm[0]: fused above)
         }
         if (s_out) break;
+        // the maps are written from here on: an asynchronous copy of the previous run's maps
+        // (sm_download_disp_async) must be done reading them
+        if (c->copy_pending && (e = hipStreamWaitEvent(c->st, c->ev_copy, 0)) != hipSuccess) {
+            s_out = hip_fail(c, e, "hipStreamWaitEvent (async map copy)");
+            break;
+        }
         if (ns > 1 && (e = hipEventRecord(c->xev[1 + k % 8], c->st)) != hipSuccess) {
             s_out = hip_fail(c, e, "hipEventRecord (group CBCA done)");
             break;
@@ -1320,6 +1350,24 @@ sm_status sm_download_disp(sm_ctx* c, int32_t n, int16_t* disp_out) {
     if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
     HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDefault, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
+    return SM_OK;
+}
+
+sm_status sm_download_disp_async(sm_ctx* c, int32_t n, int16_t* disp_out) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!disp_out || n < 1 || n > c->cap) return fail(c, SM_EINVAL, "bad arguments");
+    if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
+    if (!c->cst) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_run, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
+    }
+    HIP_TRY(c, hipEventRecord(c->ev_run, c->st));
+    HIP_TRY(c, hipStreamWaitEvent(c->cst, c->ev_run, 0));
+    HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDefault, c->cst));
+    HIP_TRY(c, hipEventRecord(c->ev_copy, c->cst));
+    c->copy_pending = true;
     return SM_OK;
 }
 
@@ -1370,6 +1418,10 @@ sm_status sm_synchronize(sm_ctx* c) {
     sm_status s = check(c);
     if (s) return s;
     HIP_TRY(c, hipStreamSynchronize(c->st));
+    if (c->cst) {
+        HIP_TRY(c, hipStreamSynchronize(c->cst));
+        c->copy_pending = false;
+    }
     return SM_OK;
 }
 

@@ -330,6 +330,15 @@ class StereoBatch:
         _capi.check(self._lib, self._ctx, self._lib.sm_get_disp(self._ctx, view, _capi.ptr(out)), "get_disp")
         return out
 
+    def download_async(self, out):
+        """sm_download_disp_async: the n maps into `out` (page-locked host memory, e.g. a
+        pin_memory torch tensor's numpy view, or device memory) on the copy stream; complete after
+        synchronize().  The next run's map-writing kernels wait for the copy."""
+        dst = C.c_void_p(out.data_ptr()) if _is_device_tensor(out) or type(out).__module__.startswith("torch") \
+            else _capi.ptr(out)
+        _capi.check(self._lib, self._ctx, self._lib.sm_download_disp_async(self._ctx, self.n, dst), "download_async")
+        return out
+
     def synchronize(self):
         _capi.check(self._lib, self._ctx, self._lib.sm_synchronize(self._ctx), "sync")
 

@@ -172,3 +172,25 @@ def test_runner_rccl_hd1080_rank_shard():
         np.testing.assert_array_equal(got, sb.run(0.3))
     finally:
         sb.close()
+
+
+def test_async_map_download_overlaps_next_run(oracle):
+    """sm_download_disp_async: the copy of run k's maps (copy stream) must not see run k+1's maps
+    -- run k+1's map-writing kernels wait for it -- and must be complete after synchronize()."""
+    import torch
+    H, W, md, n = 29, 61, 19, 3
+    a = S.make_batch(n, H, W, md + 1, first_index=460)
+    b = S.make_batch(n, H, W, md + 1, first_index=470)
+    sb = StereoBatch(md, H, W, n, device=0)
+    try:
+        bufs = [torch.empty((n, H, W), dtype=torch.int16, pin_memory=True).numpy() for _ in range(2)]
+        for rnd in range(2):
+            for i, bt in enumerate((a, b)):
+                sb.upload(*(bt[k] for k in KEYS))
+                sb.run(0.3, download=False)
+                sb.download_async(bufs[i])
+            sb.synchronize()
+            np.testing.assert_array_equal(bufs[0], _oracle_maps(oracle, a, H, W, md), err_msg=f"round {rnd}, batch a")
+            np.testing.assert_array_equal(bufs[1], _oracle_maps(oracle, b, H, W, md), err_msg=f"round {rnd}, batch b")
+    finally:
+        sb.close()

@@ -439,3 +439,50 @@ def test_fuse_norm_scan_batch_and_right_view(oracle):
     for i in range(n):
         pair = {k: b[k][i] for k in ("lbgr", "rbgr", "lgray", "rgray")}
         np.testing.assert_array_equal(disp[i], oracle.run_ex(pair, cfg)["disp"])
+
+
+@pytest.mark.parametrize("H,W,md,iters,fuse,refine", [
+    (200, 90, 63, 2, 1, 0), (200, 90, 63, 1, 1, 0), (160, 150, 127, 3, 1, 0), (150, 120, 63, 4, 1, 0),
+    (130, 110, 63, 4, 0, 0), (90, 140, 191, 2, 1, 1), (70, 75, 255, 2, 0, 1), (40, 300, 63, 2, 1, 0)])
+def test_fast_sweeps_lag34(oracle, H, W, md, iters, fuse, refine):
+    """The dedicated CBCA sweeps at the reference's lag (34) and whole 64-disparity chunks: the V
+    NORM_SCAN sweep (NsV: iteration 0 without the tiny-dividend test, later iterations with it)
+    and the H normalising sweep (HNorm, with and without SolveAll's scale), both views, lines
+    long enough for steady tiles and lines shorter than the lag.  The aggregated volume
+    (cbca_core, cpp:5585-5666) and the maps must equal the oracle's bit for bit."""
+    pair = S.make_pair(H, W, md + 1, 960 + iters * 7 + md)
+    cfg = oracle.config(H, W, md, cbca_iters=iters, do_refine=refine)
+    lib = _capi.load()
+    p = _capi.default_params(md, H, W, cbca_iterations=iters, fuse_norm_scan=fuse, keep_final_volume=1,
+                             do_refine=refine)
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        a = {k: np.ascontiguousarray(pair[k]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        _capi.check(lib, ctx, lib.sm_set_images(ctx, _capi.ptr(a["lbgr"]), _capi.ptr(a["rbgr"]), W * 3,
+                                                _capi.ptr(a["lgray"]), _capi.ptr(a["rgray"]), W))
+        _capi.check(lib, ctx, lib.sm_cost_calculate(ctx))
+        ref = oracle.run_ex(pair, cfg, dumps=("agg", "agg_right") if refine else ("agg",))
+        for view in ((0, 1) if refine else (0,)):
+            got = np.empty((H, W, md + 1), np.float32)
+            _capi.check(lib, ctx, lib.sm_get_volume(ctx, view, _capi.ptr(got)))
+            np.testing.assert_array_equal(bits(got), bits(ref["agg" if view == 0 else "agg_right"]), err_msg=f"view {view}")
+        _capi.check(lib, ctx, lib.sm_solve_all(ctx, 1, 0.3))
+        dp = np.empty((H, W), np.int16)
+        _capi.check(lib, ctx, lib.sm_disp_optimize(ctx, _capi.ptr(dp)))
+        if refine:
+            _capi.check(lib, ctx, lib.sm_refine(ctx, _capi.ptr(dp)))
+        np.testing.assert_array_equal(dp, ref["disp"])
+    finally:
+        lib.sm_destroy(ctx)
+    # the batched path fuses SolveAll into the last (H) normalising sweep
+    sb = StereoBatch(md, H, W, 2, cbca_iterations=iters, fuse_norm_scan=fuse, do_refine=refine)
+    try:
+        b = S.make_batch(2, H, W, md + 1, first_index=990 + iters)
+        sb.upload(b["lbgr"], b["rbgr"], b["lgray"], b["rgray"])
+        got = sb.run(0.3)
+        for i in range(2):
+            pr = {k: b[k][i] for k in ("lbgr", "rbgr", "lgray", "rgray")}
+            np.testing.assert_array_equal(got[i], oracle.run_ex(pr, cfg)["disp"], err_msg=f"pair {i}")
+    finally:
+        sb.close()

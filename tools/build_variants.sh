@@ -21,6 +21,8 @@ OBJS="build/sm_kernels.o build/sm_cbca.o build/sm_sgm.o build/sm_refine.o build/
 for o in build/var/${SRC}__*.o; do
   name=${o#build/var/${SRC}__}; name=${name%.o}
   objs=${OBJS/build\/$SRC.o/$o}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/abvar/libsm_hip_$name.so $objs
+  # (linked to a temporary name and renamed: a gpurun snapshot never sees a half-written library)
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/abvar/.tmp_$name.so $objs
+  mv ../../tools/abvar/.tmp_$name.so ../../tools/abvar/libsm_hip_$name.so
   echo "built tools/abvar/libsm_hip_$name.so"
 done

@@ -14,8 +14,9 @@ grep -q " passed" $O/pytest_ns.log && ! grep -qE "FAILED|ERROR|Timeout" $O/pytes
 timeout -k 10 900 $PT -m gpu tests > $O/pytest_gpu.log 2>&1 ; tail -3 $O/pytest_gpu.log; grep -E "FAILED|ERROR" $O/pytest_gpu.log | head -20
 grep -q " passed" $O/pytest_gpu.log && ! grep -qE "FAILED|ERROR|Timeout" $O/pytest_gpu.log || exit 1
 A="timeout -k 10 400 python -u tools/ab_inproc.py"
-$A --workload fullres --rounds 5 --steps 3 --copies 2 --kernels cbca,step base gen nohn > $O/ab_fr.txt 2>&1 && tail -4 $O/ab_fr.txt \
+$A --workload fullres --rounds 5 --steps 3 --copies 2 --kernels cbca,cost,step base gen nohn expskip > $O/ab_fr.txt 2>&1 && tail -4 $O/ab_fr.txt \
  && $A --workload hd --rounds 4 --steps 2 --copies 1 --kernels cbca,step base gen nohn > $O/ab_hd.txt 2>&1 && tail -4 $O/ab_hd.txt \
+ && $A --workload teddy --rounds 6 --steps 10 --copies 2 --kernels cbca,step base base:fuse_norm_scan=1 gen > $O/ab_teddy.txt 2>&1 && tail -4 $O/ab_teddy.txt \
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log \
  && timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && cat $O/bench.json \
  && cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/kt -o kt -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/$O/kt.log 2>&1 \

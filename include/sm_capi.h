@@ -122,8 +122,10 @@ typedef struct sm_params {
                                   * group k + 1 starting once group k's CBCA is done */
     int32_t fuse_norm_scan;      /* CBCA: iteration k's normalising sweep fused with iteration k+1's
                                   * scan (one sweep, 8 B per element less): 1 = always, 0 = never,
-                                  * -1 (default) = when a pair's volume is >= 256 MiB (measured
-                                  * faster at 1080p and full resolution, slower at Teddy size) */
+                                  * -1 (default) = when the dedicated sweep for the reference's lag
+                                  * applies (arm length 34, D % 64 == 0) or a pair's volume is
+                                  * >= 256 MiB (measured faster there; the generic fused sweep is
+                                  * slower at Teddy size) */
     /* alternative aggregators */
     float gf_eps;                /* gf_eps[0] = 0.0001 (h:298; radius gf_r[0] = 9, h:297) */
     int32_t gf_mode;             /* sm_gf_mode: SM_GF_XIMGPROC (default, the shipped build) or SM_GF_MY_GUIDE */

@@ -55,6 +55,8 @@ struct sm_ctx {
     float* vm0 = nullptr;       // [cap][npix][D]
     float* vm1 = nullptr;       // [cap][npix][D] (right view, optional)
     float* acc = nullptr;       // [cap][npix][D]
+    float* ck = nullptr;        // [cap][ck_pair]: checkpointed SGM path pairs (k_sgm_ck)
+    size_t ck_pair = 0;         // floats per pair: lines x segments x D of the longer direction
     int16_t* disp = nullptr;    // [cap][npix] DP[0]
     int16_t* disp1 = nullptr;   // [cap][npix] DP[1] (do_refine)
     int16_t* disp_tmp = nullptr;// [cap][npix] refine ping-pong (do_refine)
@@ -308,7 +310,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 }
 
 void free_all(sm_ctx* c) {
-    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->disp,
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->ck, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
                     c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
                     c->nl_table, c->nl_val, c->nl_oup, c->nl_ofin, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->nl_walk,
@@ -368,6 +370,7 @@ struct Bufs {
     float* vm0;
     float* vm1;
     float* acc;
+    float* ck;
     int16_t* disp;
     int16_t* disp1;
     int16_t* disp_tmp;
@@ -390,6 +393,7 @@ Bufs at(const sm_ctx* c, int off) {
     b.vm0 = c->vm0 + o * nv;
     b.vm1 = c->vm1 ? c->vm1 + o * nv : nullptr;
     b.acc = c->acc ? c->acc + o * nv : nullptr;
+    b.ck = c->ck ? c->ck + o * c->ck_pair : nullptr;
     b.disp = c->disp + o * np;
     b.disp1 = c->disp1 ? c->disp1 + o * np : nullptr;
     b.disp_tmp = c->disp_tmp ? c->disp_tmp + o * np : nullptr;
@@ -703,6 +707,30 @@ sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
         a.redu = p.sgm_redu_coeff;
         a.keep_final = p.keep_final_volume;
         a.signed_costs = p.aggregation == SM_AGG_GF;   // the guided filter's output can be < 0
+        if (B.ck) {
+            // checkpointed pairs (0, 1) and (2, 3): 4 + 8 + 4 + 8 B per element (+ 4 / S for
+            // the checkpoints each way) instead of 8 + 12 + 12 + 8
+            a.ck = B.ck;
+            const double ckb = 4.0 / sm::sgm_ck_seg();
+            const double nv = (double)n * c->nvol;
+            struct Pass { int path, mode; const char* name; double per; };
+            const Pass passes[4] = {
+                {0, sm::CK_A, "sgm_ck_a01", 4.0 + ckb},
+                {0, sm::CK_B, "sgm_ck_b01", 8.0 + ckb},
+                {2, sm::CK_A, "sgm_ck_a23", 4.0 + ckb},
+                {2, sm::CK_B | sm::SGM_LAST, "sgm_last_wta", 8.0 + ckb + (p.keep_final_volume ? 4.0 : 0)}};
+            for (const Pass& ps : passes) {
+                a.rv = RV[ps.path];
+                a.ru = RU[ps.path];
+                a.dir = ps.path;
+                a.dir2 = ps.path + 1;
+                const double bytes = nv * ps.per + ((ps.mode & sm::SGM_LAST) ? (double)n * c->npix * 2 : 0);
+                const std::string name = std::string(ps.name) + sfx;
+                sm_status s = timed(c, name.c_str(), bytes, [&] { sm::launch_sgm_ck(a, ps.mode, n, c->st); });
+                if (s) return s;
+            }
+            return SM_OK;
+        }
         for (int i = 0; i < p.sgm_paths; i++) {
             a.rv = RV[i];
             a.ru = RU[i];
@@ -931,6 +959,12 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->vm1, cap * c->nvol + vpad))) return s;
     if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
         if ((s = dalloc(c, &c->acc, cap * c->nvol + vpad))) return s;
+    if (p->optimization == SM_OPT_SGM && sm::sgm_ck_ok(p->num_disparities, p->sgm_paths)) {
+        const size_t S = (size_t)sm::sgm_ck_seg(), H = (size_t)p->rows, W = (size_t)p->cols;
+        const size_t lines_x_segs = std::max(H * ((W + S - 1) / S), W * ((H + S - 1) / S));
+        c->ck_pair = lines_x_segs * (size_t)p->num_disparities;
+        if ((s = dalloc(c, &c->ck, cap * c->ck_pair))) return s;
+    }
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
     if ((s = dalloc(c, &c->dummy, 64))) return s;
     if ((s = dalloc(c, &c->flags, cap * c->npix))) return s;
@@ -983,9 +1017,12 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
                 (void*)c->acc, (void*)c->arms, (void*)c->code, (void*)c->gx, (void*)c->px);
     build_luts(c);
     {
-        // auto: the fused sweep wins where a pair's volume is large (full resolution: v_norm +
-        // v_scan 12.2 -> 11.3 ms; 1080p 16.2 -> 16.0 ms) and loses at Teddy size (0.79 -> 0.82 ms)
-        c->fuse_norm_scan = p->fuse_norm_scan == 1 || (p->fuse_norm_scan == -1 && c->nvol * 4 >= ((size_t)1 << 28));
+        // auto: the generic fused sweep wins where a pair's volume is large (full resolution:
+        // v_norm + v_scan 12.2 -> 11.3 ms; 1080p 16.2 -> 16.0 ms) and loses at Teddy size (0.79 ->
+        // 0.82 ms); the dedicated sweep at the reference's lag (NsV, D % 64 == 0) wins at every
+        // size (Teddy x16: 0.765 -> 0.692 ms, profiles/r4b/ab_teddy.txt)
+        const bool nsv = cbca_lag(*p) == 34 && p->num_disparities % 64 == 0;
+        c->fuse_norm_scan = p->fuse_norm_scan == 1 || (p->fuse_norm_scan == -1 && (nsv || c->nvol * 4 >= ((size_t)1 << 28)));
         c->sub_batch = p->sub_batch;
         c->nstreams = p->num_streams < 1 ? 1 : p->num_streams;
         for (int i = 0; i + 1 < c->nstreams; i++) HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking));

@@ -219,11 +219,13 @@ struct CbLine {
         const int range = hi < 0 ? 0 : ((hi > 0 || lo > 0x7fffffffu) ? 0x7fffffff : (int)lo);
         return buf_rsrc(base, range);
     }
-    __device__ __forceinline__ void store_tile(const __amdgpu_buffer_rsrc_t& r, int k, float v) const {
+    // `in` false: an out-of-range offset (the store is dropped), so that guarded and unguarded
+    // tiles issue the same vector-memory sequence and the loops' vmcnt waits stay exact
+    __device__ __forceinline__ void store_tile(const __amdgpu_buffer_rsrc_t& r, int k, float v, bool in = true) const {
         if (FULL)
-            buf_st(r, xo[k], 0, v);
+            buf_st(r, in ? xo[k] : 0x80000000u, 0, v);
         else
-            buf_st(r, ov, (uint32_t)k * vsb, v);
+            buf_st(r, in ? ov : 0x80000000u, (uint32_t)k * vsb, v);
     }
 
     // Tile loads: positions past the line end read the next line (or 0 past the allocation);
@@ -382,7 +384,7 @@ struct CbLine {
         if (MODE == CB_SCAN) {
 #pragma unroll
             for (int k = 0; k < T; k++)
-                if (!GUARD || (unsigned)(i0 + k) < (unsigned)len) store_tile(ob, k, shv[k] - stv[k]);
+                store_tile(ob, k, shv[k] - stv[k], !GUARD || (unsigned)(i0 + k) < (unsigned)len);
         } else {
             // genfinalVm_cbca's division (cpp:3969-3992) by the integer area, through div_area
             // (sm_device.h); tiles holding a dividend below its proven range redo the IEEE
@@ -407,7 +409,7 @@ struct CbLine {
 #pragma unroll
             for (int k = 0; k < T; k++) {
                 if (MODE == CB_NORM) {
-                    if (!GUARD || (unsigned)(i0 + k) < (unsigned)len) store_tile(ob, k, finish_norm(qv[k]));
+                    store_tile(ob, k, finish_norm(qv[k]), !GUARD || (unsigned)(i0 + k) < (unsigned)len);
                 } else {
                     float y = qv[k];                              // final value of iteration k at i
                     if (GUARD) y = (i0 + k >= 0) ? y : 0.f;       // nothing accumulates before the line
@@ -429,7 +431,7 @@ struct CbLine {
             const __amdgpu_buffer_rsrc_t ob2 = tile_rsrc(i20);
 #pragma unroll
             for (int k = 0; k < T; k++)
-                if (!GUARD || (unsigned)(i20 + k) < (unsigned)len) store_tile(ob2, k, s2h[k] - s2t[k]);
+                store_tile(ob2, k, s2h[k] - s2t[k], !GUARD || (unsigned)(i20 + k) < (unsigned)len);
         }
         ws = (ws + T == ring) ? 0 : ws + T;
         wrs = (wrs + T >= cbca_win_ring(T)) ? wrs + T - cbca_win_ring(T) : wrs + T;
@@ -651,8 +653,12 @@ struct NsV {
             s2t[k] = rd<0, float>(sp, o2, k);
         }
 #pragma unroll
-        for (int k = 0; k < T; k++)
-            if (!GUARD || (unsigned)(j0 - 2 * LAG + k) < (unsigned)len) store(ob2, k, s2h[k] - s2t[k]);
+        for (int k = 0; k < T; k++) {
+            // (outside the line: an out-of-range offset, so that both tile forms issue the same
+            // vector-memory sequence and the loop's vmcnt waits stay exact)
+            const bool in = !GUARD || (unsigned)(j0 - 2 * LAG + k) < (unsigned)len;
+            buf_st(ob2, in ? xo[k] : 0x80000000u, 0, s2h[k] - s2t[k]);
+        }
         ws = ws + T == R ? 0 : ws + T;
     }
 
@@ -731,24 +737,25 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
     const int nst = L.len + 2 * L_t::LAG;
     typename L_t::Tile ta, tb, tc;
     static_assert(L_t::NH == 6, "the loop below is written for six tiles");
+    // (the scheduler must not interleave the two prologue tiles' loads, and the loop has no exit
+    // but its condition: otherwise the compiler's vmcnt waits at the loop head are conservative
+    // and every sixth tile waits for the next tile's loads too.  Up to five tiles past the line
+    // end run: their loads read the zeroed tail pads, their stores are out of range.)
     L.load(ta);
+    __builtin_amdgcn_sched_barrier(0);
     L.load(tb);
+    __builtin_amdgcn_sched_barrier(0);
     for (int j0 = 0; j0 < nst; j0 += 6 * T) {
         L.load(tc);
         L.template process<0>(ta, j0);
-        if (j0 + T >= nst) break;
         L.load(ta);
         L.template process<1>(tb, j0 + T);
-        if (j0 + 2 * T >= nst) break;
         L.load(tb);
         L.template process<2>(tc, j0 + 2 * T);
-        if (j0 + 3 * T >= nst) break;
         L.load(tc);
         L.template process<3>(ta, j0 + 3 * T);
-        if (j0 + 4 * T >= nst) break;
         L.load(ta);
         L.template process<4>(tb, j0 + 4 * T);
-        if (j0 + 5 * T >= nst) break;
         L.load(tb);
         L.template process<5>(tc, j0 + 5 * T);
     }
@@ -760,270 +767,6 @@ template <bool RV, bool CHECK>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_cbca_nsv(const CbcaArgs a) {
     extern __shared__ float smem[];
     cbca_run_nsv<RV, CHECK>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
-}
-
-// ---------------------------------------------------------------------------------------------
-// H NORM at the reference's lag: the last CBCA pass (iteration 1's H normalisation, with
-// SolveAll's weight fused), the same budget measures as NsV: ring reads with the tile position in
-// the immediate offset against a mirrored ring (T = 5: the S ring, the u16 area ring, their
-// mirrors and the staged arm words fit five waves per CU), loads through fixed per-line resources
-// with a uniform scalar offset, and the tiny-dividend test only when the host cannot rule it out.
-// Own arm pairs: staged in LDS per tile, broadcast reads; the other image's pairs: the mirrored
-// span ring of the generic H sweep.
-#ifndef SM_CB_T_HN
-#define SM_CB_T_HN 5
-#endif
-#ifndef SM_CB_PF_HN
-#define SM_CB_PF_HN 4
-#endif
-#ifndef SM_CB_HN
-#define SM_CB_HN 1   // 0: the generic H normalising sweep (A/B builds)
-#endif
-constexpr int cbca_hn_ring() { return (2 * NSV_LAG + SM_CB_T_HN + 1 + SM_CB_T_HN - 1) / SM_CB_T_HN * SM_CB_T_HN; }
-constexpr int cbca_hn_phys() { return cbca_hn_ring() + SM_CB_T_HN - 1; }
-constexpr int cbca_hn_wr() { return 63 + SM_CB_T_HN; }
-// dynamic LDS in 4-byte words: r1 (P x 64 floats), ra (P x 64 u16), own words (2 x T), span rings (2 x 2 WR)
-constexpr int cbca_hn_smem_words() { return cbca_hn_phys() * 96 + 2 * SM_CB_T_HN + 4 * cbca_hn_wr(); }
-
-template <bool RV, bool SCALE, bool CHECK>
-struct HNorm {
-    static constexpr int T = SM_CB_T_HN;
-    static constexpr int PF = SM_CB_PF_HN;
-    static constexpr int LAG = NSV_LAG;
-    static constexpr int R = cbca_hn_ring();
-    static constexpr int P = cbca_hn_phys();
-    static constexpr int WR = cbca_hn_wr();
-
-    struct Tile {
-        float x[T];           // vm at positions j0 .. j0+T-1
-        uint32_t a0[2];       // lane k < T: own pair, set 0 at j0 + k - LAG, set 1 at j0 + k
-        uint32_t a1w[2];      // lane k < T: the span ring's k-th new word of each set
-    };
-
-    __amdgpu_buffer_rsrc_t rx;   // the line from position 0 (loads)
-    __amdgpu_buffer_rsrc_t ro;   // the line from position -LAG (stores of outputs i = j - LAG)
-    __amdgpu_buffer_rsrc_t A0r[2], A1r[2];   // own / other arm plane, from `pad` words before the line
-    uint32_t sld;             // byte offset of the next tile to load (jld * vsb)
-    uint32_t sst;             // byte offset of the next tile's outputs in ro (j0 * vsb)
-    uint32_t ald;             // (jld + pad) * 4: the next tile's set-1 own / span word offset
-    int jld;                  // first position of the next tile to load
-    uint32_t vsb;
-    uint32_t xo[T];
-    uint32_t aown;            // lane < T: lane * 4, else out of range
-    int c64, lane, len, padw;
-    uint32_t* wown;
-    uint32_t* wspan;
-    uint32_t owa;             // LDS address of wown (a VGPR: the broadcast reads' base)
-    uint32_t spa;             // LDS address of this lane's span word at wrs = 0, k = 0 (set 0)
-    float* r1;
-    uint16_t* ra;
-    uint32_t o1, oa;
-    uint32_t RR;
-    float S1, scale;
-    uint32_t Acc;
-    int ws, wrs;
-
-    __device__ __forceinline__ void load(Tile& t) {
-#pragma unroll
-        for (int k = 0; k < T; k++) t.x[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, (int)xo[k], (int)sld, 2));
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const int base = jld - (s == 0 ? LAG : 0);
-            t.a0[s] = __builtin_amdgcn_raw_buffer_load_b32(A0r[s], (int)aown, (int)(ald - (s == 0 ? LAG * 4u : 0u)), 0);
-            // the tile's T new span words q0 + 63 .. q0 + 62 + T: 0 outside the line (the
-            // reference's zeroed intersection, cpp:2794-2845)
-            const int qn = (RV ? base + c64 : base - c64 - 63) + 63 + lane;
-            t.a1w[s] = __builtin_amdgcn_raw_buffer_load_b32(A1r[s], (lane < T && (unsigned)qn < (unsigned)len) ? (uint32_t)(qn + padw) * 4u : 0x80000000u, 0, 0);
-        }
-        sld += (uint32_t)T * vsb;
-        ald += (uint32_t)T * 4u;
-        jld += T;
-    }
-
-    __device__ __forceinline__ uint32_t slots(uint32_t p, uint32_t cc) const {
-        const us2 q = __builtin_bit_cast(us2, p) * us2{0xffff, 1} + __builtin_bit_cast(us2, cc);
-        const us2 w = q + __builtin_bit_cast(us2, RR);
-        return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, w));
-    }
-    template <int H_, typename E>
-    __device__ __forceinline__ E rd(uint32_t sp, uint32_t o, int k) const {
-        typedef __attribute__((address_space(3))) const E lds_e;
-        return ((lds_e*)(size_t)mad_u32_u16<H_>(sp, 64u * (uint32_t)sizeof(E), o))[k * 64];
-    }
-
-    template <bool GUARD>
-    __device__ __forceinline__ void tile(const Tile& t, int j0) {
-        // stage the tile's arm words: own words (broadcast reads), the span ring's new words
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            if (lane < T) wown[s * T + lane] = t.a0[s];
-            uint32_t* sp = wspan + s * 2 * WR;
-            const int w = wrs + 63 + lane;   // < 2 WR
-            const int i = w >= WR ? w - WR : w;
-            if (lane < T) {
-                sp[i] = t.a1w[s];
-                sp[i + WR] = t.a1w[s];
-            }
-        }
-        const int C = ws - LAG < 0 ? ws - LAG + R : ws - LAG;
-        const uint32_t cc = ((uint32_t)(C - 1) & 0xffffu) | ((uint32_t)C << 16);
-        float* w1 = r1 + ws * 64 + lane;
-        uint16_t* wa = ra + ws * 64 + lane;
-        // arm words by integer LDS addresses, so that the tile position and the set are immediate
-        // offsets of one base (read2 pairs of set 0 / set 1)
-        typedef __attribute__((address_space(3))) const uint32_t lds_u;
-        const lds_u* ow = (const lds_u*)(size_t)owa;
-        const lds_u* sw = (const lds_u*)(size_t)(spa + (uint32_t)wrs * 4u);
-        uint32_t pi[T];
-        float s1v[T];
-        uint16_t acv[T];
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            S1 = S1 + t.x[k];
-            s1v[k] = S1;
-            w1[k * 64] = S1;
-            pi[k] = pkmin(ow[k], sw[k]);
-            const uint32_t pp = pkmin(ow[T + k], sw[2 * WR + k]);
-            Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
-            acv[k] = (uint16_t)Acc;
-            wa[k * 64] = acv[k];
-        }
-        if (ws == 0) {   // the mirror of slots 0 .. T-2
-#pragma unroll
-            for (int k = 0; k < T - 1; k++) {
-                r1[(R + k) * 64 + lane] = s1v[k];
-                ra[(R + k) * 64 + lane] = acv[k];
-            }
-        }
-        float shv[T], stv[T], dv[T], qv[T];
-        uint32_t ahv[T], atv[T];
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            const uint32_t sp = slots(pi[k], cc);
-            shv[k] = rd<1, float>(sp, o1, k);
-            stv[k] = rd<0, float>(sp, o1, k);
-            ahv[k] = rd<1, uint16_t>(sp, oa, k);
-            atv[k] = rd<0, uint16_t>(sp, oa, k);
-        }
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            dv[k] = shv[k] - stv[k];
-            qv[k] = div_area(dv[k], (ahv[k] - atv[k]) & 0xffffu);
-        }
-        if constexpr (CHECK) {
-            uint32_t tmin = 0xffffffffu;
-#pragma unroll
-            for (int k = 0; k < T; k++) tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
-            if (__ballot(tmin < 0x087fffffu)) {
-#pragma unroll
-                for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)((ahv[k] - atv[k]) & 0xffffu);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            // SolveAll's `sum = 0; sum += w * v` (cpp:2189-2201): 0 + x == x (no CBCA value is -0)
-            const float v = SCALE ? scale * qv[k] : qv[k];
-            if (!GUARD || (unsigned)(j0 - LAG + k) < (unsigned)len) buf_st(ro, xo[k], sst, v);
-        }
-        sst += (uint32_t)T * vsb;
-        ws = ws + T == R ? 0 : ws + T;
-        wrs = wrs + T >= WR ? wrs + T - WR : wrs + T;
-    }
-
-    __device__ __forceinline__ void process(const Tile& t, int j0) {
-        if (j0 - LAG >= 0 && j0 + T - 1 - LAG < len)
-            tile<false>(t, j0);
-        else
-            tile<true>(t, j0);
-    }
-};
-
-template <bool RV, bool SCALE, bool CHECK>
-__device__ __forceinline__ void cbca_run_hn(const CbcaArgs& a, const int blk, float* smem) {
-    using L_t = HNorm<RV, SCALE, CHECK>;
-    constexpr int T = L_t::T;
-    L_t L;
-    L.lane = (int)threadIdx.x;
-    const int nchunks = a.D / 64;
-    const int per_pair = a.H * nchunks;
-    const int b = blk / per_pair;
-    const int lc = blk - b * per_pair;
-    const int v = lc / nchunks, chunk = lc - v * nchunks;
-    const size_t npix = (size_t)a.H * a.W;
-    const size_t first_pix = (size_t)v * a.W;
-    L.vsb = (uint32_t)a.D * 4u;
-    const char* xline = (const char*)(a.vm + ((size_t)b * npix + first_pix) * a.D + (size_t)chunk * 64);
-    L.rx = buf_rsrc(xline);
-    L.ro = buf_rsrc(xline - (long)L_t::LAG * (long)L.vsb);
-#pragma unroll
-    for (int k = 0; k < T; k++) L.xo[k] = (uint32_t)L.lane * 4u + (uint32_t)k * L.vsb;
-    L.sld = 0;
-    L.sst = 0;
-    L.jld = 0;
-    L.len = a.W;
-    L.c64 = chunk * 64;
-    L.padw = L_t::LAG + 64;   // words before the line a resource starts at (covered by the front pad)
-    L.ald = (uint32_t)L.padw * 4u;
-    const int own = RV ? 2 : 0, other = RV ? 0 : 2;
-    const uint32_t* planeL = a.arms + ((size_t)b * 4) * npix + first_pix;
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-        const int pl = s == 0 ? 0 : 1;   // H sweeps: pass pair = (L | R) plane 0, perpendicular = plane 1
-        L.A0r[s] = buf_rsrc(planeL + (size_t)(own + pl) * npix - L.padw, 0x7fffffff);
-        L.A1r[s] = buf_rsrc(planeL + (size_t)(other + pl) * npix - L.padw, 0x7fffffff);
-    }
-    L.aown = L.lane < T ? (uint32_t)L.lane * 4u : 0x80000000u;
-    L.r1 = smem;
-    L.ra = (uint16_t*)(smem + L_t::P * 64);
-    L.wown = (uint32_t*)(smem + L_t::P * 96);
-    L.wspan = L.wown + 2 * T;
-    {
-        typedef __attribute__((address_space(3))) char lds_c;
-        L.o1 = (uint32_t)(size_t)(lds_c*)L.r1 + 4u * (uint32_t)L.lane;
-        L.oa = (uint32_t)(size_t)(lds_c*)L.ra + 2u * (uint32_t)L.lane;
-        L.owa = (uint32_t)(size_t)(lds_c*)L.wown;
-        asm volatile("" : "+v"(L.owa));   // keep the broadcast reads' base in one VGPR
-        // lane d pairs with span word k + 63 - d (left view) / k + d (right view)
-        L.spa = (uint32_t)(size_t)(lds_c*)L.wspan + 4u * (uint32_t)(RV ? L.lane : 63 - L.lane);
-    }
-    L.RR = (uint32_t)L_t::R | ((uint32_t)(65536 - L_t::R) << 16);
-    L.scale = a.scale;
-    for (int w = L.lane; w < cbca_hn_smem_words(); w += 64) smem[w] = 0.f;
-    __syncthreads();
-    L.S1 = 0.f;
-    L.Acc = 0;
-    L.ws = 0;
-    L.wrs = 0;
-    {   // span-ring prologue: the first tile's words q0 .. q0 + 62 of both sets
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const int base = s == 0 ? -L_t::LAG : 0;
-            const int q = (RV ? base + L.c64 : base - L.c64 - 63) + L.lane;
-            const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(L.A1r[s], (L.lane < 63 && (unsigned)q < (unsigned)L.len) ? (uint32_t)(q + L.padw) * 4u : 0x80000000u, 0, 0);
-            if (L.lane < 63) {
-                L.wspan[s * 2 * L_t::WR + L.lane] = w;
-                L.wspan[s * 2 * L_t::WR + L.lane + L_t::WR] = w;
-            }
-        }
-    }
-    const int nst = L.len + L_t::LAG;
-    typename L_t::Tile tt[L_t::PF + 1];
-#pragma unroll
-    for (int i = 0; i < L_t::PF; i++) L.load(tt[i]);
-    for (int j0 = 0; j0 < nst; j0 += (L_t::PF + 1) * T) {
-#pragma unroll
-        for (int i = 0; i <= L_t::PF; i++) {
-            if (j0 + i * T >= nst) break;
-            L.load(tt[(i + L_t::PF) % (L_t::PF + 1)]);
-            L.process(tt[i], j0 + i * T);
-        }
-    }
-}
-
-template <bool RV, bool SCALE, bool CHECK>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_cbca_hn(const CbcaArgs a) {
-    extern __shared__ float smem[];
-    cbca_run_hn<RV, SCALE, CHECK>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
 }
 
 template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int LAGC>
@@ -1129,42 +872,46 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     }
     const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
     typename CbLine<HORIZ, MODE, FULL, SCALE, RV, LAGC>::Tile ta, tb, tc, td;
+    // The loops have no exit but their condition and the prologue's tiles are loaded in order:
+    // otherwise the compiler's vmcnt waits at the loop head are conservative and the first tile
+    // of every trip waits for later tiles' loads too.  Tiles past the line end run (up to PF of
+    // them): their loads are bounded or read the next line, their stores are out of range.
     if constexpr (CbCfg<HORIZ, MODE>::PF == 3) {
         L.load(ta, 0);
+        __builtin_amdgcn_sched_barrier(0);
         L.load(tb, T);
+        __builtin_amdgcn_sched_barrier(0);
         L.load(tc, 2 * T);
+        __builtin_amdgcn_sched_barrier(0);
         for (int j0 = 0; j0 < nst; j0 += 4 * T) {
             L.load(td, j0 + 3 * T);
             L.template process<0>(ta, j0);
-            if (j0 + T >= nst) break;
             L.load(ta, j0 + 4 * T);
             L.template process<1>(tb, j0 + T);
-            if (j0 + 2 * T >= nst) break;
             L.load(tb, j0 + 5 * T);
             L.template process<2>(tc, j0 + 2 * T);
-            if (j0 + 3 * T >= nst) break;
             L.load(tc, j0 + 6 * T);
             L.template process<3>(td, j0 + 3 * T);
         }
     } else if constexpr (CbCfg<HORIZ, MODE>::PF == 2) {
         L.load(ta, 0);
+        __builtin_amdgcn_sched_barrier(0);
         L.load(tb, T);
+        __builtin_amdgcn_sched_barrier(0);
         for (int j0 = 0; j0 < nst; j0 += 3 * T) {
             L.load(tc, j0 + 2 * T);
             L.process(ta, j0);
-            if (j0 + T >= nst) break;
             L.load(ta, j0 + 3 * T);
             L.process(tb, j0 + T);
-            if (j0 + 2 * T >= nst) break;
             L.load(tb, j0 + 4 * T);
             L.process(tc, j0 + 2 * T);
         }
     } else {
         L.load(ta, 0);
+        __builtin_amdgcn_sched_barrier(0);
         for (int j0 = 0; j0 < nst; j0 += 2 * T) {
             L.load(tb, j0 + T);
             L.process(ta, j0);
-            if (j0 + T >= nst) break;
             L.load(ta, j0 + 2 * T);
             L.process(tb, j0 + T);
         }
@@ -1221,29 +968,8 @@ static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
     launch_lag<HORIZ, MODE, SCALE, 0>(a, n, st);
 }
 
-template <bool RV, bool SCALE>
-static void launch_hn(const CbcaArgs& a, int n, hipStream_t st) {
-    dim3 grid(a.H * (a.D / 64) * n), block(64);
-    const size_t shm = 4 * (size_t)cbca_hn_smem_words();
-    if (a.div_safe) hipLaunchKernelGGL((k_cbca_hn<RV, SCALE, false>), grid, block, shm, st, a);
-    else hipLaunchKernelGGL((k_cbca_hn<RV, SCALE, true>), grid, block, shm, st, a);
-}
-
 template <bool HORIZ, int MODE>
 static void launch_mode(const CbcaArgs& a, int n, hipStream_t st) {
-    // H NORM at the reference's lag: HNorm
-    if constexpr (HORIZ && MODE == CB_NORM) {
-        if (SM_CB_HN && a.lag == NSV_LAG && a.D % 64 == 0 && a.arm_pad_rows == 2 * NSV_LAG) {
-            if (a.view == 0) {
-                if (a.apply_scale) launch_hn<false, true>(a, n, st);
-                else launch_hn<false, false>(a, n, st);
-            } else {
-                if (a.apply_scale) launch_hn<true, true>(a, n, st);
-                else launch_hn<true, false>(a, n, st);
-            }
-            return;
-        }
-    }
     if constexpr (MODE == CB_NORM) {
         if (a.apply_scale) return launch_scaled<HORIZ, MODE, true>(a, n, st);
     }

@@ -81,6 +81,9 @@ struct SgmArgs {
     int cor_thres, redu, keep_final;
     int signed_costs;           // 1: C may be < 0 (aggregation GF): k_sgm with float minima
     int n;                      // pairs in the launch
+    // checkpointed path pairs (k_sgm_ck): the second path of the pair is the first one reversed
+    float* ck;                  // [n][lines][segments][D]: the first path's L at segment ends
+    int dir2;                   // direction index of the pair's second path
 };
 
 struct GfPix {                  // guided filter, p-independent terms of one pixel (sm_gf.hip)
@@ -180,6 +183,14 @@ size_t prep_smem_bytes(int rv, int ru, int L_out);
 void launch_cbca(const CbcaArgs& a, bool horiz, int mode, int n, hipStream_t st);
 void launch_scale(float* vm, size_t n, float w, hipStream_t st);
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st);
+// Checkpointed path pairs (sm_sgm.hip, k_sgm_ck): CK_A sweeps the pair's first path and keeps
+// its L every sgm_ck_seg() steps; CK_B sweeps the second path, recomputing the first one's L
+// segment by segment from those checkpoints, and either writes L1 + L2 (CK_B, mode 0) or adds
+// both to the path sum, takes the WTA and writes the map (mode SGM_LAST [| SGM_KEEP]).
+enum { CK_A = 16, CK_B = 32 };
+bool sgm_ck_ok(int D, int paths);
+int sgm_ck_seg();
+void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st);
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);
 void launch_div_check(int exp2, int bmax, unsigned long long* bad, hipStream_t st);

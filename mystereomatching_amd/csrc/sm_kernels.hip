@@ -932,9 +932,6 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 // the adaptive weights the weights are 1, and 1 * x + 1 * y == x + y exactly.  lamG == 1 (the
 // default) skips the division, since -G / 1 == -G.
 // ---------------------------------------------------------------------------------------
-#ifndef SM_COST_EXPSKIP
-#define SM_COST_EXPSKIP 0   // 1: waves whose 64 gradient terms all lie below -17.5 skip the exact expf (A/B)
-#endif
 #ifndef SM_COST_STORE_AUX
 #define SM_COST_STORE_AUX 2   // buffer store cache policy: slc = non-temporal (see SM_ST_AUX, sm_device.h)
 #endif
@@ -1140,13 +1137,8 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 const float g = t1 + t2;
                 const float xg = LAM1 ? -g : -g / a.lam2;
                 const float t = luta[pc];                       // fl(2 - expf(-min(pc, icd) / lamCen))
-                float res;
-                if (SM_COST_EXPSKIP && !__builtin_amdgcn_ballot_w64(xg >= -17.5f)) {
-                    res = t;   // every lane's expf(xg) <= 2^-25: t - e == t (the proof above)
-                } else {
-                    const float ex = expf_glibc_core(fmaxf(xg, -100.0f), etab);
-                    res = t - ex;
-                }
+                const float ex = expf_glibc_core(fmaxf(xg, -100.0f), etab);
+                const float res = t - ex;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, voff, soff,
                                                       SM_COST_STORE_AUX);
                 return;

@@ -605,6 +605,282 @@ static int rows_kv(const SgmArgs& a, int mode) {
     return (K + 3) / 4;
 }
 
+// ---------------------------------------------------------------------------------------
+// Checkpointed path pairs (4-path SGM).  The path sum is ((L0 + L1) + L2) + L3 (gen_sgm_vm,
+// cpp:2031-2056; 0 + L0 == L0), and paths 0 / 1 (2 / 3) walk one line direction both ways, so a
+// pair needs no L volume in memory: pass A walks the pair's first path and keeps its L only at
+// the end of every segment of S steps; pass B walks the second path segment by segment and
+// first recomputes the first path's S values of the segment from the checkpoint before it —
+// the same operations on the same inputs, hence the same bits — then combines both in
+// registers.  Per element: A reads C (4 B + 4 / S for the checkpoints); B of pair (0, 1) reads C
+// and writes L0 + L1 (8 B + 4 / S); B of pair (2, 3) reads C and L0 + L1 and writes the map
+// (8 B + 4 / S): 24 B instead of the four sweeps' 8 + 12 + 12 + 8, for half again the
+// recursion arithmetic, which sweeps that wait on memory have to spare.
+// Segment k of pass B covers the first path's steps [steps - (k+1) S, steps - k S) (the last
+// segment may start before step 0); checkpoint slot k holds the first path's L at step
+// steps - (k+1) S - 1, i.e. at the end of the A tile before it.  Layout of k_sgm<4, ..., VEC>:
+// one line per wave, four consecutive disparities per lane (D in (128, 256], D % 4 == 0).
+// ---------------------------------------------------------------------------------------
+#ifndef SM_SGM_CK
+#define SM_SGM_CK 1
+#endif
+#ifndef SM_SGM_CK_S
+#define SM_SGM_CK_S 8
+#endif
+
+bool sgm_ck_ok(int D, int paths) { return SM_SGM_CK && paths == 4 && D > SM_SGM_VEC_MIN_D && D <= 256 && D % 4 == 0; }
+int sgm_ck_seg() { return SM_SGM_CK_S; }
+
+template <bool FULL, bool SG>
+struct CkStep {
+    float p1, p2, p1r, p2r;
+    bool cv;   // the lane's four disparities lie inside D
+    // one step of updateCost (h:2206-2280): k_sgm's step, operation for operation
+    __device__ __forceinline__ void run(float (&L)[4], const float (&Lp)[4], const float (&c)[4], bool pen, bool start) const {
+        if (start) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) L[k] = (FULL || cv) ? c[k] : FLT_MAX;
+            return;
+        }
+        const float P1 = pen ? p1r : p1, P2 = pen ? p2r : p2;
+        float lm = Lp[0];
+#pragma unroll
+        for (int k = 1; k < 4; k++) lm = SG ? fminf(lm, Lp[k]) : fmin_pos(lm, Lp[k]);
+        const float m = SG ? wave_min(lm) : wave_min_pos(lm);
+        const float P1m = P1 - m;
+        const float left = dpp_shr1<4>(Lp[3]);
+        const float right = dpp_shl1<4>(Lp[0]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float prev = (k == 0) ? left : Lp[k - 1];
+            const float next = (k == 3) ? right : Lp[k + 1];
+            const float S1 = Lp[k] - m;
+            const float S2 = prev + P1m;
+            const float S3 = next + P1m;
+            const float mm = SG ? fminf(fminf(S1, S2), fminf(S3, P2)) : fmin_pos(fmin_pos(S1, S2), fmin_pos(S3, P2));
+            const float Lk = c[k] + mm;
+            L[k] = (FULL || cv) ? Lk : FLT_MAX;
+        }
+    }
+};
+
+__device__ __forceinline__ void ld4(float (&d)[4], const float* p) {
+    const float4 v = ld_stream4(p);
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+}
+__device__ __forceinline__ void cp4(float (&d)[4], const float (&s)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = s[k];
+}
+
+template <int S, int MODE, bool FULL>
+__global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
+    constexpr bool SG = (MODE & SGM_SIGNED) != 0;
+    constexpr bool LAST = (MODE & SGM_LAST) != 0;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int H = a.H, W = a.W, D = a.D;
+    const int b = blockIdx.y;
+    const bool horiz = a.rv == 0;             // straight directions only (sgm_ck_ok: 4 paths)
+    const int nlines = horiz ? H : W;
+    if (wave >= nlines) return;               // wave-uniform
+    const int steps = horiz ? W : H;
+    const int v0 = horiz ? wave : (a.rv > 0 ? H - 1 : 0);
+    const int u0 = horiz ? (a.ru > 0 ? W - 1 : 0) : wave;
+    const int pstep = -a.rv * W - a.ru;       // pixel delta per step of the pair's FIRST path
+    const size_t npix = (size_t)H * W;
+    const size_t p0 = (size_t)v0 * W + u0;
+    const long vstep = (long)pstep * D;
+    const int d0 = lane * 4;
+    const bool cv = d0 < D;
+    const int ldc = cv ? d0 : D - 4;          // lanes past D load a valid (unused) chunk
+    const float* cld = a.vm + ((size_t)b * npix + p0) * D + ldc;
+    const float* ald = a.acc + ((size_t)b * npix + p0) * D + ldc;
+    float* ast = a.acc + ((size_t)b * npix + p0) * D + d0;
+    float* fst = a.vm + ((size_t)b * npix + p0) * D + d0;
+    const uint8_t* flbase = a.flags + (size_t)b * npix + p0;
+    int16_t* dbase = a.disp + (size_t)b * npix + p0;
+    const int nseg = (steps + S - 1) / S;     // segments of the line (= its checkpoint slots)
+    float* ckl = a.ck + ((size_t)b * nlines + wave) * (size_t)nseg * D;
+    const CkStep<FULL, SG> st{a.p1, a.p2, a.p1 / (float)a.redu, a.p2 / (float)a.redu, cv};
+    const int dirA = a.dir, dirB = a.dir2;
+    auto clampj = [&](int j) { return j < 0 ? 0 : (j >= steps ? steps - 1 : j); };
+    auto pen = [&](uint32_t fl, int s, int dir) { return (((uint32_t)__builtin_amdgcn_readlane((int)fl, s) >> dir) & 1u) != 0; };
+
+    if constexpr ((MODE & CK_A) != 0) {
+        // pass A: the first path; tile t covers steps [steps - (nseg - t) S, ... + S), so every
+        // tile but the last ends on a checkpoint (slot nseg - t - 2)
+        struct Tl {
+            float c[S][4];
+            uint32_t fl;   // lane s < S: flags of the tile's step s
+        };
+        auto load = [&](Tl& t, int tt) {
+            const int j0 = steps - (nseg - tt) * S;
+#pragma unroll
+            for (int s = 0; s < S; s++) ld4(t.c[s], cld + (long)clampj(j0 + s) * vstep);
+            t.fl = flbase[(long)clampj(j0 + min(lane, S - 1)) * pstep];
+        };
+        float Lp[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+        auto process = [&](const Tl& t, int tt) {
+            const int j0 = steps - (nseg - tt) * S;
+            if (j0 > 0) {
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    float L[4];
+                    st.run(L, Lp, t.c[s], pen(t.fl, s, dirA), false);
+                    cp4(Lp, L);
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < S; s++)
+                    if (j0 + s >= 0) {
+                        float L[4];
+                        st.run(L, Lp, t.c[s], pen(t.fl, s, dirA), j0 + s == 0);
+                        cp4(Lp, L);
+                    }
+            }
+            if (tt <= nseg - 2 && (FULL || cv))
+                st_stream4(ckl + (size_t)(nseg - tt - 2) * D + d0, make_float4(Lp[0], Lp[1], Lp[2], Lp[3]));
+        };
+        Tl ta, tb;
+        load(ta, 0);
+        for (int tt = 0; tt < nseg; tt += 2) {
+            load(tb, tt + 1);
+            process(ta, tt);
+            load(ta, tt + 2);
+            if (tt + 1 < nseg) process(tb, tt + 1);
+        }
+    } else {
+        // pass B: the second path, segment k = the first path's steps [aj0, aj0 + S), walked
+        // from aj0 + S - 1 down; the first path's L over the segment is recomputed in registers
+        struct Sg {
+            float c[S][4];
+            float acc[LAST ? S : 1][4];   // L0 + L1 (pair (2, 3))
+            float ck[4];                  // the first path's L at step aj0 - 1
+            uint32_t fl;
+        };
+        auto load = [&](Sg& g, int k) {
+            const int aj0 = steps - (k + 1) * S;
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+                const long off = (long)clampj(aj0 + s) * vstep;
+                ld4(g.c[s], cld + off);
+                if (LAST) ld4(g.acc[s], ald + off);
+            }
+            ld4(g.ck, ckl + (size_t)(k < nseg - 1 ? k : 0) * D + ldc);
+            g.fl = flbase[(long)clampj(aj0 + min(lane, S - 1)) * pstep];
+        };
+        float Lp[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+        int dacc = -1;   // LAST: lane s holds the disparity of segment step s until the map store
+        auto emit = [&](const Sg& g, int s, int j, const float (&LA)[4], const float (&LB)[4]) {
+            float f[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) f[q] = LAST ? (g.acc[s][q] + LA[q]) + LB[q] : LA[q] + LB[q];
+            if (!LAST) {
+                if (FULL || cv) st_stream4(ast + (long)j * vstep, make_float4(f[0], f[1], f[2], f[3]));
+                return;
+            }
+            if ((MODE & SGM_KEEP) && (FULL || cv)) st_stream4(fst + (long)j * vstep, make_float4(f[0], f[1], f[2], f[3]));
+            float bm = f[0];
+            int bi = d0;
+#pragma unroll
+            for (int q = 1; q < 4; q++)
+                if (bm > f[q]) {
+                    bm = f[q];
+                    bi = d0 + q;
+                }
+            const float wm = SG ? wave_min(bm) : wave_min_pos(bm);
+            const uint64_t hit = __ballot(bm == wm);
+            const int widx = __builtin_amdgcn_readlane(bi, (int)__builtin_ctzll(hit));
+            const int dsel = (wm < FLT_MAX) ? widx : -1;
+            dacc = (lane == s) ? dsel : dacc;
+        };
+        auto process = [&](const Sg& g, int k) {
+            const int aj0 = steps - (k + 1) * S;
+            float LA[S][4];
+            if (k > 0 && aj0 > 0) {   // neither path starts inside the segment
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    if (s == 0)
+                        st.run(LA[0], g.ck, g.c[0], pen(g.fl, 0, dirA), false);
+                    else
+                        st.run(LA[s], LA[s - 1], g.c[s], pen(g.fl, s, dirA), false);
+                }
+#pragma unroll
+                for (int s = S - 1; s >= 0; s--) {
+                    float L[4];
+                    st.run(L, Lp, g.c[s], pen(g.fl, s, dirB), false);
+                    cp4(Lp, L);
+                    emit(g, s, aj0 + s, LA[s], L);
+                }
+            } else {
+                float prev[4];
+                cp4(prev, g.ck);
+#pragma unroll
+                for (int s = 0; s < S; s++)
+                    if (aj0 + s >= 0) {
+                        st.run(LA[s], prev, g.c[s], pen(g.fl, s, dirA), aj0 + s == 0);
+                        cp4(prev, LA[s]);
+                    }
+#pragma unroll
+                for (int s = S - 1; s >= 0; s--)
+                    if (aj0 + s >= 0) {
+                        float L[4];
+                        st.run(L, Lp, g.c[s], pen(g.fl, s, dirB), aj0 + s == steps - 1);
+                        cp4(Lp, L);
+                        emit(g, s, aj0 + s, LA[s], L);
+                    }
+            }
+            if (LAST) {   // one store instruction per segment for the int16 disparities
+                if (lane < S && aj0 + lane >= 0) dbase[(long)(aj0 + lane) * pstep] = (int16_t)dacc;
+            }
+        };
+        Sg ga, gb;
+        load(ga, 0);
+        for (int k = 0; k < nseg; k += 2) {
+            load(gb, k + 1);
+            process(ga, k);
+            load(ga, k + 2);
+            if (k + 1 < nseg) process(gb, k + 1);
+        }
+    }
+}
+
+template <int MODE, bool FULL>
+static void launch_ck_m(const SgmArgs& a, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((k_sgm_ck<SM_SGM_CK_S, MODE, FULL>), grid, dim3(256), 0, st, a);
+}
+template <bool FULL, int SGN>
+static void launch_ck_f(const SgmArgs& a, int mode, dim3 grid, hipStream_t st) {
+    switch (mode) {
+        case CK_A: return launch_ck_m<SGN | CK_A, FULL>(a, grid, st);
+        case CK_B: return launch_ck_m<SGN | CK_B, FULL>(a, grid, st);
+        case CK_B | SGM_LAST: return launch_ck_m<SGN | CK_B | SGM_LAST, FULL>(a, grid, st);
+        default: return launch_ck_m<SGN | CK_B | SGM_LAST | SGM_KEEP, FULL>(a, grid, st);
+    }
+}
+void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st) {
+    SgmArgs b = a;
+    b.n = n;
+    const int nlines = a.rv == 0 ? a.H : a.W;
+    const dim3 grid((nlines + 3) / 4, n);
+    if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
+    if (a.signed_costs) {
+        if (a.D == 256)
+            launch_ck_f<true, SGM_SIGNED>(b, mode, grid, st);
+        else
+            launch_ck_f<false, SGM_SIGNED>(b, mode, grid, st);
+    } else {
+        if (a.D == 256)
+            launch_ck_f<true, 0>(b, mode, grid, st);
+        else
+            launch_ck_f<false, 0>(b, mode, grid, st);
+    }
+}
+
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st) {
     SgmArgs b = a;
     b.n = n;

@@ -290,6 +290,28 @@ def test_shapes_and_edge_cases(oracle, H, W, md, paths):
     np.testing.assert_array_equal(dp, ref["disp"])
 
 
+@pytest.mark.parametrize("H,W,md", [(2, 2, 131), (2, 9, 255), (8, 8, 199), (9, 17, 255), (16, 24, 131),
+                                     (17, 33, 255), (23, 7, 199), (40, 41, 255)])
+def test_sgm_checkpointed_pairs(oracle, H, W, md):
+    """4-path SGM with 128 < D <= 256, D % 4 == 0 runs as two checkpointed path pairs (k_sgm_ck,
+    segments of 8 steps): lines shorter than, equal to and one longer than a segment, ragged
+    tails, D below 256; the summed volume (keep_final) and the map bit-exact, and the map again
+    through the batch path (no final volume)."""
+    pair = S.make_pair(H, W, md + 1, 50 + H + W)
+    cfg = oracle.config(H, W, md, sgm_paths=4)
+    ref = oracle.run(pair, cfg, dumps=True)
+    _, agg, final, dp = run_reference_order(pair, md, paths=4)
+    np.testing.assert_array_equal(bits(agg), bits(ref["agg"]))
+    np.testing.assert_array_equal(bits(final), bits(ref["final"]))
+    np.testing.assert_array_equal(dp, ref["disp"])
+    sb = StereoBatch(md, H, W, 2, sgm_paths=4)
+    sb.upload(*(np.stack([pair[k], pair[k]]) for k in ("lbgr", "rbgr", "lgray", "rgray")))
+    disp = sb.run(0.3)
+    sb.close()
+    np.testing.assert_array_equal(disp[0], ref["disp"])
+    np.testing.assert_array_equal(disp[1], ref["disp"])
+
+
 def test_flat_images_long_arms(oracle):
     """Uniform regions: arms saturate at L_out = 34, prefix sums run long."""
     H, W, md = 60, 90, 31

@@ -22,6 +22,17 @@ def profile_name(sym: str, seen: dict) -> str:
         h = m.group(1) == "true"
         mode = {"0": "scan", "1": "norm", "2": "norm_scan"}[m.group(2)]
         return f"cbca_{'h' if h else 'v'}_{mode}"
+    if "k_cbca_nsv" in sym:
+        return "cbca_v_norm_scan"
+    if "k_cbca_hn" in sym:
+        return "cbca_h_norm"
+    m = re.search(r"k_sgm_ck<\d+, (\d+),", sym)
+    if m:
+        mode = int(m.group(1))  # CK_A = 16, CK_B = 32, SGM_LAST = 2
+        if mode & 16:
+            seen["ck_a"] = seen.get("ck_a", 0) + 1
+            return "sgm_ck_a01" if seen["ck_a"] % 2 == 1 else "sgm_ck_a23"
+        return "sgm_last_wta" if mode & 2 else "sgm_ck_b01"
     m = re.search(r"k_sgm(?:_rows)?<\d+, (\d+),", sym)
     if m:
         mode = int(m.group(1))  # SGM_FIRST = 1, SGM_LAST = 2, SGM_KEEP = 4

@@ -707,18 +707,22 @@ sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
         a.redu = p.sgm_redu_coeff;
         a.keep_final = p.keep_final_volume;
         a.signed_costs = p.aggregation == SM_AGG_GF;   // the guided filter's output can be < 0
+        int first = 0;   // first path left to the plain sweeps
         if (B.ck) {
             // checkpointed pairs (0, 1) and (2, 3): 4 + 8 + 4 + 8 B per element (+ 4 / S for
-            // the checkpoints each way) instead of 8 + 12 + 12 + 8
+            // the checkpoints each way) instead of 8 + 12 + 12 + 8; with 8 paths the second
+            // pair adds into the running sum (12 B) and paths 4 .. 7 follow as sweeps
             a.ck = B.ck;
-            const double ckb = 4.0 / sm::sgm_ck_seg();
+            const double ckb = 4.0 / sm::sgm_ck_seg(p.num_disparities);
             const double nv = (double)n * c->nvol;
+            const bool four = p.sgm_paths == 4;
             struct Pass { int path, mode; const char* name; double per; };
             const Pass passes[4] = {
                 {0, sm::CK_A, "sgm_ck_a01", 4.0 + ckb},
                 {0, sm::CK_B, "sgm_ck_b01", 8.0 + ckb},
                 {2, sm::CK_A, "sgm_ck_a23", 4.0 + ckb},
-                {2, sm::CK_B | sm::SGM_LAST, "sgm_last_wta", 8.0 + ckb + (p.keep_final_volume ? 4.0 : 0)}};
+                four ? Pass{2, sm::CK_B | sm::SGM_LAST, "sgm_last_wta", 8.0 + ckb + (p.keep_final_volume ? 4.0 : 0)}
+                     : Pass{2, sm::CK_B | sm::CK_MID, "sgm_ck_b23", 12.0 + ckb}};
             for (const Pass& ps : passes) {
                 a.rv = RV[ps.path];
                 a.ru = RU[ps.path];
@@ -729,9 +733,9 @@ sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
                 sm_status s = timed(c, name.c_str(), bytes, [&] { sm::launch_sgm_ck(a, ps.mode, n, c->st); });
                 if (s) return s;
             }
-            return SM_OK;
+            first = 4;
         }
-        for (int i = 0; i < p.sgm_paths; i++) {
+        for (int i = first; i < p.sgm_paths; i++) {
             a.rv = RV[i];
             a.ru = RU[i];
             a.dir = i;
@@ -960,7 +964,7 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if (p->optimization == SM_OPT_SGM && p->sgm_paths > 1)
         if ((s = dalloc(c, &c->acc, cap * c->nvol + vpad))) return s;
     if (p->optimization == SM_OPT_SGM && sm::sgm_ck_ok(p->num_disparities, p->sgm_paths)) {
-        const size_t S = (size_t)sm::sgm_ck_seg(), H = (size_t)p->rows, W = (size_t)p->cols;
+        const size_t S = (size_t)sm::sgm_ck_seg(p->num_disparities), H = (size_t)p->rows, W = (size_t)p->cols;
         const size_t lines_x_segs = std::max(H * ((W + S - 1) / S), W * ((H + S - 1) / S));
         c->ck_pair = lines_x_segs * (size_t)p->num_disparities;
         if ((s = dalloc(c, &c->ck, cap * c->ck_pair))) return s;

@@ -184,12 +184,13 @@ void launch_cbca(const CbcaArgs& a, bool horiz, int mode, int n, hipStream_t st)
 void launch_scale(float* vm, size_t n, float w, hipStream_t st);
 void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st);
 // Checkpointed path pairs (sm_sgm.hip, k_sgm_ck): CK_A sweeps the pair's first path and keeps
-// its L every sgm_ck_seg() steps; CK_B sweeps the second path, recomputing the first one's L
-// segment by segment from those checkpoints, and either writes L1 + L2 (CK_B, mode 0) or adds
-// both to the path sum, takes the WTA and writes the map (mode SGM_LAST [| SGM_KEEP]).
-enum { CK_A = 16, CK_B = 32 };
+// its L every sgm_ck_seg(D) steps; CK_B sweeps the second path, recomputing the first one's L
+// segment by segment from those checkpoints, and writes L_first + L_second (CK_B), adds both to
+// the running sum (CK_B | CK_MID, 8 paths) or adds them, takes the WTA and writes the map
+// (CK_B | SGM_LAST [| SGM_KEEP]).
+enum { CK_A = 16, CK_B = 32, CK_MID = 64 };
 bool sgm_ck_ok(int D, int paths);
-int sgm_ck_seg();
+int sgm_ck_seg(int D);
 void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st);
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);

@@ -606,7 +606,7 @@ static int rows_kv(const SgmArgs& a, int mode) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Checkpointed path pairs (4-path SGM).  The path sum is ((L0 + L1) + L2) + L3 (gen_sgm_vm,
+// Checkpointed path pairs.  The path sum is ((L0 + L1) + L2) + L3 ... (gen_sgm_vm,
 // cpp:2031-2056; 0 + L0 == L0), and paths 0 / 1 (2 / 3) walk one line direction both ways, so a
 // pair needs no L volume in memory: pass A walks the pair's first path and keeps its L only at
 // the end of every segment of S steps; pass B walks the second path segment by segment and
@@ -614,136 +614,191 @@ static int rows_kv(const SgmArgs& a, int mode) {
 // the same operations on the same inputs, hence the same bits — then combines both in
 // registers.  Per element: A reads C (4 B + 4 / S for the checkpoints); B of pair (0, 1) reads C
 // and writes L0 + L1 (8 B + 4 / S); B of pair (2, 3) reads C and L0 + L1 and writes the map
-// (8 B + 4 / S): 24 B instead of the four sweeps' 8 + 12 + 12 + 8, for half again the
-// recursion arithmetic, which sweeps that wait on memory have to spare.
+// (8 B + 4 / S) or, with 8 paths, the running sum (12 B + 4 / S): 24 B instead of the four
+// sweeps' 8 + 12 + 12 + 8, for half again the recursion arithmetic, which sweeps that wait on
+// memory have to spare.  Paths 4 .. 7 (8 paths) then run as k_sgm / k_sgm_rows sweeps.
 // Segment k of pass B covers the first path's steps [steps - (k+1) S, steps - k S) (the last
 // segment may start before step 0); checkpoint slot k holds the first path's L at step
-// steps - (k+1) S - 1, i.e. at the end of the A tile before it.  Layout of k_sgm<4, ..., VEC>:
-// one line per wave, four consecutive disparities per lane (D in (128, 256], D % 4 == 0).
+// steps - (k+1) S - 1, i.e. at the end of the A tile before it.
+// Layouts: D in (128, 256]: k_sgm<4, ..., VEC>'s, one line per wave, four consecutive
+// disparities per lane (dwordx4); D <= 128: k_sgm_rows's, four lines per wave, a DPP row of 16
+// lanes per line, 4 KV disparities per lane.  D % 4 == 0 throughout.
 // ---------------------------------------------------------------------------------------
 #ifndef SM_SGM_CK
 #define SM_SGM_CK 1
 #endif
 #ifndef SM_SGM_CK_S
-#define SM_SGM_CK_S 8
+#define SM_SGM_CK_S 8        // segment steps (layouts with 4 disparities per lane)
+#endif
+#ifndef SM_SGM_CK_S2
+#define SM_SGM_CK_S2 4       // segment steps with 8 disparities per lane (D in (64, 128])
 #endif
 
-bool sgm_ck_ok(int D, int paths) { return SM_SGM_CK && paths == 4 && D > SM_SGM_VEC_MIN_D && D <= 256 && D % 4 == 0; }
-int sgm_ck_seg() { return SM_SGM_CK_S; }
+bool sgm_ck_ok(int D, int paths) { return SM_SGM_CK && (paths == 4 || paths == 8) && D <= 256 && D % 4 == 0; }
+static int ck_kv(int D) { return D > SM_SGM_VEC_MIN_D ? 0 : ((D + 15) / 16 + 3) / 4; }   // 0: one line per wave
+int sgm_ck_seg(int D) { return ck_kv(D) == 2 ? SM_SGM_CK_S2 : SM_SGM_CK_S; }
 
-template <bool FULL, bool SG>
+template <int KV, bool ROWS, bool FULL, bool SG>
 struct CkStep {
+    static constexpr int K = 4 * KV;
     float p1, p2, p1r, p2r;
-    bool cv;   // the lane's four disparities lie inside D
-    // one step of updateCost (h:2206-2280): k_sgm's step, operation for operation
-    __device__ __forceinline__ void run(float (&L)[4], const float (&Lp)[4], const float (&c)[4], bool pen, bool start) const {
+    bool cv[KV];   // the lane's c-th chunk of four disparities lies inside D
+    __device__ __forceinline__ float mn(float x, float y) const { return SG ? fminf(x, y) : fmin_pos(x, y); }
+    __device__ __forceinline__ float line_min(float x) const {
+        if (ROWS) return SG ? row_fmin(x) : __builtin_bit_cast(float, row_umin(__builtin_bit_cast(uint32_t, x)));
+        return SG ? wave_min(x) : wave_min_pos(x);
+    }
+    // one step of updateCost (h:2206-2280): k_sgm's / k_sgm_rows's step, operation for operation
+    __device__ __forceinline__ void run(float (&L)[K], const float (&Lp)[K], const float (&c)[K], bool pen, bool start) const {
         if (start) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) L[k] = (FULL || cv) ? c[k] : FLT_MAX;
+            for (int k = 0; k < K; k++) L[k] = (FULL || cv[k / 4]) ? c[k] : FLT_MAX;
             return;
         }
         const float P1 = pen ? p1r : p1, P2 = pen ? p2r : p2;
         float lm = Lp[0];
 #pragma unroll
-        for (int k = 1; k < 4; k++) lm = SG ? fminf(lm, Lp[k]) : fmin_pos(lm, Lp[k]);
-        const float m = SG ? wave_min(lm) : wave_min_pos(lm);
+        for (int k = 1; k < K; k++) lm = mn(lm, Lp[k]);
+        const float m = line_min(lm);
         const float P1m = P1 - m;
-        const float left = dpp_shr1<4>(Lp[3]);
-        const float right = dpp_shl1<4>(Lp[0]);
+        const float left = ROWS ? row_shift<DPP_ROW_SHR1>(Lp[K - 1]) : dpp_shr1<K>(Lp[K - 1]);
+        const float right = ROWS ? row_shift<DPP_ROW_SHL1>(Lp[0]) : dpp_shl1<K>(Lp[0]);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < K; k++) {
             const float prev = (k == 0) ? left : Lp[k - 1];
-            const float next = (k == 3) ? right : Lp[k + 1];
+            const float next = (k == K - 1) ? right : Lp[k + 1];
             const float S1 = Lp[k] - m;
             const float S2 = prev + P1m;
             const float S3 = next + P1m;
-            const float mm = SG ? fminf(fminf(S1, S2), fminf(S3, P2)) : fmin_pos(fmin_pos(S1, S2), fmin_pos(S3, P2));
+            const float mm = mn(mn(S1, S2), mn(S3, P2));
             const float Lk = c[k] + mm;
-            L[k] = (FULL || cv) ? Lk : FLT_MAX;
+            L[k] = (FULL || cv[k / 4]) ? Lk : FLT_MAX;
         }
     }
 };
 
-__device__ __forceinline__ void ld4(float (&d)[4], const float* p) {
-    const float4 v = ld_stream4(p);
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-    d[3] = v.w;
-}
-__device__ __forceinline__ void cp4(float (&d)[4], const float (&s)[4]) {
+template <int K>
+__device__ __forceinline__ void cpk(float (&d)[K], const float (&s)[K]) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) d[k] = s[k];
+    for (int k = 0; k < K; k++) d[k] = s[k];
 }
 
-template <int S, int MODE, bool FULL>
+template <int S, int MODE, int KV, bool ROWS, bool FULL>
 __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
+    static_assert(ROWS || KV == 1, "one line per wave: four disparities per lane");
+    constexpr int K = 4 * KV;
+    constexpr int LPL = ROWS ? 16 : 64;   // lanes per line
     constexpr bool SG = (MODE & SGM_SIGNED) != 0;
     constexpr bool LAST = (MODE & SGM_LAST) != 0;
-    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    constexpr bool ACC_IN = LAST || (MODE & CK_MID) != 0;
     const int lane = threadIdx.x & 63;
+    const int row = ROWS ? lane >> 4 : 0, ll = ROWS ? lane & 15 : lane;
     const int H = a.H, W = a.W, D = a.D;
-    const int b = blockIdx.y;
-    const bool horiz = a.rv == 0;             // straight directions only (sgm_ck_ok: 4 paths)
-    const int nlines = horiz ? H : W;
-    if (wave >= nlines) return;               // wave-uniform
+    const bool horiz = a.rv == 0;             // straight directions only
+    const int nl = horiz ? H : W;
     const int steps = horiz ? W : H;
-    const int v0 = horiz ? wave : (a.rv > 0 ? H - 1 : 0);
-    const int u0 = horiz ? (a.ru > 0 ? W - 1 : 0) : wave;
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256 + threadIdx.x) >> 6));
+    int b, line;
+    bool line_ok;
+    if (ROWS) {   // 1-D grid over (pair, group of four lines)
+        const int wpp = (nl + 3) >> 2;
+        b = wave / wpp;
+        if (b >= a.n) return;                 // wave-uniform
+        const int l = 4 * (wave - b * wpp) + row;
+        line_ok = l < nl;
+        line = line_ok ? l : nl - 1;          // rows past the last line run a copy and store nothing
+    } else {      // 2-D grid: (line, pair)
+        b = blockIdx.y;
+        if (wave >= nl) return;               // wave-uniform
+        line = wave;
+        line_ok = true;
+    }
+    const int v0 = horiz ? line : (a.rv > 0 ? H - 1 : 0);
+    const int u0 = horiz ? (a.ru > 0 ? W - 1 : 0) : line;
     const int pstep = -a.rv * W - a.ru;       // pixel delta per step of the pair's FIRST path
     const size_t npix = (size_t)H * W;
     const size_t p0 = (size_t)v0 * W + u0;
     const long vstep = (long)pstep * D;
-    const int d0 = lane * 4;
-    const bool cv = d0 < D;
-    const int ldc = cv ? d0 : D - 4;          // lanes past D load a valid (unused) chunk
-    const float* cld = a.vm + ((size_t)b * npix + p0) * D + ldc;
-    const float* ald = a.acc + ((size_t)b * npix + p0) * D + ldc;
-    float* ast = a.acc + ((size_t)b * npix + p0) * D + d0;
-    float* fst = a.vm + ((size_t)b * npix + p0) * D + d0;
+    const int d0 = ll * K;
+    CkStep<KV, ROWS, FULL, SG> st;
+    st.p1 = a.p1;
+    st.p2 = a.p2;
+    st.p1r = a.p1 / (float)a.redu;
+    st.p2r = a.p2 / (float)a.redu;
+    int ldc[KV];                              // chunk load column (chunks past D: a valid one)
+#pragma unroll
+    for (int c = 0; c < KV; c++) {
+        st.cv[c] = d0 + 4 * c < D;
+        ldc[c] = st.cv[c] ? d0 + 4 * c : D - 4;
+    }
+    const float* cld = a.vm + ((size_t)b * npix + p0) * D;
+    const float* ald = a.acc + ((size_t)b * npix + p0) * D;
+    float* ast = a.acc + ((size_t)b * npix + p0) * D;
+    float* fst = a.vm + ((size_t)b * npix + p0) * D;
     const uint8_t* flbase = a.flags + (size_t)b * npix + p0;
     int16_t* dbase = a.disp + (size_t)b * npix + p0;
     const int nseg = (steps + S - 1) / S;     // segments of the line (= its checkpoint slots)
-    float* ckl = a.ck + ((size_t)b * nlines + wave) * (size_t)nseg * D;
-    const CkStep<FULL, SG> st{a.p1, a.p2, a.p1 / (float)a.redu, a.p2 / (float)a.redu, cv};
+    float* ckl = a.ck + ((size_t)b * nl + line) * (size_t)nseg * D;
     const int dirA = a.dir, dirB = a.dir2;
     auto clampj = [&](int j) { return j < 0 ? 0 : (j >= steps ? steps - 1 : j); };
-    auto pen = [&](uint32_t fl, int s, int dir) { return (((uint32_t)__builtin_amdgcn_readlane((int)fl, s) >> dir) & 1u) != 0; };
+    auto pen = [&](uint32_t fl, int s, int dir) {
+        const uint32_t f = ROWS ? (uint32_t)__builtin_amdgcn_ds_bpermute(row * 64 + s * 4, (int)fl)   // the row's lane s
+                                : (uint32_t)__builtin_amdgcn_readlane((int)fl, s);
+        return ((f >> dir) & 1u) != 0;
+    };
+    auto ldK = [&](float (&d)[K], const float* base, long off) {
+#pragma unroll
+        for (int c = 0; c < KV; c++) {
+            const float4 v = ld_stream4(base + off + ldc[c]);
+            d[4 * c + 0] = v.x;
+            d[4 * c + 1] = v.y;
+            d[4 * c + 2] = v.z;
+            d[4 * c + 3] = v.w;
+        }
+    };
+    auto stK = [&](float* base, long off, const float (&f)[K]) {
+        if (!line_ok) return;
+#pragma unroll
+        for (int c = 0; c < KV; c++)
+            if (FULL || st.cv[c]) st_stream4(base + off + d0 + 4 * c, make_float4(f[4 * c + 0], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]));
+    };
+    auto flag_of = [&](int j0) { return (uint32_t)flbase[(long)clampj(j0 + min(ll, S - 1)) * pstep]; };
 
     if constexpr ((MODE & CK_A) != 0) {
         // pass A: the first path; tile t covers steps [steps - (nseg - t) S, ... + S), so every
         // tile but the last ends on a checkpoint (slot nseg - t - 2)
         struct Tl {
-            float c[S][4];
-            uint32_t fl;   // lane s < S: flags of the tile's step s
+            float c[S][K];
+            uint32_t fl;   // lane s < S (of each line): flags of the tile's step s
         };
         auto load = [&](Tl& t, int tt) {
             const int j0 = steps - (nseg - tt) * S;
 #pragma unroll
-            for (int s = 0; s < S; s++) ld4(t.c[s], cld + (long)clampj(j0 + s) * vstep);
-            t.fl = flbase[(long)clampj(j0 + min(lane, S - 1)) * pstep];
+            for (int s = 0; s < S; s++) ldK(t.c[s], cld, (long)clampj(j0 + s) * vstep);
+            t.fl = flag_of(j0);
         };
-        float Lp[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+        float Lp[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) Lp[k] = FLT_MAX;
         auto process = [&](const Tl& t, int tt) {
             const int j0 = steps - (nseg - tt) * S;
             if (j0 > 0) {
 #pragma unroll
                 for (int s = 0; s < S; s++) {
-                    float L[4];
+                    float L[K];
                     st.run(L, Lp, t.c[s], pen(t.fl, s, dirA), false);
-                    cp4(Lp, L);
+                    cpk(Lp, L);
                 }
             } else {
 #pragma unroll
                 for (int s = 0; s < S; s++)
                     if (j0 + s >= 0) {
-                        float L[4];
+                        float L[K];
                         st.run(L, Lp, t.c[s], pen(t.fl, s, dirA), j0 + s == 0);
-                        cp4(Lp, L);
+                        cpk(Lp, L);
                     }
             }
-            if (tt <= nseg - 2 && (FULL || cv))
-                st_stream4(ckl + (size_t)(nseg - tt - 2) * D + d0, make_float4(Lp[0], Lp[1], Lp[2], Lp[3]));
+            if (tt <= nseg - 2) stK(ckl, (long)(nseg - tt - 2) * D, Lp);
         };
         Tl ta, tb;
         load(ta, 0);
@@ -757,9 +812,9 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
         // pass B: the second path, segment k = the first path's steps [aj0, aj0 + S), walked
         // from aj0 + S - 1 down; the first path's L over the segment is recomputed in registers
         struct Sg {
-            float c[S][4];
-            float acc[LAST ? S : 1][4];   // L0 + L1 (pair (2, 3))
-            float ck[4];                  // the first path's L at step aj0 - 1
+            float c[S][K];
+            float acc[ACC_IN ? S : 1][K];   // the running sum (pair (2, 3))
+            float ck[K];                    // the first path's L at step aj0 - 1
             uint32_t fl;
         };
         auto load = [&](Sg& g, int k) {
@@ -767,40 +822,50 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
 #pragma unroll
             for (int s = 0; s < S; s++) {
                 const long off = (long)clampj(aj0 + s) * vstep;
-                ld4(g.c[s], cld + off);
-                if (LAST) ld4(g.acc[s], ald + off);
+                ldK(g.c[s], cld, off);
+                if (ACC_IN) ldK(g.acc[s], ald, off);
             }
-            ld4(g.ck, ckl + (size_t)(k < nseg - 1 ? k : 0) * D + ldc);
-            g.fl = flbase[(long)clampj(aj0 + min(lane, S - 1)) * pstep];
+            ldK(g.ck, ckl, (long)(k < nseg - 1 ? k : 0) * D);
+            g.fl = flag_of(aj0);
         };
-        float Lp[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
-        int dacc = -1;   // LAST: lane s holds the disparity of segment step s until the map store
-        auto emit = [&](const Sg& g, int s, int j, const float (&LA)[4], const float (&LB)[4]) {
-            float f[4];
+        float Lp[K];
 #pragma unroll
-            for (int q = 0; q < 4; q++) f[q] = LAST ? (g.acc[s][q] + LA[q]) + LB[q] : LA[q] + LB[q];
+        for (int k = 0; k < K; k++) Lp[k] = FLT_MAX;
+        int dacc = -1;   // LAST: lane s (of each line) holds the disparity of segment step s
+        auto emit = [&](const Sg& g, int s, int j, const float (&LA)[K], const float (&LB)[K]) {
+            float f[K];
+#pragma unroll
+            for (int q = 0; q < K; q++) f[q] = ACC_IN ? (g.acc[s][q] + LA[q]) + LB[q] : LA[q] + LB[q];
             if (!LAST) {
-                if (FULL || cv) st_stream4(ast + (long)j * vstep, make_float4(f[0], f[1], f[2], f[3]));
+                stK(ast, (long)j * vstep, f);
                 return;
             }
-            if ((MODE & SGM_KEEP) && (FULL || cv)) st_stream4(fst + (long)j * vstep, make_float4(f[0], f[1], f[2], f[3]));
+            if (MODE & SGM_KEEP) stK(fst, (long)j * vstep, f);
+            // first minimum: the lowest lane of the line holding its minimum, then that lane's
+            // first index (lanes past D hold FLT_MAX or more: -1 only when everything does)
             float bm = f[0];
             int bi = d0;
 #pragma unroll
-            for (int q = 1; q < 4; q++)
+            for (int q = 1; q < K; q++)
                 if (bm > f[q]) {
                     bm = f[q];
                     bi = d0 + q;
                 }
-            const float wm = SG ? wave_min(bm) : wave_min_pos(bm);
+            const float wm = st.line_min(bm);
             const uint64_t hit = __ballot(bm == wm);
-            const int widx = __builtin_amdgcn_readlane(bi, (int)__builtin_ctzll(hit));
+            int widx;
+            if (ROWS) {
+                const uint32_t rmask = (uint32_t)(hit >> (row * 16)) & 0xffffu;
+                widx = __builtin_amdgcn_ds_bpermute((row * 16 + __builtin_ctz(rmask)) * 4, bi);
+            } else {
+                widx = __builtin_amdgcn_readlane(bi, (int)__builtin_ctzll(hit));
+            }
             const int dsel = (wm < FLT_MAX) ? widx : -1;
-            dacc = (lane == s) ? dsel : dacc;
+            dacc = (ll == s) ? dsel : dacc;
         };
         auto process = [&](const Sg& g, int k) {
             const int aj0 = steps - (k + 1) * S;
-            float LA[S][4];
+            float LA[S][K];
             if (k > 0 && aj0 > 0) {   // neither path starts inside the segment
 #pragma unroll
                 for (int s = 0; s < S; s++) {
@@ -811,31 +876,31 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
                 }
 #pragma unroll
                 for (int s = S - 1; s >= 0; s--) {
-                    float L[4];
+                    float L[K];
                     st.run(L, Lp, g.c[s], pen(g.fl, s, dirB), false);
-                    cp4(Lp, L);
+                    cpk(Lp, L);
                     emit(g, s, aj0 + s, LA[s], L);
                 }
             } else {
-                float prev[4];
-                cp4(prev, g.ck);
+                float prev[K];
+                cpk(prev, g.ck);
 #pragma unroll
                 for (int s = 0; s < S; s++)
                     if (aj0 + s >= 0) {
                         st.run(LA[s], prev, g.c[s], pen(g.fl, s, dirA), aj0 + s == 0);
-                        cp4(prev, LA[s]);
+                        cpk(prev, LA[s]);
                     }
 #pragma unroll
                 for (int s = S - 1; s >= 0; s--)
                     if (aj0 + s >= 0) {
-                        float L[4];
+                        float L[K];
                         st.run(L, Lp, g.c[s], pen(g.fl, s, dirB), aj0 + s == steps - 1);
-                        cp4(Lp, L);
+                        cpk(Lp, L);
                         emit(g, s, aj0 + s, LA[s], L);
                     }
             }
-            if (LAST) {   // one store instruction per segment for the int16 disparities
-                if (lane < S && aj0 + lane >= 0) dbase[(long)(aj0 + lane) * pstep] = (int16_t)dacc;
+            if (LAST) {   // one store instruction per segment (and line) for the int16 disparities
+                if (line_ok && ll < S && aj0 + ll >= 0) dbase[(long)(aj0 + ll) * pstep] = (int16_t)dacc;
             }
         };
         Sg ga, gb;
@@ -849,35 +914,49 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
     }
 }
 
-template <int MODE, bool FULL>
-static void launch_ck_m(const SgmArgs& a, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((k_sgm_ck<SM_SGM_CK_S, MODE, FULL>), grid, dim3(256), 0, st, a);
-}
-template <bool FULL, int SGN>
-static void launch_ck_f(const SgmArgs& a, int mode, dim3 grid, hipStream_t st) {
-    switch (mode) {
-        case CK_A: return launch_ck_m<SGN | CK_A, FULL>(a, grid, st);
-        case CK_B: return launch_ck_m<SGN | CK_B, FULL>(a, grid, st);
-        case CK_B | SGM_LAST: return launch_ck_m<SGN | CK_B | SGM_LAST, FULL>(a, grid, st);
-        default: return launch_ck_m<SGN | CK_B | SGM_LAST | SGM_KEEP, FULL>(a, grid, st);
+template <int S, int MODE, int KV, bool ROWS, bool FULL>
+static void launch_ck_one(const SgmArgs& a, hipStream_t st) {
+    const int nl = a.rv == 0 ? a.H : a.W;
+    if (ROWS) {
+        const int waves = (nl + 3) / 4 * a.n;
+        hipLaunchKernelGGL((k_sgm_ck<S, MODE, KV, ROWS, FULL>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL((k_sgm_ck<S, MODE, KV, ROWS, FULL>), dim3((nl + 3) / 4, a.n), dim3(256), 0, st, a);
     }
 }
+template <int S, int KV, bool ROWS, bool FULL, int SGN>
+static void launch_ck_f(const SgmArgs& a, int mode, hipStream_t st) {
+    switch (mode) {
+        case CK_A: return launch_ck_one<S, SGN | CK_A, KV, ROWS, FULL>(a, st);
+        case CK_B: return launch_ck_one<S, SGN | CK_B, KV, ROWS, FULL>(a, st);
+        case CK_B | CK_MID: return launch_ck_one<S, SGN | CK_B | CK_MID, KV, ROWS, FULL>(a, st);
+        case CK_B | SGM_LAST: return launch_ck_one<S, SGN | CK_B | SGM_LAST, KV, ROWS, FULL>(a, st);
+        default: return launch_ck_one<S, SGN | CK_B | SGM_LAST | SGM_KEEP, KV, ROWS, FULL>(a, st);
+    }
+}
+template <int S, int KV, bool ROWS, bool FULL>
+static void launch_ck_s(const SgmArgs& a, int mode, hipStream_t st) {
+    if (a.signed_costs)
+        launch_ck_f<S, KV, ROWS, FULL, SGM_SIGNED>(a, mode, st);
+    else
+        launch_ck_f<S, KV, ROWS, FULL, 0>(a, mode, st);
+}
+// mode: CK_A, CK_B (acc = L_first + L_second), CK_B | CK_MID (8 paths: acc = (acc + L2) + L3),
+// CK_B | SGM_LAST (the map; SGM_KEEP added here when the final volume is kept)
 void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st) {
     SgmArgs b = a;
     b.n = n;
-    const int nlines = a.rv == 0 ? a.H : a.W;
-    const dim3 grid((nlines + 3) / 4, n);
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
-    if (a.signed_costs) {
-        if (a.D == 256)
-            launch_ck_f<true, SGM_SIGNED>(b, mode, grid, st);
-        else
-            launch_ck_f<false, SGM_SIGNED>(b, mode, grid, st);
-    } else {
-        if (a.D == 256)
-            launch_ck_f<true, 0>(b, mode, grid, st);
-        else
-            launch_ck_f<false, 0>(b, mode, grid, st);
+    switch (ck_kv(a.D)) {
+        case 0:
+            if (a.D == 256) return launch_ck_s<SM_SGM_CK_S, 1, false, true>(b, mode, st);
+            return launch_ck_s<SM_SGM_CK_S, 1, false, false>(b, mode, st);
+        case 1:
+            if (a.D == 64) return launch_ck_s<SM_SGM_CK_S, 1, true, true>(b, mode, st);
+            return launch_ck_s<SM_SGM_CK_S, 1, true, false>(b, mode, st);
+        default:
+            if (a.D == 128) return launch_ck_s<SM_SGM_CK_S2, 2, true, true>(b, mode, st);
+            return launch_ck_s<SM_SGM_CK_S2, 2, true, false>(b, mode, st);
     }
 }
 

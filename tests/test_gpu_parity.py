@@ -290,21 +290,25 @@ def test_shapes_and_edge_cases(oracle, H, W, md, paths):
     np.testing.assert_array_equal(dp, ref["disp"])
 
 
-@pytest.mark.parametrize("H,W,md", [(2, 2, 131), (2, 9, 255), (8, 8, 199), (9, 17, 255), (16, 24, 131),
-                                     (17, 33, 255), (23, 7, 199), (40, 41, 255)])
-def test_sgm_checkpointed_pairs(oracle, H, W, md):
-    """4-path SGM with 128 < D <= 256, D % 4 == 0 runs as two checkpointed path pairs (k_sgm_ck,
-    segments of 8 steps): lines shorter than, equal to and one longer than a segment, ragged
-    tails, D below 256; the summed volume (keep_final) and the map bit-exact, and the map again
-    through the batch path (no final volume)."""
+@pytest.mark.parametrize("H,W,md,paths", [(2, 2, 131, 4), (2, 9, 255, 4), (8, 8, 199, 4), (9, 17, 255, 4),
+                                           (16, 24, 131, 4), (17, 33, 255, 4), (23, 7, 199, 4), (40, 41, 255, 4),
+                                           (9, 17, 63, 4), (17, 10, 127, 4), (8, 8, 99, 4), (16, 9, 59, 4),
+                                           (5, 13, 3, 4), (12, 19, 255, 8), (10, 11, 63, 8), (9, 9, 119, 8)])
+def test_sgm_checkpointed_pairs(oracle, H, W, md, paths):
+    """SGM with D % 4 == 0 runs paths 0 / 1 and 2 / 3 as checkpointed pairs (k_sgm_ck: segments of
+    8 steps, 4 with 8 disparities per lane): one line per wave for 128 < D <= 256, four lines
+    per wave below; lines shorter than, equal to and one longer than a segment, ragged tails, D
+    below the layout's full width, 8 paths (the second pair adds into the running sum, paths
+    4 .. 7 follow as sweeps).  The summed volume (keep_final) and the map bit-exact, and the map
+    again through the batch path (no final volume)."""
     pair = S.make_pair(H, W, md + 1, 50 + H + W)
-    cfg = oracle.config(H, W, md, sgm_paths=4)
+    cfg = oracle.config(H, W, md, sgm_paths=paths)
     ref = oracle.run(pair, cfg, dumps=True)
-    _, agg, final, dp = run_reference_order(pair, md, paths=4)
+    _, agg, final, dp = run_reference_order(pair, md, paths=paths)
     np.testing.assert_array_equal(bits(agg), bits(ref["agg"]))
     np.testing.assert_array_equal(bits(final), bits(ref["final"]))
     np.testing.assert_array_equal(dp, ref["disp"])
-    sb = StereoBatch(md, H, W, 2, sgm_paths=4)
+    sb = StereoBatch(md, H, W, 2, sgm_paths=paths)
     sb.upload(*(np.stack([pair[k], pair[k]]) for k in ("lbgr", "rbgr", "lgray", "rgray")))
     disp = sb.run(0.3)
     sb.close()

@@ -89,8 +89,16 @@ struct sm_ctx {
     int* nl_offs = nullptr;                 // round offsets + error flags (device)
     int* nl_offs_h = nullptr;               // the same, page-locked host copy
     int nl_set = 0;                         // record / table set of the next call (double-buffered)
+    int nl_opt_set = 0;                     // pipelined NL: the set the current call's optimiser reads
     hipStream_t nl_st = nullptr;        // NL front (median, edge weights, spanning trees, tree walk)
     hipEvent_t nl_ev_set[2] = {nullptr, nullptr};   // the last filter reading each record / table set (on c->st)
+    // pipelined NL front (sm_run with NL + SGM, one view): the call's prep and cost volume also run
+    // on nl_st, into a cost volume and penalty flags of the call's set, so they overlap the
+    // previous call's filter and SGM on c->st
+    bool nl_pipe = false;
+    float* nl_vc = nullptr;                 // [2][cap][nvol] cost volumes (filter input)
+    uint8_t* nl_fl = nullptr;               // [2][cap][npix] SGM penalty flags
+    hipEvent_t nl_ev_opt[2] = {nullptr, nullptr};   // the last optimiser reading each set (on c->st)
     double* nl_table = nullptr; // [256]
     double* nl_val = nullptr;   // [cap][nvol]
     double* nl_oup = nullptr;   // [cap][npix] the ones channel: up sums
@@ -109,6 +117,7 @@ struct sm_ctx {
     hipEvent_t ev_run = nullptr, ev_copy = nullptr;     // run done (c->st) / async copy done (cst)
     bool copy_pending = false;  // an async copy may still read the maps
     std::vector<hipEvent_t> xev;                        // stagger / join events
+    hipEvent_t stagger_ev = nullptr;                    // SM_STAGGER_STAGE 1: recorded after the first CBCA sweep
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
@@ -314,7 +323,7 @@ void free_all(sm_ctx* c) {
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
                     c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
                     c->nl_table, c->nl_val, c->nl_oup, c->nl_ofin, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->nl_walk,
-                    c->nl_offs, c->luts};
+                    c->nl_offs, c->luts, c->nl_vc, c->nl_fl};
     for (void* q : ptrs)
         if (q) hipFree(q);
     if (c->nl_st) {
@@ -322,12 +331,13 @@ void free_all(sm_ctx* c) {
         hipStreamDestroy(c->nl_st);
         c->nl_st = nullptr;
     }
-    for (hipEvent_t& e : c->nl_ev_set)
-        if (e) {
-            hipEventSynchronize(e);
-            hipEventDestroy(e);
-            e = nullptr;
-        }
+    for (hipEvent_t* ev : {c->nl_ev_set, c->nl_ev_opt})
+        for (int i = 0; i < 2; i++)
+            if (ev[i]) {
+                hipEventSynchronize(ev[i]);
+                hipEventDestroy(ev[i]);
+                ev[i] = nullptr;
+            }
     if (c->nl_offs_h) {
         hipHostFree(c->nl_offs_h);
         c->nl_offs_h = nullptr;
@@ -505,6 +515,10 @@ sm_status run_cbca(sm_ctx* c, int n, int view, bool fuse_scale, float w, const B
     auto nm = [&](const char* base) { static thread_local std::string t; t = std::string(base) + sfx; return t.c_str(); };
     sm_status s = timed(c, nm("cbca_h_scan"), bytes, [&] { sm::launch_cbca(a, true, sm::CB_SCAN, n, c->st); });
     if (s) return s;
+    if (c->stagger_ev) {   // the next group may start: this group's next sweep is LDS- and issue-bound
+        HIP_TRY(c, hipEventRecord(c->stagger_ev, c->st));
+        c->stagger_ev = nullptr;
+    }
     for (int k = 0; k < N; k++) {
         const bool dir_h = (k % 2 == 1);  // direction of iteration k's second pass
         a.div_safe = cbca_div_safe(p, k) ? 1 : 0;   // this step's normalisation is iteration k's
@@ -584,8 +598,11 @@ sm_status run_gf(sm_ctx* c, int n, int view, const Bufs& B, bool solve_all, floa
 }
 
 // NL() on vm[0] (cpp:4892-4917): edge weights, spanning trees, the tree walk and the tree filter,
+#ifndef SM_NL_PIPE
+#define SM_NL_PIPE 1   // sm_run: NL's prep and cost volume on the front stream (A/B switch)
+#endif
 // all on the GPU (sm_nl.hip, sm_nl_mst.hip, sm_nl_walk.hip)
-sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
+sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w, Bufs* pipe = nullptr) {
     const size_t off = (size_t)(B.vm0 - c->vm0) / c->nvol, np = c->npix;
     const int H = c->p.rows, W = c->p.cols, D = c->p.num_disparities;
     const size_t ne = (size_t)H * (W - 1) + (size_t)(H - 1) * W;
@@ -598,10 +615,11 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     // only for the filter that last read the set it writes.
     if (!c->nl_st) {
         HIP_TRY(c, hipStreamCreateWithFlags(&c->nl_st, hipStreamNonBlocking));
-        for (hipEvent_t& e : c->nl_ev_set) {
-            HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HIP_TRY(c, hipEventRecord(e, c->st));
-        }
+        for (hipEvent_t* ev : {c->nl_ev_set, c->nl_ev_opt})
+            for (int i = 0; i < 2; i++) {
+                HIP_TRY(c, hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+                HIP_TRY(c, hipEventRecord(ev[i], c->st));
+            }
     }
     const int set = c->nl_set;
     c->nl_set ^= 1;
@@ -616,6 +634,16 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
             ~Swap() { c->st = keep; }
         } sw{c, c->st};
         c->st = c->nl_st;
+        if (pipe) {
+            // this call's prep and cost volume, into the set's flags and cost volume: the set was
+            // last read by the optimiser two calls back (its filter read the cost volume before)
+            *pipe = B;
+            pipe->vm0 = c->nl_vc + ((size_t)set * c->cap + off) * c->nvol;
+            pipe->flags = c->nl_fl + ((size_t)set * c->cap + off) * np;
+            HIP_TRY(c, hipStreamWaitEvent(c->st, c->nl_ev_opt[set], 0));
+            if ((s = run_prep(c, n, *pipe))) return s;
+            if ((s = run_cost(c, n, 0, *pipe))) return s;
+        }
         s = timed(c, "nl_edges", (double)n * np * 4, [&] {
             sm::launch_nl_edges(B.bgr, 2 * np * 3, c->nl_med + off * np * 3, c->nl_ew + off * ne, H, W, n, c->st);
         });
@@ -650,6 +678,7 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     a.table = c->nl_table;
     a.val = c->nl_val;
     a.vm = B.vm0;
+    a.vc = pipe ? pipe->vm0 : B.vm0;
     a.oup = c->nl_oup;
     a.ofin = c->nl_ofin;
     a.nodes = (long)n * (long)np;
@@ -665,6 +694,10 @@ sm_status run_nl(sm_ctx* c, int n, const Bufs& B, bool solve_all, float w) {
     });
     if (s) return s;
     HIP_TRY(c, hipEventRecord(c->nl_ev_set[set], c->st));
+    if (pipe) {   // the optimiser reads the final volume (vm[0]) and this set's flags
+        pipe->vm0 = B.vm0;
+        c->nl_opt_set = set;
+    }
     return SM_OK;
 }
 
@@ -1011,6 +1044,12 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->nl_best, cap * c->npix))) return s;
         if ((s = dalloc(c, &c->nl_mst, sm::nl_mst_scratch_bytes(p->rows, p->cols, cap)))) return s;
         if ((s = dalloc(c, &c->nl_adj, cap * c->npix))) return s;
+        // sm_run's pipelined front (one view, SGM): two sets of cost volume and penalty flags
+        c->nl_pipe = SM_NL_PIPE && p->optimization == SM_OPT_SGM && !right_view(*p);
+        if (c->nl_pipe) {
+            if ((s = dalloc(c, &c->nl_vc, 2 * cap * c->nvol + vpad))) return s;
+            if ((s = dalloc(c, &c->nl_fl, 2 * cap * c->npix))) return s;
+        }
         double table[256];
         const double sg = p->nl_sigma < 0.01 ? 0.01 : p->nl_sigma;   // update_table (qx_tree_filter.cpp:23-24)
         for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));
@@ -1311,6 +1350,9 @@ sm_status sm_upload_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8
     return upload(c, n, lbgr, rbgr, (size_t)c->p.cols * 3, lgray, rgray, (size_t)c->p.cols);
 }
 
+#ifndef SM_STAGGER_STAGE
+#define SM_STAGGER_STAGE 0
+#endif
 sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
@@ -1325,6 +1367,10 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     // previous one; the main stream joins every stream at the end.
     const int g = c->sub_batch > 0 ? c->sub_batch : n;
     const int ns = c->nstreams;
+    // where group k + 1 starts: 0 = after group k's CBCA, 1 = after group k's first CBCA sweep
+    // (with CBCA; then the next group's prep, cost and first sweep share the CUs with this
+    // group's LDS-bound NORM_SCAN sweep)
+    const bool early = SM_STAGGER_STAGE == 1 && c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0;
     hipStream_t main_st = c->st;
     int k = 0;
     sm_status s_out = SM_OK;
@@ -1341,11 +1387,18 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
             s_out = hip_fail(c, e, "hipStreamWaitEvent (group stagger)");
             break;
         }
-        if ((s_out = run_prep(c, m2, B))) break;
-        if ((s_out = run_cost(c, m2, 0, B))) break;
-        if (right_view(c->p) && (s_out = run_cost(c, m2, 1, B))) break;
-        if ((s_out = run_other_agg(c, m2, B, SM_FUSE_SOLVE_ALL, w))) break;   // SolveAll fused into GF / NL
-        for (int v = 0; v < n_views(c->p) && !s_out; v++) {
+        Bufs Bo = B;   // what the optimiser reads
+        const bool pipe = c->nl_pipe && m2 == n && ns == 1 && SM_FUSE_SOLVE_ALL;
+        if (pipe) {   // prep, cost volume and trees on the NL front stream (run_nl)
+            if ((s_out = run_nl(c, m2, B, true, w, &Bo))) break;
+        } else {
+            if ((s_out = run_prep(c, m2, B))) break;
+            if ((s_out = run_cost(c, m2, 0, B))) break;
+            if (right_view(c->p) && (s_out = run_cost(c, m2, 1, B))) break;
+            if ((s_out = run_other_agg(c, m2, B, SM_FUSE_SOLVE_ALL, w))) break;   // SolveAll fused into GF / NL
+        }
+        if (ns > 1 && early) c->stagger_ev = c->xev[1 + k % 8];
+        for (int v = 0; v < n_views(c->p) && !s_out && !pipe; v++) {
             if (c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0)
                 s_out = run_cbca(c, m2, v, true, w, B);   // SolveAll fused into the last pass
             else if (!SM_FUSE_SOLVE_ALL || !(c->p.aggregation == SM_AGG_GF || (c->p.aggregation == SM_AGG_NL && v == 0)))
@@ -1358,15 +1411,21 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
             s_out = hip_fail(c, e, "hipStreamWaitEvent (async map copy)");
             break;
         }
-        if (ns > 1 && (e = hipEventRecord(c->xev[1 + k % 8], c->st)) != hipSuccess) {
+        c->stagger_ev = nullptr;
+        if (ns > 1 && !early && (e = hipEventRecord(c->xev[1 + k % 8], c->st)) != hipSuccess) {
             s_out = hip_fail(c, e, "hipEventRecord (group CBCA done)");
             break;
         }
-        for (int v = 0; v < opt_views(c->p) && !s_out; v++) s_out = run_optimize(c, m2, v, B);
+        for (int v = 0; v < opt_views(c->p) && !s_out; v++) s_out = run_optimize(c, m2, v, Bo);
         if (s_out) break;
+        if (pipe && (e = hipEventRecord(c->nl_ev_opt[c->nl_opt_set], c->st)) != hipSuccess) {
+            s_out = hip_fail(c, e, "hipEventRecord (NL set released)");
+            break;
+        }
         if (c->p.do_refine && (s_out = run_refine(c, m2, B))) break;
     }
     c->st = main_st;
+    c->stagger_ev = nullptr;
     if (ns > 1) {   // the join runs on the error path too: nothing stays queued behind the main stream
         for (int i = 0; i + 1 < ns; i++) {
             hipError_t e = hipEventRecord(c->xev[9 + i], c->xst[i]);

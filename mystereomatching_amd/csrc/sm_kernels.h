@@ -135,7 +135,8 @@ struct NlArgs {                 // non-local tree filter (sm_nl.hip); node ids =
     const int* order_down;      // path indices sorted by down round
     const double* table;        // exp(-i / (255 sigma)), i = 0..255
     double* val;                // [nodes][D] up sums, then final values (in place)
-    float* vm;                  // [nodes][D] costs in, normalised aggregated costs out
+    float* vm;                  // [nodes][D] normalised aggregated costs out
+    const float* vc;            // [nodes][D] costs in (vm itself, or the pipelined front's volume)
     int solve_all;              // 1: vm out is SolveAll's `0 + w * v` (cpp:2189-2201), w = scale
     float scale;
     double* oup;                // [nodes] the ones volume's up sums (qx_tree_filter on ones)

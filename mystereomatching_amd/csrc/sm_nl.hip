@@ -152,7 +152,7 @@ __device__ __forceinline__ void nl_up_load(NlUpBlock<K>& B, const NlArgs& a, con
 #pragma unroll
         for (int j = 0; j < 4; j++) B.lm[k][j] = B.lo[k][j] = 0.0;
         if (b + k >= len) continue;                     // no loads past the path
-        B.cost[k] = a.vm[(size_t)r.x * P + d];
+        B.cost[k] = a.vc[(size_t)r.x * P + d];
 #pragma unroll
         for (int j = 0; j < 4; j++)
             if (j < nc && j != hv) {
@@ -448,7 +448,7 @@ __device__ __forceinline__ void nl_up_producer(PcUpSlot* S, const NlArgs& a, con
 #pragma unroll
             for (int j = 0; j < 4; j++) xm[kk][j] = 0.0;
             if (c * PC_C + k >= len) continue;
-            if (dok) xc[kk] = a.vm[(size_t)x * P + d];
+            if (dok) xc[kk] = a.vc[(size_t)x * P + d];
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if (j < nc && j != hv && dok) xm[kk][j] = a.val[(size_t)nl_child(x, meta, j, a.W) * P + d];

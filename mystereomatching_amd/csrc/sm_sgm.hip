@@ -826,6 +826,10 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
                 if (ACC_IN) ldK(g.acc[s], ald, off);
             }
             ldK(g.ck, ckl, (long)(k < nseg - 1 ? k : 0) * D);
+            // chunks past D: checkpoints are only stored inside D, and those lanes must hold
+            // FLT_MAX (the d + 1 neighbour of the last disparity) as in pass A
+#pragma unroll
+            for (int q = 0; q < K; q++) g.ck[q] = (FULL || st.cv[q / 4]) ? g.ck[q] : FLT_MAX;
             g.fl = flag_of(aj0);
         };
         float Lp[K];

@@ -118,8 +118,12 @@ typedef struct sm_params {
     int32_t do_last_median_blur; /* Do_lastMedianBlur = 1 (h:80) */
     /* scheduling of sm_run (results are identical for every setting): */
     int32_t sub_batch;           /* run the n pairs in groups of k (0 = one group), stages back to back */
-    int32_t num_streams;         /* 0/1: one stream; 2-4: groups alternate over that many streams,
-                                  * group k + 1 starting once group k's CBCA is done */
+    int32_t num_streams;         /* 0 (default): auto -- with CBCA and a volume >= 256 MiB per pair, two
+                                  * streams and (sub_batch 0) two groups of n / 2 pairs, each group
+                                  * starting after the previous one's first CBCA sweep; else one
+                                  * stream; 1: one stream; 2-4: groups alternate over that many
+                                  * streams (group k + 1 starts after group k's first CBCA sweep, or
+                                  * its aggregation without CBCA) */
     int32_t fuse_norm_scan;      /* CBCA: iteration k's normalising sweep fused with iteration k+1's
                                   * scan (one sweep, 8 B per element less): 1 = always, 0 = never,
                                   * -1 (default) = when the dedicated sweep for the reference's lag

@@ -474,6 +474,9 @@ struct CbLine {
 #ifndef SM_CB_NSV
 #define SM_CB_NSV 1   // 0: the generic REUSE2 sweep (A/B builds)
 #endif
+#ifndef SM_CB_NSV_AH
+#define SM_CB_NSV_AH 1   // 1: the scan stage reads at the norm stage's saved addresses (S2 at slot p mod R)
+#endif
 constexpr int NSV_LAG = 34;
 constexpr int cbca_nsv_ring() { return (2 * NSV_LAG + SM_CB_T_NSV + 1 + SM_CB_T_NSV - 1) / SM_CB_T_NSV * SM_CB_T_NSV; }
 constexpr int cbca_nsv_phys() { return cbca_nsv_ring() + SM_CB_T_NSV - 1; }
@@ -521,7 +524,15 @@ struct NsV {
     float S1, S2;
     uint32_t Acc;
     int ws;                   // ring slot of the tile's first input row (multiple of T)
+#if SM_CB_NSV_AH
+    // S2 holds position p at slot p mod R like S1, so the scan stage's window at i2 = j - 2 LAG
+    // sits at the very slots the norm stage's window at i = (j - LAG) - LAG read LAG positions
+    // earlier: the history keeps those S1 read addresses (head, tail) of the last NH tiles, and
+    // the scan stage reads S2 at them plus the ring distance, with no slot arithmetic of its own
+    uint32_t hh[NH][T], ht[NH][T];
+#else
     uint32_t ph[NH][T];       // pass intersections of the last NH tiles (slot = tile index mod NH)
+#endif
 
     // loads the next tile (tiles are loaded in order, T rows apart)
     __device__ __forceinline__ void load(Tile& t) {
@@ -558,6 +569,123 @@ struct NsV {
         buf_st(r, xo[k], 0, v);
     }
 
+#if SM_CB_NSV_AH
+    // One code copy for every tile: the two line ends differ only in uniform branches around the
+    // zeroing of pre-line inputs and the stores' offsets, so the saved addresses need no copies
+    // at a merge of two tile variants.
+    template <int RT>   // RT: the tile's slot in the NH-tile loop
+    __device__ __forceinline__ void tile(const Tile& t, int j0, bool guard) {
+        const int C = ws - LAG < 0 ? ws - LAG + R : ws - LAG;   // ring slot of output row i0 = j0 - LAG
+        const uint32_t cc = ((uint32_t)(C - 1) & 0xffffu) | ((uint32_t)C << 16);
+        const bool mirror = ws == 0;
+        float* w1 = r1 + ws * 64 + lane;
+        uint16_t* wa = ra + ws * 64 + lane;
+        // phase A: rows j0 .. j0+T-1 into the S1 / area rings; pass intersections at i = j - LAG
+        uint32_t pi[T];
+        float s1v[T];
+        uint16_t acv[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            S1 = S1 + t.x[k];
+            s1v[k] = S1;
+            w1[k * 64] = S1;
+            pi[k] = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[0], k), t.a1[0][k]);
+            const uint32_t pp = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[1], k), t.a1[1][k]);
+            Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
+            acv[k] = (uint16_t)Acc;
+            wa[k * 64] = acv[k];
+        }
+        if (mirror) {
+#pragma unroll
+            for (int k = 0; k < T - 1; k++) {
+                r1[(R + k) * 64 + lane] = s1v[k];
+                ra[(R + k) * 64 + lane] = acv[k];
+            }
+        }
+        // phase B: normalised outputs at i = j - LAG; their prefix S2 (iteration k+1's scan input)
+        const __amdgpu_buffer_rsrc_t ob2 = buf_rsrc(xst);
+        xst += (long)T * (long)vsb;
+        typedef __attribute__((address_space(3))) const float lds_f;
+        typedef __attribute__((address_space(3))) const uint16_t lds_h;
+        float qv[T], dv[T], shv[T], stv[T];
+        uint32_t ahv[T], atv[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            const uint32_t sp = slots(pi[k], cc);
+            const uint32_t a1h = mad_u32_u16<1>(sp, 256u, o1), a1t = mad_u32_u16<0>(sp, 256u, o1);
+            hh[RT][k] = a1h;
+            ht[RT][k] = a1t;
+            shv[k] = ((lds_f*)(size_t)a1h)[k * 64];
+            stv[k] = ((lds_f*)(size_t)a1t)[k * 64];
+            ahv[k] = rd<1, uint16_t>(sp, oa, k);
+            atv[k] = rd<0, uint16_t>(sp, oa, k);
+        }
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            dv[k] = shv[k] - stv[k];
+            qv[k] = div_area(dv[k], (ahv[k] - atv[k]) & 0xffffu);
+        }
+        if constexpr (CHECK) {
+            // dividends are >= +0, so "0 < dv < 2^-110" is "bits(dv) - 1 < 0x087fffff" (unsigned)
+            uint32_t tmin = 0xffffffffu;
+#pragma unroll
+            for (int k = 0; k < T; k++) tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
+            if (__ballot(tmin < 0x087fffffu)) {
+#pragma unroll
+                for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)((ahv[k] - atv[k]) & 0xffffu);
+            }
+        }
+        // S2 of positions i0 .. i0+T-1 at slots C .. C+T-1 (C + k may pass R: the mirror slots;
+        // a logical slot below T - 1 is kept in both copies)
+        float s2v[T];
+        float* w2 = r2 + C * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            float y = qv[k];
+            if (guard) y = (j0 - LAG + k >= 0) ? y : 0.f;   // nothing accumulates before the line
+            S2 = S2 + y;
+            s2v[k] = S2;
+            w2[k * 64] = S2;
+        }
+        if (C + T - 1 >= R || C <= T - 2) {   // two of the R / T tile positions
+#pragma unroll
+            for (int k = 0; k < T; k++) {
+                if (C + k >= R) r2[(C + k - R) * 64 + lane] = s2v[k];
+                if (C + k <= T - 2) r2[(C + k + R) * 64 + lane] = s2v[k];
+            }
+        }
+        // phase C: scan outputs at i2 = j - 2 LAG, read at the norm stage's S1 addresses of
+        // position j - LAG (tile RT + dt, index q - dt T) plus the ring distance P slots
+        float s2h[T], s2t[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            const int q = k - LAG;
+            const int dt = -((-q + T - 1) / T);
+            const int src = (RT + dt + 4 * NH) % NH, idx = q - dt * T;
+            s2h[k] = ((lds_f*)(size_t)hh[src][idx])[(idx + P) * 64];
+            s2t[k] = ((lds_f*)(size_t)ht[src][idx])[(idx + P) * 64];
+        }
+        // (outside the line: an out-of-range offset; both branches issue the same vector-memory
+        // sequence, so the loop's vmcnt waits stay exact)
+        if (guard) {
+#pragma unroll
+            for (int k = 0; k < T; k++) {
+                const bool in = (unsigned)(j0 - 2 * LAG + k) < (unsigned)len;
+                buf_st(ob2, in ? xo[k] : 0x80000000u, 0, s2h[k] - s2t[k]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < T; k++) buf_st(ob2, xo[k], 0, s2h[k] - s2t[k]);
+        }
+        ws = ws + T == R ? 0 : ws + T;
+    }
+
+    template <int RT>
+    __device__ __forceinline__ void process(const Tile& t, int j0) {
+        // (stage-1 outputs past the line end only feed S2 positions no stored window reaches)
+        tile<RT>(t, j0, !(j0 - 2 * LAG >= 0 && j0 + T - 1 - 2 * LAG < len));
+    }
+#else
     template <bool GUARD, int RT>   // RT: the tile's slot in the NH-tile loop
     __device__ __forceinline__ void tile(const Tile& t, int j0) {
         const int C = ws - LAG < 0 ? ws - LAG + R : ws - LAG;   // ring slot of output row i0 = j0 - LAG
@@ -670,6 +798,8 @@ struct NsV {
         else
             tile<true, RT>(t, j0);
     }
+#endif
+
 };
 
 template <bool RV, bool CHECK>
@@ -729,7 +859,13 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
 #pragma unroll
     for (int r = 0; r < L_t::NH; r++)
 #pragma unroll
-        for (int k = 0; k < T; k++) L.ph[r][k] = 0u;
+        for (int k = 0; k < T; k++) {
+#if SM_CB_NSV_AH
+            L.hh[r][k] = L.ht[r][k] = L.o1;   // rows before the line: any in-ring address (outputs < 0 are not stored)
+#else
+            L.ph[r][k] = 0u;
+#endif
+        }
     __syncthreads();
     L.S1 = L.S2 = 0.f;
     L.Acc = 0;

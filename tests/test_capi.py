@@ -57,7 +57,7 @@ def test_params_struct_layout_and_defaults():
     assert (p.do_refine, p.lr_max_diff, p.do_region_vote, p.region_vote_nums, p.rv_s) == (0, 0.0, 1, 2, 20)
     assert (p.do_proper_ipol, p.disp_occ, p.do_last_median_blur) == (1, -32, 1)
     assert np.float32(p.rv_ratio) == np.float32(0.4)
-    assert (p.sub_batch, p.num_streams, p.fuse_norm_scan) == (0, 1, -1)
+    assert (p.sub_batch, p.num_streams, p.fuse_norm_scan) == (0, 0, -1)
     assert np.float32(p.gf_eps) == np.float32(1e-4) and p.nl_sigma == 0.1
     assert p.gf_mode == 0   # SM_GF_XIMGPROC: the shipped build (`//#define MY_GUIDE`, h:38)
     assert p.struct_size == C.sizeof(_capi.sm_params)

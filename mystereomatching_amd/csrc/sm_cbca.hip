@@ -639,11 +639,13 @@ struct NsV {
         // a logical slot below T - 1 is kept in both copies)
         float s2v[T];
         float* w2 = r2 + C * 64 + lane;
+        if (guard) {   // nothing accumulates before the line (one uniform branch per tile)
+#pragma unroll
+            for (int k = 0; k < T; k++) qv[k] = (j0 - LAG + k >= 0) ? qv[k] : 0.f;
+        }
 #pragma unroll
         for (int k = 0; k < T; k++) {
-            float y = qv[k];
-            if (guard) y = (j0 - LAG + k >= 0) ? y : 0.f;   // nothing accumulates before the line
-            S2 = S2 + y;
+            S2 = S2 + qv[k];
             s2v[k] = S2;
             w2[k * 64] = S2;
         }
@@ -835,8 +837,10 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
 #pragma unroll
     for (int s = 0; s < 2; s++) {
         const int pl = s == 0 ? 1 : 0;   // V sweeps: pass pair = (U | D) plane 1, perpendicular = plane 0
-        L.A0r[s] = buf_rsrc((const char*)(a.arms + ((size_t)b * 4 + own + pl) * npix + u) - pad, 0x7fffffff);
-        L.A1r[s] = buf_rsrc((const char*)(a.arms + ((size_t)b * 4 + other + pl) * npix) - pad, 0x7fffffff);
+        // (distinct, all effectively unbounded ranges: with one shared upper half the compiler
+        // re-forms the four descriptors from it with s_mov pairs in every tile)
+        L.A0r[s] = buf_rsrc((const char*)(a.arms + ((size_t)b * 4 + own + pl) * npix + u) - pad, 0x7fffffff - 2 * s);
+        L.A1r[s] = buf_rsrc((const char*)(a.arms + ((size_t)b * 4 + other + pl) * npix) - pad, 0x7ffffffe - 2 * s);
     }
     L.aown = L.lane < T ? (uint32_t)L.lane * L.rowb : 0x80000000u;
     {

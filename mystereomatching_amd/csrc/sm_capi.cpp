@@ -1070,9 +1070,12 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         c->sub_batch = p->sub_batch;
         // num_streams 0 (auto): two streams with CBCA at volumes >= 256 MiB per pair, where the
         // next group's prep, cost and H scan share the CUs with this group's LDS-bound NORM_SCAN
-        // sweep (full resolution 37.8 -> 36.0 ms, 1080p x8 53.0 -> 50.3 ms, profiles/r4j)
+        // sweep (full resolution 37.8 -> 36.0 ms, 1080p x8 53.0 -> 50.3 ms, profiles/r4j); and for
+        // batches of >= 8 smaller pairs with 4-path SGM and no refinement (Teddy x16 in two groups
+        // of 8: 2.60 -> 2.54 ms, profiles/r4q; KITTI's 8-path SGM got slower, 8.27 -> 8.52 ms)
         c->auto_groups = p->num_streams == 0 && p->aggregation == SM_AGG_CBCA && p->cbca_iterations > 0 &&
-                         c->nvol * 4 >= ((size_t)1 << 28);
+                         (c->nvol * 4 >= ((size_t)1 << 28) ||
+                          (cap >= 8 && p->optimization == SM_OPT_SGM && p->sgm_paths == 4 && !p->do_refine));
         c->nstreams = c->auto_groups ? 2 : (p->num_streams < 1 ? 1 : p->num_streams);
         for (int i = 0; i + 1 < c->nstreams; i++) HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking));
         for (int i = 0; i < 16; i++) {

@@ -477,9 +477,6 @@ struct CbLine {
 #ifndef SM_CB_NSV_AH
 #define SM_CB_NSV_AH 1   // 1: the scan stage reads at the norm stage's saved addresses (S2 at slot p mod R)
 #endif
-#ifndef SM_CB_NSV_RB
-#define SM_CB_NSV_RB 0   // 1: volume load / store descriptors rebased once per six-tile loop trip (A/B)
-#endif
 constexpr int NSV_LAG = 34;
 constexpr int cbca_nsv_ring() { return (2 * NSV_LAG + SM_CB_T_NSV + 1 + SM_CB_T_NSV - 1) / SM_CB_T_NSV * SM_CB_T_NSV; }
 constexpr int cbca_nsv_phys() { return cbca_nsv_ring() + SM_CB_T_NSV - 1; }
@@ -535,37 +532,6 @@ struct NsV {
     uint32_t hh[NH][T], ht[NH][T];
 #else
     uint32_t ph[NH][T];       // pass intersections of the last NH tiles (slot = tile index mod NH)
-#endif
-
-#if SM_CB_NSV_RB
-    // SM_CB_NSV_RB: the volume's load / store descriptors of a loop trip (six tiles), built once
-    // per trip; a tile's rows sit at a uniform soffset r * T * vsb above the trip's first
-    __amdgpu_buffer_rsrc_t rxi, obi;
-    uint32_t soffs[NH];
-    // the trip's load descriptor: rows from jld, the range ending at the allocation (rows past
-    // it read 0); its store descriptor: outputs from row j0 - 2 LAG of the trip's first tile
-    __device__ __forceinline__ void rebase() {
-        const long rows = (long)rows_avail - (long)jld;
-        const long room = rows <= 0 ? 0 : rows * (long)vsb;
-        rxi = buf_rsrc(xld, room > 0x7fffffffL ? 0x7fffffff : (int)room);
-        xld += (long)(NH * T) * (long)vsb;
-        obi = buf_rsrc(xst);
-        xst += (long)(NH * T) * (long)vsb;
-    }
-    template <int R_>
-    __device__ __forceinline__ void load_rb(Tile& t) {
-#pragma unroll
-        for (int k = 0; k < T; k++) t.x[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)xo[k], (int)soffs[R_], 2));
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const uint32_t roff = s == 0 ? rld - (uint32_t)LAG * rowb : rld;
-            t.a0[s] = __builtin_amdgcn_raw_buffer_load_b32(A0r[s], (int)aown, (int)roff, 0);
-#pragma unroll
-            for (int k = 0; k < T; k++) t.a1[s][k] = __builtin_amdgcn_raw_buffer_load_b32(A1r[s], (int)ao[k], (int)roff, 0);
-        }
-        jld += T;
-        rld += (uint32_t)T * rowb;
-    }
 #endif
 
     // loads the next tile (tiles are loaded in order, T rows apart)
@@ -637,14 +603,8 @@ struct NsV {
             }
         }
         // phase B: normalised outputs at i = j - LAG; their prefix S2 (iteration k+1's scan input)
-#if SM_CB_NSV_RB
-        const __amdgpu_buffer_rsrc_t ob2 = obi;
-        const uint32_t so2 = soffs[RT];
-#else
         const __amdgpu_buffer_rsrc_t ob2 = buf_rsrc(xst);
         xst += (long)T * (long)vsb;
-        const uint32_t so2 = 0;
-#endif
         typedef __attribute__((address_space(3))) const float lds_f;
         typedef __attribute__((address_space(3))) const uint16_t lds_h;
         float qv[T], dv[T], shv[T], stv[T];
@@ -713,11 +673,11 @@ struct NsV {
 #pragma unroll
             for (int k = 0; k < T; k++) {
                 const bool in = (unsigned)(j0 - 2 * LAG + k) < (unsigned)len;
-                buf_st(ob2, in ? xo[k] : 0x80000000u, so2, s2h[k] - s2t[k]);
+                buf_st(ob2, in ? xo[k] : 0x80000000u, 0, s2h[k] - s2t[k]);
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < T; k++) buf_st(ob2, xo[k], so2, s2h[k] - s2t[k]);
+            for (int k = 0; k < T; k++) buf_st(ob2, xo[k], 0, s2h[k] - s2t[k]);
         }
         ws = ws + T == R ? 0 : ws + T;
     }
@@ -925,25 +885,6 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
     __builtin_amdgcn_sched_barrier(0);
     L.load(tb);
     __builtin_amdgcn_sched_barrier(0);
-#if SM_CB_NSV_RB && SM_CB_NSV_AH
-#pragma unroll
-    for (int r = 0; r < L_t::NH; r++) L.soffs[r] = (uint32_t)(r * T) * L.vsb;
-    for (int j0 = 0; j0 < nst; j0 += 6 * T) {
-        L.rebase();
-        L.template load_rb<0>(tc);
-        L.template process<0>(ta, j0);
-        L.template load_rb<1>(ta);
-        L.template process<1>(tb, j0 + T);
-        L.template load_rb<2>(tb);
-        L.template process<2>(tc, j0 + 2 * T);
-        L.template load_rb<3>(tc);
-        L.template process<3>(ta, j0 + 3 * T);
-        L.template load_rb<4>(ta);
-        L.template process<4>(tb, j0 + 4 * T);
-        L.template load_rb<5>(tb);
-        L.template process<5>(tc, j0 + 5 * T);
-    }
-#else
     for (int j0 = 0; j0 < nst; j0 += 6 * T) {
         L.load(tc);
         L.template process<0>(ta, j0);
@@ -958,7 +899,6 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
         L.load(tb);
         L.template process<5>(tc, j0 + 5 * T);
     }
-#endif
 }
 
 // (at most three waves per CU fit the rings: tell the scheduler so that it schedules for latency,

@@ -73,6 +73,22 @@ def test_multi_stream_sub_batches(oracle, sub_batch, num_streams):
         sb.close()
 
 
+def test_auto_two_groups(oracle):
+    """num_streams 0 (auto) with batch_capacity >= 8, CBCA and 4-path SGM: sm_run splits the 9
+    pairs into groups of 5 and 4 on two streams, the second starting after the first's first CBCA
+    sweep; the maps must equal the oracle's."""
+    H, W, md, n = 29, 61, 31, 9
+    batch = S.make_batch(n, H, W, md + 1, first_index=520)
+    sb = StereoBatch(md, H, W, n, device=0)
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        first = sb.run(0.3)
+        np.testing.assert_array_equal(first, _oracle_maps(oracle, batch, H, W, md))
+        np.testing.assert_array_equal(sb.run(0.3), first)
+    finally:
+        sb.close()
+
+
 @pytest.mark.parametrize("n,caps", [(5, (3, 3)), (4, (2, 2, 2)), (1, (1, 1))])
 def test_run_batch_multi_contexts(oracle, n, caps):
     """sm_run_batch_multi over several contexts on device 0 (one host thread each): contiguous

@@ -683,25 +683,8 @@ __device__ __forceinline__ void cpk(float (&d)[K], const float (&s)[K]) {
     for (int k = 0; k < K; k++) d[k] = s[k];
 }
 
-// minimum waves per SIMD the register allocation must allow, per pass (0: the compiler's choice);
-// tuning switches for the same-box sweeps (tools/build_variants.sh)
-#ifndef SM_SGM_CK_WA
-#define SM_SGM_CK_WA 0       // pass A
-#endif
-#ifndef SM_SGM_CK_WB
-#define SM_SGM_CK_WB 0       // pass B of the first pair
-#endif
-#ifndef SM_SGM_CK_WL
-#define SM_SGM_CK_WL 0       // pass B with the running sum (the map, or 8 paths' middle pair)
-#endif
-template <int MODE>
-constexpr int ck_min_waves() {
-    return (MODE & CK_A) ? SM_SGM_CK_WA : ((MODE & (SGM_LAST | CK_MID)) ? SM_SGM_CK_WL : SM_SGM_CK_WB);
-}
-
 template <int S, int MODE, int KV, bool ROWS, bool FULL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ck_min_waves<MODE>() > 0 ? ck_min_waves<MODE>() : 1)))
-void k_sgm_ck(const SgmArgs a) {
+__global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
     static_assert(ROWS || KV == 1, "one line per wave: four disparities per lane");
     constexpr int K = 4 * KV;
     constexpr int LPL = ROWS ? 16 : 64;   // lanes per line

@@ -563,7 +563,13 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
 #ifndef SM_PREP_SPLIT
 #define SM_PREP_SPLIT 1
 #endif
-constexpr int PH_TW = 256, PH_TH = 4, PV_TW = 64, PV_TH = 64;
+#ifndef SM_PREP_HTH
+#define SM_PREP_HTH 4    // k_prep_h tile rows
+#endif
+#ifndef SM_PREP_VTH
+#define SM_PREP_VTH 64   // k_prep_v tile rows
+#endif
+constexpr int PH_TW = 256, PH_TH = SM_PREP_HTH, PV_TW = 64, PV_TH = SM_PREP_VTH;
 #ifndef SM_PREP_QUAD
 #define SM_PREP_QUAD 1   // strips filled four pixels per load_quad_bgr (else three byte loads per pixel)
 #endif

@@ -40,6 +40,7 @@ def main():
     H, W, md, paths, B, _ = bench.WORKLOADS[a.workload]
     batch = S.make_batch(B, H, W, md + 1)
     sbs = {}
+    maps = {}   # each instance's first maps: every variant must reproduce the first one's bits
     if a.copies > 1:
         a.variants = [v for _ in range(a.copies) for v in a.variants]
     names = [f"{v}#{i}" if a.variants.count(v) > 1 else v for i, v in enumerate(a.variants)]
@@ -60,13 +61,17 @@ def main():
             os.environ["SM_HIP_LIB"] = os.path.join(ROOT, "tools", "abvar", f"libsm_hip_{v}.so")
         sb = StereoBatch(md, H, W, B, sgm_paths=paths, aggregation=a.agg, **params)
         sb.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
-        sb.run(0.3, download=False)
-        sb.synchronize()
+        maps[key] = sb.run(0.3)
         sbs[key] = sb
         for kv in filter(None, envs.split(",")):
             if not kv.partition("=")[0].islower():
                 os.environ.pop(kv.partition("=")[0], None)
     _capi._lib = None
+    import numpy as np
+    first = names[0]
+    for v in names[1:]:
+        same = np.array_equal(maps[v], maps[first])
+        print(f"maps {v} == {first}: {'identical' if same else 'DIFFERENT'}", flush=True)
     step_ms = {v: [] for v in names}
     kern = {v: {} for v in names}
     for r in range(a.rounds):

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round-4 final GPU round on the final tree: the whole -m gpu suite, smoke, the default bench
 # (configs[3]) and every other workload's bench line on the same box, rocprofv3 kernel stats of
-# the default bench, and its PMC HBM traffic (FETCH_SIZE and WRITE_SIZE in separate passes).
+# the default bench, and its PMC HBM traffic (FETCH_SIZE and WRITE_SIZE in separate passes); the
+# profiled runs use one stream (--streams 1), the launch shape of bench.py's per-kernel pass, so the
+# rocprof averages and PMC bytes per launch match the roofline's HIP-event times.
 set -o pipefail
 O=gpurun_out/${1:-r4_final}
 mkdir -p $O
@@ -21,9 +23,9 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
  && $B --workload teddy --agg GF --no-cpu-baseline > $O/bench_gf.json 2> $O/bench_gf.err \
  && $B --workload teddy --agg NL --no-cpu-baseline > $O/bench_nl.json 2> $O/bench_nl.err \
  && for f in hd teddy kitti refine so gf nl; do python3 -c "import json,sys; d=json.load(open('$O/bench_$f.json')); print('$f', d['value'], d['ms_per_step'], d.get('parity'))"; done \
- && cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/kt -o kt -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/$O/kt.log 2>&1 \
- && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $GRAFT_REPO_ROOT/$O/pf -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-parity > $GRAFT_REPO_ROOT/$O/pf.log 2>&1 \
- && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $GRAFT_REPO_ROOT/$O/pw -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-parity > $GRAFT_REPO_ROOT/$O/pw.log 2>&1 \
+ && cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/kt -o kt -- python3 $GRAFT_REPO_ROOT/bench.py --streams 1 --steps 10 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/$O/kt.log 2>&1 \
+ && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $GRAFT_REPO_ROOT/$O/pf -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py --streams 1 --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-parity > $GRAFT_REPO_ROOT/$O/pf.log 2>&1 \
+ && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $GRAFT_REPO_ROOT/$O/pw -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py --streams 1 --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-parity > $GRAFT_REPO_ROOT/$O/pw.log 2>&1 \
  && cd $GRAFT_REPO_ROOT && find $O/kt -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/kt_kernel_stats.csv && head -16 $O/kt_kernel_stats.csv \
  && python3 tools/pmc_summary.py $(find $O/pf -name "*counter_collection.csv" | head -1) $(find $O/pw -name "*counter_collection.csv" | head -1) $O/pmc_fullres_b2.json \
  && echo "r4 final done"

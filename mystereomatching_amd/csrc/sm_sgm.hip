@@ -630,6 +630,9 @@ static int rows_kv(const SgmArgs& a, int mode) {
 #ifndef SM_SGM_CK_S
 #define SM_SGM_CK_S 8        // segment steps (layouts with 4 disparities per lane)
 #endif
+#ifndef SM_SGM_CK_APF
+#define SM_SGM_CK_APF 2      // pass A: tiles in the register ring (APF - 1 in flight)
+#endif
 #ifndef SM_SGM_CK_S2
 #define SM_SGM_CK_S2 4       // segment steps with 8 disparities per lane (D in (64, 128])
 #endif
@@ -800,6 +803,9 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
             }
             if (tt <= nseg - 2) stK(ckl, (long)(nseg - tt - 2) * D, Lp);
         };
+        // SM_SGM_CK_APF tiles in the register ring: the loads of the next APF - 1 tiles are in
+        // flight while one is processed (tiles past the line end read clamped pixels)
+#if SM_SGM_CK_APF == 2
         Tl ta, tb;
         load(ta, 0);
         for (int tt = 0; tt < nseg; tt += 2) {
@@ -808,6 +814,19 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
             load(ta, tt + 2);
             if (tt + 1 < nseg) process(tb, tt + 1);
         }
+#else
+        constexpr int NT = SM_SGM_CK_APF;
+        Tl t[NT];
+#pragma unroll
+        for (int i = 0; i < NT - 1; i++) load(t[i], i);
+        for (int tt = 0; tt < nseg; tt += NT) {
+#pragma unroll
+            for (int r = 0; r < NT; r++) {
+                load(t[(r + NT - 1) % NT], tt + r + NT - 1);
+                if (tt + r < nseg) process(t[r], tt + r);
+            }
+        }
+#endif
     } else {
         // pass B: the second path, segment k = the first path's steps [aj0, aj0 + S), walked
         // from aj0 + S - 1 down; the first path's L over the segment is recomputed in registers

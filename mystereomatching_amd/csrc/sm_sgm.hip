@@ -633,6 +633,12 @@ static int rows_kv(const SgmArgs& a, int mode) {
 #ifndef SM_SGM_CK_APF
 #define SM_SGM_CK_APF 2      // pass A: tiles in the register ring (APF - 1 in flight)
 #endif
+#ifndef SM_SGM_CK_BPF_FULL
+#define SM_SGM_CK_BPF_FULL 2 // pass B of the first pair, D == 256: segments in the register ring
+#endif
+#ifndef SM_SGM_CK_APF_FULL
+#define SM_SGM_CK_APF_FULL 2 // the same for D == 256 (one line per wave, every lane inside D)
+#endif
 #ifndef SM_SGM_CK_S2
 #define SM_SGM_CK_S2 4       // segment steps with 8 disparities per lane (D in (64, 128])
 #endif
@@ -803,30 +809,30 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
             }
             if (tt <= nseg - 2) stK(ckl, (long)(nseg - tt - 2) * D, Lp);
         };
-        // SM_SGM_CK_APF tiles in the register ring: the loads of the next APF - 1 tiles are in
-        // flight while one is processed (tiles past the line end read clamped pixels)
-#if SM_SGM_CK_APF == 2
-        Tl ta, tb;
-        load(ta, 0);
-        for (int tt = 0; tt < nseg; tt += 2) {
-            load(tb, tt + 1);
-            process(ta, tt);
-            load(ta, tt + 2);
-            if (tt + 1 < nseg) process(tb, tt + 1);
-        }
-#else
-        constexpr int NT = SM_SGM_CK_APF;
-        Tl t[NT];
+        // NT tiles in the register ring: the loads of the next NT - 1 tiles are in flight while
+        // one is processed (tiles past the line end read clamped pixels)
+        constexpr int NT = (!ROWS && FULL) ? SM_SGM_CK_APF_FULL : SM_SGM_CK_APF;
+        if constexpr (NT == 2) {
+            Tl ta, tb;
+            load(ta, 0);
+            for (int tt = 0; tt < nseg; tt += 2) {
+                load(tb, tt + 1);
+                process(ta, tt);
+                load(ta, tt + 2);
+                if (tt + 1 < nseg) process(tb, tt + 1);
+            }
+        } else {
+            Tl t[NT];
 #pragma unroll
-        for (int i = 0; i < NT - 1; i++) load(t[i], i);
-        for (int tt = 0; tt < nseg; tt += NT) {
+            for (int i = 0; i < NT - 1; i++) load(t[i], i);
+            for (int tt = 0; tt < nseg; tt += NT) {
 #pragma unroll
-            for (int r = 0; r < NT; r++) {
-                load(t[(r + NT - 1) % NT], tt + r + NT - 1);
-                if (tt + r < nseg) process(t[r], tt + r);
+                for (int r = 0; r < NT; r++) {
+                    load(t[(r + NT - 1) % NT], tt + r + NT - 1);
+                    if (tt + r < nseg) process(t[r], tt + r);
+                }
             }
         }
-#endif
     } else {
         // pass B: the second path, segment k = the first path's steps [aj0, aj0 + S), walked
         // from aj0 + S - 1 down; the first path's L over the segment is recomputed in registers
@@ -926,13 +932,27 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
                 if (line_ok && ll < S && aj0 + ll >= 0) dbase[(long)(aj0 + ll) * pstep] = (int16_t)dacc;
             }
         };
-        Sg ga, gb;
-        load(ga, 0);
-        for (int k = 0; k < nseg; k += 2) {
-            load(gb, k + 1);
-            process(ga, k);
-            load(ga, k + 2);
-            if (k + 1 < nseg) process(gb, k + 1);
+        constexpr int NB = (!ROWS && FULL && !ACC_IN) ? SM_SGM_CK_BPF_FULL : 2;   // segments in the ring
+        if constexpr (NB == 2) {
+            Sg ga, gb;
+            load(ga, 0);
+            for (int k = 0; k < nseg; k += 2) {
+                load(gb, k + 1);
+                process(ga, k);
+                load(ga, k + 2);
+                if (k + 1 < nseg) process(gb, k + 1);
+            }
+        } else {
+            Sg g[NB];
+#pragma unroll
+            for (int i = 0; i < NB - 1; i++) load(g[i], i);
+            for (int k = 0; k < nseg; k += NB) {
+#pragma unroll
+                for (int r = 0; r < NB; r++) {
+                    load(g[(r + NB - 1) % NB], k + r + NB - 1);
+                    if (k + r < nseg) process(g[r], k + r);
+                }
+            }
         }
     }
 }

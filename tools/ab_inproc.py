@@ -74,8 +74,10 @@ def main():
         print(f"maps {v} == {first}: {'identical' if same else 'DIFFERENT'}", flush=True)
     step_ms = {v: [] for v in names}
     kern = {v: {} for v in names}
+    order = list(sbs.items())
     for r in range(a.rounds):
-        for v, sb in sbs.items():
+        # each round starts one instance later, so no variant always runs first after the print
+        for v, sb in order[r % len(order):] + order[:r % len(order)]:
             sb.profile(True)
             sb.profile_reset()
             sb.synchronize()

@@ -634,10 +634,10 @@ static int rows_kv(const SgmArgs& a, int mode) {
 #define SM_SGM_CK_APF 2      // pass A: tiles in the register ring (APF - 1 in flight)
 #endif
 #ifndef SM_SGM_CK_BPF_FULL
-#define SM_SGM_CK_BPF_FULL 2 // pass B of the first pair, D == 256: segments in the register ring
+#define SM_SGM_CK_BPF_FULL 3 // pass B of the first pair, D == 256: segments in the register ring
 #endif
 #ifndef SM_SGM_CK_APF_FULL
-#define SM_SGM_CK_APF_FULL 2 // the same for D == 256 (one line per wave, every lane inside D)
+#define SM_SGM_CK_APF_FULL 4 // pass A for D == 256 (one line per wave, every lane inside D)
 #endif
 #ifndef SM_SGM_CK_S2
 #define SM_SGM_CK_S2 4       // segment steps with 8 disparities per lane (D in (64, 128])

@@ -633,12 +633,22 @@ static int rows_kv(const SgmArgs& a, int mode) {
 #ifndef SM_SGM_CK_APF
 #define SM_SGM_CK_APF 2      // pass A: tiles in the register ring (APF - 1 in flight)
 #endif
+// Deep rings (CK_DEEP launches): D == 256 (one line per wave, every lane inside D) and a launch of
+// at most SM_SGM_CK_DEEP_LINES lines, which then all fit at the two waves per SIMD the deeper rings'
+// registers allow — pass A keeps four tiles (three in flight), pass B of the first pair three
+// segments.  Larger launches keep two: at 4000 lines (full resolution, two pairs in one launch) the
+// deep pass B runs two rounds of waves, 4.69 -> 5.10 ms (profiles/r4_final2); at 2000 (one pair per
+// stream group, the default schedule) the step got faster (profiles/r4y, r4z).
 #ifndef SM_SGM_CK_BPF_FULL
-#define SM_SGM_CK_BPF_FULL 3 // pass B of the first pair, D == 256: segments in the register ring
+#define SM_SGM_CK_BPF_FULL 3
 #endif
 #ifndef SM_SGM_CK_APF_FULL
-#define SM_SGM_CK_APF_FULL 4 // pass A for D == 256 (one line per wave, every lane inside D)
+#define SM_SGM_CK_APF_FULL 4
 #endif
+#ifndef SM_SGM_CK_DEEP_LINES
+#define SM_SGM_CK_DEEP_LINES 2048
+#endif
+constexpr int CK_DEEP = 128;   // launch-internal mode bit (k_sgm_ck's MODE)
 #ifndef SM_SGM_CK_S2
 #define SM_SGM_CK_S2 4       // segment steps with 8 disparities per lane (D in (64, 128])
 #endif
@@ -811,7 +821,7 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
         };
         // NT tiles in the register ring: the loads of the next NT - 1 tiles are in flight while
         // one is processed (tiles past the line end read clamped pixels)
-        constexpr int NT = (!ROWS && FULL) ? SM_SGM_CK_APF_FULL : SM_SGM_CK_APF;
+        constexpr int NT = (MODE & CK_DEEP) ? SM_SGM_CK_APF_FULL : SM_SGM_CK_APF;
         if constexpr (NT == 2) {
             Tl ta, tb;
             load(ta, 0);
@@ -932,7 +942,7 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
                 if (line_ok && ll < S && aj0 + ll >= 0) dbase[(long)(aj0 + ll) * pstep] = (int16_t)dacc;
             }
         };
-        constexpr int NB = (!ROWS && FULL && !ACC_IN) ? SM_SGM_CK_BPF_FULL : 2;   // segments in the ring
+        constexpr int NB = ((MODE & CK_DEEP) && !ACC_IN) ? SM_SGM_CK_BPF_FULL : 2;   // segments in the ring
         if constexpr (NB == 2) {
             Sg ga, gb;
             load(ga, 0);
@@ -969,7 +979,11 @@ static void launch_ck_one(const SgmArgs& a, hipStream_t st) {
 }
 template <int S, int KV, bool ROWS, bool FULL, int SGN>
 static void launch_ck_f(const SgmArgs& a, int mode, hipStream_t st) {
-    switch (mode) {
+    if constexpr (!ROWS && FULL) {
+        if (mode == (CK_A | CK_DEEP)) return launch_ck_one<S, SGN | CK_A | CK_DEEP, KV, ROWS, FULL>(a, st);
+        if (mode == (CK_B | CK_DEEP)) return launch_ck_one<S, SGN | CK_B | CK_DEEP, KV, ROWS, FULL>(a, st);
+    }
+    switch (mode & ~CK_DEEP) {
         case CK_A: return launch_ck_one<S, SGN | CK_A, KV, ROWS, FULL>(a, st);
         case CK_B: return launch_ck_one<S, SGN | CK_B, KV, ROWS, FULL>(a, st);
         case CK_B | CK_MID: return launch_ck_one<S, SGN | CK_B | CK_MID, KV, ROWS, FULL>(a, st);
@@ -992,7 +1006,11 @@ void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st) {
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
     switch (ck_kv(a.D)) {
         case 0:
-            if (a.D == 256) return launch_ck_s<SM_SGM_CK_S, 1, false, true>(b, mode, st);
+            if (a.D == 256) {
+                const long lines = (long)(a.rv == 0 ? a.H : a.W) * n;
+                if ((mode == CK_A || mode == CK_B) && lines <= SM_SGM_CK_DEEP_LINES) mode |= CK_DEEP;
+                return launch_ck_s<SM_SGM_CK_S, 1, false, true>(b, mode, st);
+            }
             return launch_ck_s<SM_SGM_CK_S, 1, false, false>(b, mode, st);
         case 1:
             if (a.D == 64) return launch_ck_s<SM_SGM_CK_S, 1, true, true>(b, mode, st);

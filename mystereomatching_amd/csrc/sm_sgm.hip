@@ -630,25 +630,6 @@ static int rows_kv(const SgmArgs& a, int mode) {
 #ifndef SM_SGM_CK_S
 #define SM_SGM_CK_S 8        // segment steps (layouts with 4 disparities per lane)
 #endif
-#ifndef SM_SGM_CK_APF
-#define SM_SGM_CK_APF 2      // pass A: tiles in the register ring (APF - 1 in flight)
-#endif
-// Deep rings (CK_DEEP launches): D == 256 (one line per wave, every lane inside D) and a launch of
-// at most SM_SGM_CK_DEEP_LINES lines, which then all fit at the two waves per SIMD the deeper rings'
-// registers allow — pass A keeps four tiles (three in flight), pass B of the first pair three
-// segments.  Larger launches keep two: at 4000 lines (full resolution, two pairs in one launch) the
-// deep pass B runs two rounds of waves, 4.69 -> 5.10 ms (profiles/r4_final2); at 2000 (one pair per
-// stream group, the default schedule) the step got faster (profiles/r4y, r4z).
-#ifndef SM_SGM_CK_BPF_FULL
-#define SM_SGM_CK_BPF_FULL 3
-#endif
-#ifndef SM_SGM_CK_APF_FULL
-#define SM_SGM_CK_APF_FULL 4
-#endif
-#ifndef SM_SGM_CK_DEEP_LINES
-#define SM_SGM_CK_DEEP_LINES 2048
-#endif
-constexpr int CK_DEEP = 128;   // launch-internal mode bit (k_sgm_ck's MODE)
 #ifndef SM_SGM_CK_S2
 #define SM_SGM_CK_S2 4       // segment steps with 8 disparities per lane (D in (64, 128])
 #endif
@@ -819,29 +800,13 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
             }
             if (tt <= nseg - 2) stK(ckl, (long)(nseg - tt - 2) * D, Lp);
         };
-        // NT tiles in the register ring: the loads of the next NT - 1 tiles are in flight while
-        // one is processed (tiles past the line end read clamped pixels)
-        constexpr int NT = (MODE & CK_DEEP) ? SM_SGM_CK_APF_FULL : SM_SGM_CK_APF;
-        if constexpr (NT == 2) {
-            Tl ta, tb;
-            load(ta, 0);
-            for (int tt = 0; tt < nseg; tt += 2) {
-                load(tb, tt + 1);
-                process(ta, tt);
-                load(ta, tt + 2);
-                if (tt + 1 < nseg) process(tb, tt + 1);
-            }
-        } else {
-            Tl t[NT];
-#pragma unroll
-            for (int i = 0; i < NT - 1; i++) load(t[i], i);
-            for (int tt = 0; tt < nseg; tt += NT) {
-#pragma unroll
-                for (int r = 0; r < NT; r++) {
-                    load(t[(r + NT - 1) % NT], tt + r + NT - 1);
-                    if (tt + r < nseg) process(t[r], tt + r);
-                }
-            }
+        Tl ta, tb;
+        load(ta, 0);
+        for (int tt = 0; tt < nseg; tt += 2) {
+            load(tb, tt + 1);
+            process(ta, tt);
+            load(ta, tt + 2);
+            if (tt + 1 < nseg) process(tb, tt + 1);
         }
     } else {
         // pass B: the second path, segment k = the first path's steps [aj0, aj0 + S), walked
@@ -942,27 +907,13 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
                 if (line_ok && ll < S && aj0 + ll >= 0) dbase[(long)(aj0 + ll) * pstep] = (int16_t)dacc;
             }
         };
-        constexpr int NB = ((MODE & CK_DEEP) && !ACC_IN) ? SM_SGM_CK_BPF_FULL : 2;   // segments in the ring
-        if constexpr (NB == 2) {
-            Sg ga, gb;
-            load(ga, 0);
-            for (int k = 0; k < nseg; k += 2) {
-                load(gb, k + 1);
-                process(ga, k);
-                load(ga, k + 2);
-                if (k + 1 < nseg) process(gb, k + 1);
-            }
-        } else {
-            Sg g[NB];
-#pragma unroll
-            for (int i = 0; i < NB - 1; i++) load(g[i], i);
-            for (int k = 0; k < nseg; k += NB) {
-#pragma unroll
-                for (int r = 0; r < NB; r++) {
-                    load(g[(r + NB - 1) % NB], k + r + NB - 1);
-                    if (k + r < nseg) process(g[r], k + r);
-                }
-            }
+        Sg ga, gb;
+        load(ga, 0);
+        for (int k = 0; k < nseg; k += 2) {
+            load(gb, k + 1);
+            process(ga, k);
+            load(ga, k + 2);
+            if (k + 1 < nseg) process(gb, k + 1);
         }
     }
 }
@@ -979,11 +930,7 @@ static void launch_ck_one(const SgmArgs& a, hipStream_t st) {
 }
 template <int S, int KV, bool ROWS, bool FULL, int SGN>
 static void launch_ck_f(const SgmArgs& a, int mode, hipStream_t st) {
-    if constexpr (!ROWS && FULL) {
-        if (mode == (CK_A | CK_DEEP)) return launch_ck_one<S, SGN | CK_A | CK_DEEP, KV, ROWS, FULL>(a, st);
-        if (mode == (CK_B | CK_DEEP)) return launch_ck_one<S, SGN | CK_B | CK_DEEP, KV, ROWS, FULL>(a, st);
-    }
-    switch (mode & ~CK_DEEP) {
+    switch (mode) {
         case CK_A: return launch_ck_one<S, SGN | CK_A, KV, ROWS, FULL>(a, st);
         case CK_B: return launch_ck_one<S, SGN | CK_B, KV, ROWS, FULL>(a, st);
         case CK_B | CK_MID: return launch_ck_one<S, SGN | CK_B | CK_MID, KV, ROWS, FULL>(a, st);
@@ -1006,11 +953,7 @@ void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st) {
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
     switch (ck_kv(a.D)) {
         case 0:
-            if (a.D == 256) {
-                const long lines = (long)(a.rv == 0 ? a.H : a.W) * n;
-                if ((mode == CK_A || mode == CK_B) && lines <= SM_SGM_CK_DEEP_LINES) mode |= CK_DEEP;
-                return launch_ck_s<SM_SGM_CK_S, 1, false, true>(b, mode, st);
-            }
+            if (a.D == 256) return launch_ck_s<SM_SGM_CK_S, 1, false, true>(b, mode, st);
             return launch_ck_s<SM_SGM_CK_S, 1, false, false>(b, mode, st);
         case 1:
             if (a.D == 64) return launch_ck_s<SM_SGM_CK_S, 1, true, true>(b, mode, st);

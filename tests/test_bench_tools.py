@@ -37,11 +37,7 @@ def test_pmc_profile_names():
         "void sm::k_sgm_ck<8, 16, 1, false, true>(sm::SgmArgs)",
         "void sm::k_sgm_ck<8, 34, 1, false, true>(sm::SgmArgs)",
         "void sm::k_cost<0, true, 3, false, true, 4>(sm::CostArgs)",
-        # deep-ring launches (CK_DEEP = 128) and 8 paths' middle pair (CK_MID = 64)
-        "void sm::k_sgm_ck<8, 144, 1, false, true>(sm::SgmArgs)",
-        "void sm::k_sgm_ck<8, 160, 1, false, true>(sm::SgmArgs)",
-        "void sm::k_sgm_ck<8, 144, 1, false, true>(sm::SgmArgs)",
+        # 8 paths' middle pair (CK_MID = 64)
         "void sm::k_sgm_ck<8, 96, 1, false, false>(sm::SgmArgs)")]
     assert names == ["cbca_h_scan", "cbca_v_norm_scan", "cbca_h_norm", "sgm_ck_a01", "sgm_ck_b01",
-                     "sgm_ck_a23", "sgm_last_wta", "cost_volume", "sgm_ck_a01", "sgm_ck_b01", "sgm_ck_a23",
-                     "sgm_ck_b23"]
+                     "sgm_ck_a23", "sgm_last_wta", "cost_volume", "sgm_ck_b23"]

@@ -28,7 +28,7 @@ def profile_name(sym: str, seen: dict) -> str:
         return "cbca_h_norm"
     m = re.search(r"k_sgm_ck<\d+, (\d+),", sym)
     if m:
-        mode = int(m.group(1))  # CK_A = 16, CK_B = 32, CK_MID = 64, CK_DEEP = 128, SGM_LAST = 2
+        mode = int(m.group(1))  # CK_A = 16, CK_B = 32, CK_MID = 64, SGM_LAST = 2
         if mode & 16:
             seen["ck_a"] = seen.get("ck_a", 0) + 1
             return "sgm_ck_a01" if seen["ck_a"] % 2 == 1 else "sgm_ck_a23"

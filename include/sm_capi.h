@@ -135,6 +135,9 @@ typedef struct sm_params {
     float gf_eps;                /* gf_eps[0] = 0.0001 (h:298; radius gf_r[0] = 9, h:297) */
     int32_t gf_mode;             /* sm_gf_mode: SM_GF_XIMGPROC (default, the shipped build) or SM_GF_MY_GUIDE */
     double nl_sigma;             /* NLCCA sigma = 0.1 (NL/NLCCA.cpp:33): weights exp(-c / (255 sigma)) */
+    int32_t lr_consis;           /* Do_LRConsis = 1 (h:72): "so" optimises both views, DP[1] = so(vm[1])
+                                  * (num = Do_LRConsis ? 2 : 1, cpp:1093); 0: "so" builds and optimises
+                                  * the left view only */
 } sm_params;
 
 typedef struct sm_ctx sm_ctx;

@@ -518,6 +518,7 @@ class StereoMatching {
         p.do_proper_ipol = Do_properIpol ? 1 : 0;
         p.do_last_median_blur = Do_lastMedianBlur ? 1 : 0;
         p.gf_mode = gf_my_guide ? SM_GF_MY_GUIDE : SM_GF_XIMGPROC;
+        p.lr_consis = Do_LRConsis ? 1 : 0;
         check(sm_create(&ctx_, &p, hip_device), "sm_create");
         check(sm_set_images(ctx_, I1_c.data, I2_c.data, I1_c.step, I1_g.data, I2_g.data, I1_g.step), "sm_set_images");
     }

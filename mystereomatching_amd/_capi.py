@@ -41,6 +41,7 @@ class sm_params(C.Structure):
         ("do_proper_ipol", C.c_int32), ("disp_occ", C.c_int32), ("do_last_median_blur", C.c_int32),
         ("sub_batch", C.c_int32), ("num_streams", C.c_int32), ("fuse_norm_scan", C.c_int32),
         ("gf_eps", C.c_float), ("gf_mode", C.c_int32), ("nl_sigma", C.c_double),
+        ("lr_consis", C.c_int32),
     ]
 
 

@@ -197,14 +197,16 @@ bool needs_census(const sm_params& p) { return p.cost_method != SM_COST_AD; }
 bool needs_arms(const sm_params& p) {
     return p.cost_method == SM_COST_CENSUS_GRAD || p.aggregation == SM_AGG_CBCA || p.do_refine;  // + regionVote (cpp:1393-1396)
 }
-// "so" runs on both views (num = Do_LRConsis ? 2 : 1, cpp:1093, Do_LRConsis = 1, h:72), so DP[1]
-// = so(vm[1]) needs the right cost volume even without Do_refine
-bool right_view(const sm_params& p) { return p.compute_right_view || p.do_refine || p.optimization == SM_OPT_SO; }
+// "so" runs on both views when Do_LRConsis (num = Do_LRConsis ? 2 : 1, cpp:1093, Do_LRConsis = 1,
+// h:72; imgNum = Do_LRConsis ? 2 : 1 in costCalculate, cpp:952), so DP[1] = so(vm[1]) needs the
+// right cost volume even without Do_refine
+bool so_views2(const sm_params& p) { return p.optimization == SM_OPT_SO && p.lr_consis; }
+bool right_view(const sm_params& p) { return p.compute_right_view || p.do_refine || so_views2(p); }
 int n_views(const sm_params& p) { return p.do_refine ? 2 : 1; }   // imgNum = Do_refine && Do_LRConsis ? 2 : 1
 // views dispOptimize runs on: sgm / WTA num = Do_refine && Do_LRConsis ? 2 : 1 (cpp:1054, 1110);
 // so num = Do_LRConsis ? 2 : 1 (cpp:1093) -- on vm[1] as costCalculate left it (CBCA and
 // SolveAll touch vm[1] only with Do_refine, cpp:5592, 2178)
-int opt_views(const sm_params& p) { return p.optimization == SM_OPT_SO ? 2 : n_views(p); }
+int opt_views(const sm_params& p) { return p.optimization == SM_OPT_SO ? (p.lr_consis ? 2 : 1) : n_views(p); }
 
 int cbca_lag(const sm_params& p) { return p.arm_l_out > p.arm_min_l ? p.arm_l_out : p.arm_min_l; }
 
@@ -222,10 +224,12 @@ bool cbca_div_safe(const sm_params& p, int k) {
         f0 = -24;
     } else if (p.cost_method == SM_COST_CENSUS) {
         f0 = 0;
-    } else {   // AD: min(s / 3, trunc)
+    } else if (p.cost_method == SM_COST_AD) {   // AD: min(s / 3, trunc)
         if (p.ad_trunc_ad == 0.0f) return true;   // every cost is 0
         const float m = std::min(1.0f / 3.0f, p.ad_trunc_ad);
         f0 = std::ilogb(m);
+    } else {
+        return false;   // a cost method without a proof keeps the IEEE fallback
     }
     return f0 - 61 * k - 46 >= -110;
 }
@@ -926,14 +930,19 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->do_last_median_blur = 1; // h:80
     p->sub_batch = 0;
     p->num_streams = 0;        // auto (see sm_capi.h)
-    p->fuse_norm_scan = -1;   // auto: fused for volumes >= 256 MiB per pair
+    p->fuse_norm_scan = -1;   // auto: fused where the lag-34 sweep applies or for volumes >= 256 MiB per pair
     p->gf_eps = 0.0001f;        // gf_eps[0] = 1e-4 (h:298; guidedFilter / guideFilterCore_matlab, cpp:4509-4513)
     p->gf_mode = SM_GF_XIMGPROC;  // `//#define MY_GUIDE` (h:38): the shipped build calls ximgproc::guidedFilter
     p->nl_sigma = 0.1;          // NLCCA::aggreCV (NL/NLCCA.cpp:33)
+    p->lr_consis = 1;           // Do_LRConsis (h:72)
 }
 
 const char* sm_status_string(sm_status s) {
-    switch (s) {
+    // (a C caller may pass any int: read the bits, never an out-of-range enum value)
+    int32_t v;
+    static_assert(sizeof(v) == sizeof(s), "sm_status is an int");
+    memcpy(&v, &s, sizeof v);
+    switch (v) {
         case SM_OK: return "ok";
         case SM_EINVAL: return "invalid argument";
         case SM_ENOMEM: return "out of memory";

@@ -144,18 +144,11 @@ __host__ __device__ inline int prep_gray_bytes(int rv, int ru) {
 __host__ __device__ inline int prep_strip_words(int Lo) {
     return PREP_TY * (PREP_TX + 2 * Lo) + (PREP_TY + 2 * Lo) * PREP_TX;
 }
-// fused prep (k_pack_arms folded into k_prep): the packed pixels of the strips plus a one-pixel
-// rim, PH = rows v0 - 1 .. v0 + 16 over columns u0 - Lo - 1 .. u0 + 64 + Lo, PV = rows
-// v0 - Lo - 1 .. v0 + 16 + Lo over the tile's 64 columns; the arm-walk words replace them in place
-__host__ __device__ inline int prep_fused_hc(int Lo) { return PREP_TX + 2 * Lo + 2; }
-__host__ __device__ inline int prep_fused_words(int Lo) {
-    return (PREP_TY + 2) * prep_fused_hc(Lo) + (PREP_TY + 2 * Lo + 2) * PREP_TX;
-}
 // guard-bit test of two pack10 words (see ARM_M above): every channel within t, -1 <= t <= 255
 __device__ __forceinline__ bool ok10(uint32_t c, uint32_t p, uint32_t ka, uint32_t kb) {
     return (((c + ka - p) & ~(c + kb - p)) & ARM_B9) == ARM_B9;
 }
-constexpr uint32_t PREP_OUT = 0xffffffffu;   // fused regions: a pixel outside the image
+constexpr uint32_t PREP_OUT = 0xffffffffu;   // packed-pixel strips: a pixel outside the image
 
 #ifndef SM_PREP_WALK
 #define SM_PREP_WALK 1    // arm-walk steps whose LDS reads are issued together (tuning)
@@ -344,15 +337,9 @@ __device__ __forceinline__ int arm_final(int arm, int minL, int u, int v, int du
 // TRV/TRU/TRING >= 0: census geometry fixed at compile time (the default 7 x 9 window with the
 // ring bits), so the bit loop unrolls into straight-line compares with immediate LDS offsets;
 // -1: the runtime geometry.  STRIPS: arm walks over the LDS strips (else over global memory).
-// FUSED (with STRIPS): the arm-walk words and the SGM penalty flags are made here from the packed
-// image (k_pack_arms's work), so the pxh / pxv planes never reach memory.  Bit-exact (136 GPU
-// tests), but slower: a tile needs the words of its whole strips, 7.3 per output pixel against
-// k_pack_arms's 2, and the kernel is VALU-bound (~690 VALU per pixel, SQ counters).  Same-process
-// A/B (tools/ab_inproc.py): prep 0.203 -> 0.261 ms (Teddy x16), 0.80 -> 1.05 ms (full res); off.
-#ifndef SM_PREP_FUSED
-#define SM_PREP_FUSED 0
-#endif
-template <int TRV, int TRU, int TRING, bool STRIPS, bool FUSED>
+// (Making the arm-walk words and flags inside this kernel, so the pxh / pxv planes never reach
+// memory, was bit-exact and slower: tools/experiments/prep_fused_words.patch.)
+template <int TRV, int TRU, int TRING, bool STRIPS>
 __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
     extern __shared__ __align__(16) unsigned char prep_raw[];
     const int H = a.H, W = a.W, Lo = a.L_out;
@@ -396,90 +383,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
     const int hsw = PREP_TX + 2 * Lo;
     uint32_t* hs = (uint32_t*)(prep_raw + prep_gray_bytes(rv, ru));
     uint32_t* vs = hs + PREP_TY * hsw;
-    // fused regions (FUSED): PH [PREP_TY + 2][hc], PV [PREP_TY + 2 Lo + 2][64]
-    const int fhc = prep_fused_hc(Lo);
-    uint32_t* PHr = hs;
-    uint32_t* PVr = hs + (PREP_TY + 2) * fhc;
-    if (FUSED) {
-        // packed pixels (pack10) of both regions, PREP_OUT outside the image
-        const float rinv = 1.0f / (float)fhc;
-        fill(PHr, (PREP_TY + 2) * fhc, [&](int i) -> uint32_t {
-            const int r = (int)(((float)i + 0.5f) * rinv), vv = v0 - 1 + r, uu = u0 - Lo - 1 + (i - r * fhc);
-            return ((unsigned)vv < (unsigned)H && (unsigned)uu < (unsigned)W) ? pack10(P[(size_t)vv * W + uu]) : PREP_OUT;
-        });
-        fill(PVr, (PREP_TY + 2 * Lo + 2) * PREP_TX, [&](int i) -> uint32_t {
-            const int vv = v0 - Lo - 1 + (i >> 6), uu = u0 + (i & 63);
-            return ((unsigned)vv < (unsigned)H && uu < W) ? pack10(P[(size_t)vv * W + uu]) : PREP_OUT;
-        });
-        __syncthreads();
-        // words (k_pack_arms): pack10 | bit 30 (p, p + 1) / (p, p + W) within C_D | bit 31 (p, p - 1) /
-        // (p, p - W) within C_D; 0 outside.  Computed into registers, then written over the packed
-        // pixels after a barrier (the tests read the neighbours).
-        const int tc = min(max(a.C_D, -1), 255);
-        const uint32_t ka = (uint32_t)(512 + tc) * ARM_M, kb = (uint32_t)(511 - tc) * ARM_M;
-        auto word = [&](uint32_t p, uint32_t nb30, uint32_t nb31) -> uint32_t {
-            if (p == PREP_OUT) return 0u;
-            uint32_t w = p;
-            if (nb30 != PREP_OUT && ok10(p, nb30, ka, kb)) w |= 1u << 30;
-            if (nb31 != PREP_OUT && ok10(p, nb31, ka, kb)) w |= 1u << 31;
-            return w;
-        };
-        constexpr int MH = (PREP_TY * (PREP_TX + 128) + 255) / 256, MV = ((PREP_TY + 128) * PREP_TX + 255) / 256;
-        const int nh = PREP_TY * hsw, nv = (PREP_TY + 2 * Lo) * PREP_TX;
-        uint32_t wh[MH], wv[MV];
-        const float hinv = 1.0f / (float)hsw;
-#pragma unroll
-        for (int m = 0; m < MH; m++) {
-            const int i = m * 256 + tid;
-            if (i < nh) {
-                const int r = (int)(((float)i + 0.5f) * hinv), c = i - r * hsw;
-                const uint32_t* q = PHr + (r + 1) * fhc + c + 1;
-                wh[m] = word(q[0], q[1], q[-1]);
-            }
-        }
-#pragma unroll
-        for (int m = 0; m < MV; m++) {
-            const int i = m * 256 + tid;
-            if (i < nv) {
-                const uint32_t* q = PVr + i + PREP_TX;
-                wv[m] = word(q[0], q[PREP_TX], q[-PREP_TX]);
-            }
-        }
-        // SGM penalty flags of the tile's pixels (k_pack_arms), from PH's rim
-        if (a.do_flags && (view == 0 || a.flags1)) {
-            const int tf = min(max(a.cor_thres, -1), 255);
-            const uint32_t fa = (uint32_t)(512 + tf) * ARM_M, fb = (uint32_t)(511 - tf) * ARM_M;
-            for (int yy = tid >> 6; yy < PREP_TY; yy += 4) {
-                const int x = tid & 63, u = u0 + x, v = v0 + yy;
-                if (u >= W || v >= H) continue;
-                const uint32_t* q = PHr + (yy + 1) * fhc + x + Lo + 1;
-                const uint32_t c = q[0];
-                // directions 0..7: (rv, ru) = (+1,0) (-1,0) (0,+1) (0,-1) (+1,-1) (+1,+1) (-1,+1) (-1,-1)
-                const int offs[8] = {fhc, -fhc, 1, -1, fhc - 1, fhc + 1, 1 - fhc, -1 - fhc};
-                uint32_t fl = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t nb = q[offs[k]];
-                    if (nb != PREP_OUT && !ok10(c, nb, fa, fb)) fl |= 1u << k;
-                }
-                (view == 0 ? a.flags : a.flags1)[(size_t)b * npix + (size_t)v * W + u] = (uint8_t)fl;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int m = 0; m < MH; m++) {
-            const int i = m * 256 + tid;
-            if (i < nh) {
-                const int r = (int)(((float)i + 0.5f) * hinv), c = i - r * hsw;
-                PHr[(r + 1) * fhc + c + 1] = wh[m];
-            }
-        }
-#pragma unroll
-        for (int m = 0; m < MV; m++) {
-            const int i = m * 256 + tid;
-            if (i < nv) PVr[i + PREP_TX] = wv[m];
-        }
-    } else if (STRIPS && a.do_arms) {
+    if (STRIPS && a.do_arms) {
         const uint32_t* PH = a.pxh + img * npix;
         const uint32_t* PV = a.pxv + img * npix;
         // hs rows are hsw = 64 + 2 Lo words long (runtime): row index by a float reciprocal
@@ -508,10 +412,10 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
         if (a.do_arms) {
             uint32_t packed = 0;
             // strip walks: centre words and the two thresholds' guard-bit operands
-            const uint32_t* hc = FUSED ? PHr + (yy + 1) * fhc + (x + Lo + 1) : hs + yy * hsw + (x + Lo);
-            const uint32_t* vc = FUSED ? PVr + (yy + Lo + 1) * PREP_TX + x : vs + (yy + Lo) * PREP_TX + x;
-            const uint32_t center = FUSED ? 0u : pc[0];
-            const uint32_t cf = FUSED ? hc[0] & 0x3fffffffu : pack10(center);
+            const uint32_t* hc = hs + yy * hsw + (x + Lo);
+            const uint32_t* vc = vs + (yy + Lo) * PREP_TX + x;
+            const uint32_t center = pc[0];
+            const uint32_t cf = pack10(center);
             const int t1 = min(max(a.C_D, -1), 255), t2 = min(max(a.C_D_out, -1), 255);
             const uint32_t ca1 = cf + (uint32_t)(512 + t1) * ARM_M, cb1 = cf + (uint32_t)(511 - t1) * ARM_M;
             const uint32_t ca2 = cf + (uint32_t)(512 + t2) * ARM_M, cb2 = cf + (uint32_t)(511 - t2) * ARM_M;
@@ -857,17 +761,15 @@ static bool prep_strips(int L_out) { return L_out >= 0 && L_out <= 64; }
 
 size_t prep_smem_bytes(int rv, int ru, int L_out) {
     return (size_t)prep_gray_bytes(rv, ru) +
-           (prep_strips(L_out) ? 4 * (size_t)(SM_PREP_FUSED ? prep_fused_words(L_out) : prep_strip_words(L_out)) : 0);
+           (prep_strips(L_out) ? 4 * (size_t)prep_strip_words(L_out) : 0);
 }
 
 template <int TRV, int TRU, int TRING>
-static void launch_prep_g(const PrepArgs& a, dim3 grid, size_t shm, bool strips, bool fused, hipStream_t st) {
-    if (fused)
-        hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, true, true>), grid, dim3(256), shm, st, a);
-    else if (strips)
-        hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, true, false>), grid, dim3(256), shm, st, a);
+static void launch_prep_g(const PrepArgs& a, dim3 grid, size_t shm, bool strips, hipStream_t st) {
+    if (strips)
+        hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, true>), grid, dim3(256), shm, st, a);
     else
-        hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, false, false>), grid, dim3(256), shm, st, a);
+        hipLaunchKernelGGL((k_prep<TRV, TRU, TRING, false>), grid, dim3(256), shm, st, a);
 }
 
 static void launch_prep_split(const PrepArgs& a, int n, hipStream_t st) {
@@ -908,17 +810,16 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
         launch_prep_split(a, n, st);
         return;
     }
-    const bool fused = strips && SM_PREP_FUSED;   // words and flags made inside k_prep
-    if (!fused && (strips || a.do_flags))   // arm-walk planes and the SGM penalty flags
+    if (strips || a.do_flags)   // arm-walk planes and the SGM penalty flags
         hipLaunchKernelGGL(k_pack_arms, dim3((a.W + 255) / 256, (a.H + SM_PACK_ROWS - 1) / SM_PACK_ROWS, 2 * n), dim3(256), 0,
                            st, a, (int)strips);
     dim3 grid((a.W + PREP_TX - 1) / PREP_TX, (a.H + PREP_TY - 1) / PREP_TY, 2 * n);
     const size_t shm = (size_t)prep_gray_bytes(a.rv, a.ru) +
-                       (strips ? 4 * (size_t)(fused ? prep_fused_words(a.L_out) : prep_strip_words(a.L_out)) : 0);
+                       (strips ? 4 * (size_t)prep_strip_words(a.L_out) : 0);
     if (a.rv == 3 && a.ru == 4 && a.ring == 1)   // the reference's default census window (cpp:815)
-        launch_prep_g<3, 4, 1>(a, grid, shm, strips, fused, st);
+        launch_prep_g<3, 4, 1>(a, grid, shm, strips, st);
     else
-        launch_prep_g<-1, -1, -1>(a, grid, shm, strips, fused, st);
+        launch_prep_g<-1, -1, -1>(a, grid, shm, strips, st);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -79,7 +79,8 @@ class StereoMatching:
 
         def to_c(self, cost: str, aggregation: str, optimization: str, batch: int = 1,
                  compute_right_view: bool = False, keep_final_volume: bool = False,
-                 do_refine: bool = False, switches=(True, True, True), my_guide: bool = False) -> _capi.sm_params:
+                 do_refine: bool = False, switches=(True, True, True), my_guide: bool = False,
+                 lr_consis: bool = True) -> _capi.sm_params:
             if self.censusFunc not in (0, 3):
                 raise ValueError("censusFunc must be 0 (plain census) or 3 (census + ring bits)")
             p = _capi.default_params(self.numDisparities - 1, self.rows, self.cols)
@@ -108,6 +109,7 @@ class StereoMatching:
             p.rv_ratio, p.rv_s = float(self.rv_ratio), int(self.rv_s)
             p.do_region_vote, p.do_proper_ipol, p.do_last_median_blur = (int(x) for x in switches)
             p.gf_mode = 1 if my_guide else 0
+            p.lr_consis = int(lr_consis)
             return p
 
     def __init__(self, I1_c, I2_c, I1_g, I2_g, DT=None, all_mask=None, nonocc_mask=None, disc_mask=None,
@@ -134,9 +136,10 @@ class StereoMatching:
             raise ValueError("Do_refine needs Do_LRConsis (refine() starts with the LR check, cpp:1364)")
         p = param.to_c(self.costcalculation, self.aggregation, self.optimization, my_guide=self.MY_GUIDE,
                        compute_right_view=self.Do_LRConsis and self.Do_refine,
-                       keep_final_volume=keep_final_volume, do_refine=self.Do_refine,
+                       keep_final_volume=keep_final_volume, do_refine=self.Do_refine, lr_consis=self.Do_LRConsis,
                        switches=(self.Do_regionVote, self.Do_properIpol, self.Do_lastMedianBlur))
         self._refine_on = bool(self.Do_refine)
+        self._so_views2 = self.optimization == "so" and bool(self.Do_LRConsis)   # as passed to sm_create
         p.rows, p.cols = h, w
         ctx = C.c_void_p()
         st = self._lib.sm_create(C.byref(ctx), C.byref(p), device)
@@ -163,7 +166,7 @@ class StereoMatching:
         dp = np.empty((self.h_, self.w_), np.int16)
         _capi.check(self._lib, self._ctx, self._lib.sm_disp_optimize(self._ctx, _capi.ptr(dp)), "dispOptimize")
         self.DP[0] = dp
-        if self._refine_on or (self.optimization == "so" and self.Do_LRConsis):
+        if self._refine_on or self._so_views2:
             d1 = np.empty((self.h_, self.w_), np.int16)
             _capi.check(self._lib, self._ctx, self._lib.sm_get_disp(self._ctx, 1, _capi.ptr(d1)), "DP[1]")
             self.DP[1] = d1
@@ -276,11 +279,13 @@ class StereoBatch:
         self._ctx = ctx
         _capi.check(self._lib, ctx, st, "sm_create")
         self.n = 0
+        self._async_out = []   # buffers of download_async copies still in flight
 
     def close(self):
         if getattr(self, "_ctx", None) is not None and self._ctx.value:
-            self._lib.sm_destroy(self._ctx)
+            self._lib.sm_destroy(self._ctx)   # (waits for the context's streams)
             self._ctx = None
+        getattr(self, "_async_out", []).clear()
 
     def __del__(self):
         self.close()
@@ -310,17 +315,26 @@ class StereoBatch:
         _capi.check(self._lib, self._ctx, st, "sm_run")
         return out
 
+    def _map_dst(self, out, what: str):
+        """C pointer of `out` after checking it can take the n int16 maps: a C-contiguous int16
+        numpy array or torch tensor (host or device) of at least n*H*W elements."""
+        need = self.n * self.shape[0] * self.shape[1]
+        if type(out).__module__.startswith("torch"):
+            import torch
+            if out.dtype != torch.int16 or not out.is_contiguous() or out.numel() < need:
+                raise ValueError(f"{what}: out must be a contiguous int16 tensor of at least n*H*W = {need} elements")
+            return C.c_void_p(out.data_ptr())
+        if not isinstance(out, np.ndarray) or out.dtype != np.int16 or not out.flags["C_CONTIGUOUS"] \
+                or out.size < need:
+            raise ValueError(f"{what}: out must be a C-contiguous int16 array of at least n*H*W = {need} elements")
+        return _capi.ptr(out)
+
     def download(self, out=None):
         """The n int16 maps into a new numpy array, or into `out` (numpy, or an int16 torch
         tensor on the GPU: device-to-device copy)."""
         if out is None:
             out = np.empty((self.n, self.shape[0], self.shape[1]), np.int16)
-        if _is_device_tensor(out):
-            if not out.is_contiguous() or out.numel() < self.n * self.shape[0] * self.shape[1]:
-                raise ValueError("out must be a contiguous tensor of at least n*H*W int16")
-            dst = C.c_void_p(out.data_ptr())
-        else:
-            dst = _capi.ptr(out)
+        dst = self._map_dst(out, "download")
         _capi.check(self._lib, self._ctx, self._lib.sm_download_disp(self._ctx, self.n, dst), "download")
         return out
 
@@ -333,14 +347,17 @@ class StereoBatch:
     def download_async(self, out):
         """sm_download_disp_async: the n maps into `out` (page-locked host memory, e.g. a
         pin_memory torch tensor's numpy view, or device memory) on the copy stream; complete after
-        synchronize().  The next run's map-writing kernels wait for the copy."""
-        dst = C.c_void_p(out.data_ptr()) if _is_device_tensor(out) or type(out).__module__.startswith("torch") \
-            else _capi.ptr(out)
+        synchronize().  The next run's map-writing kernels wait for the copy.  `out` is checked like
+        download()'s and kept referenced until synchronize() or close(), so the copy never writes
+        into a freed buffer."""
+        dst = self._map_dst(out, "download_async")
         _capi.check(self._lib, self._ctx, self._lib.sm_download_disp_async(self._ctx, self.n, dst), "download_async")
+        self._async_out.append(out)
         return out
 
     def synchronize(self):
         _capi.check(self._lib, self._ctx, self._lib.sm_synchronize(self._ctx), "sync")
+        self._async_out.clear()
 
     def profile(self, on: bool = True):
         self._lib.sm_profile_enable(self._ctx, int(on))

@@ -205,6 +205,12 @@ def main():
         if host_maps is not None:
             sb.download_async(host_maps)
 
+    # measured HBM ceiling next to the 8 TB/s spec: a dwordx4 copy over a buffer the
+    # size of one pair's volume (at least 2 GiB, far past the 256 MB Infinity Cache)
+    ceiling = None
+    if not args.no_profile:
+        ceiling = sb.copy_ceiling(max(H * W * D * 4, 2 << 30), reps=5)
+
     for _ in range(args.warmup):
         step()
     sb.synchronize()
@@ -225,6 +231,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # Schedule A/B on the SAME context (same device allocations, sm_set_schedule): the default
+    # schedule and one stream, timed bare in interleaved rounds (order alternating), so the
+    # default can be checked against one stream without the per-instance placement spread
+    # (DESIGN §6).  Reported beside the contract's timing, never instead of it.
+    sched_ab = None
+    if not args.no_profile and args.streams != 1 and world == 1:
+        sched_ab = {"default": [], "one_stream": []}
+        for r in range(3):
+            order = (("default", args.streams), ("one_stream", 1))
+            for name, ns in (order if r % 2 == 0 else order[::-1]):
+                sb.set_schedule(ns, args.sub_batch)
+                step()
+                sb.synchronize()
+                ta = time.perf_counter()
+                for _ in range(args.steps):
+                    step()
+                sb.synchronize()
+                sched_ab[name].append(round((time.perf_counter() - ta) / args.steps * 1e3, 4))
+        sb.set_schedule(args.streams, args.sub_batch)
+
     # Per-kernel durations: the same K steps again with a HIP event pair around every kernel on
     # the context stream.  Kept out of the throughput timing above: each event record is a
     # barrier packet on the queue (~0.14 ms per Teddy x16 step), which perturbs the step time
@@ -236,17 +262,14 @@ def main():
     profile = not args.no_profile
     kernels, ms_prof = {}, None
     kern_schedule = "one stream: the timed loop's own context" if args.streams == 1 else \
-        "one stream (a second context on the same pairs): each kernel alone; the timed loop runs " \
-        "sm_params.num_streams = %d (0 = auto: two pair groups on two streams for CBCA >= 256 MiB per pair)" % args.streams
+        "one stream (the timed loop's own context switched by sm_set_schedule): each kernel alone; the timed " \
+        "loop runs sm_params.num_streams = %d (0 = auto: two pair groups on two streams for CBCA >= 256 MiB " \
+        "per pair)" % args.streams
     if profile:
         sbk = sb
         if args.streams != 1:
-            sbk = StereoBatch(md, H, W, B, device=local, sgm_paths=paths, do_refine=int(args.refine), optimization=args.opt,
-                              aggregation=args.agg, fuse_norm_scan={"auto": -1, "on": 1, "off": 0}[args.fuse_norm_scan],
-                              sub_batch=args.sub_batch, num_streams=1)
-            sbk.upload(batch["lbgr"], batch["rbgr"], batch["lgray"], batch["rgray"])
-            for _ in range(args.warmup):
-                sbk.run(0.3, download=False)
+            sbk.set_schedule(1, args.sub_batch)
+            sbk.run(0.3, download=False)
             sbk.synchronize()
         sbk.profile(True)
         sbk.profile_reset()
@@ -257,8 +280,7 @@ def main():
         ms_prof = (time.perf_counter() - tp) / args.steps * 1e3
         kernels = sbk.profile_read()
         sbk.profile(False)
-        if sbk is not sb:
-            sbk.close()
+        sbk.set_schedule(args.streams, args.sub_batch)
     disp = sb.download()
     parity = fixture_check(args.workload, args.refine or args.agg != "CBCA", args.opt, disp[0]) \
         if rank == 0 and not args.no_parity else None
@@ -306,6 +328,12 @@ def main():
         roofline = {"bound": "hbm", "kernel": dom, "profile_names": members, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "bytes_per_launch": gbytes / launches}
+        if ceiling is not None:
+            roofline["copy_ceiling"] = round(ceiling[0], 1)
+            roofline["copy_ceiling_median"] = round(ceiling[1], 1)
+            roofline["frac_of_ceiling"] = round(ach / ceiling[0], 4)
+            roofline["copy_ceiling_how"] = ("sm_copy_ceiling: dwordx4 non-temporal copy of %.2f GB (read + write "
+                                            "counted), grids 4K/16K/64K x 5 launches, best sample" % (max(H * W * D * 4, 2 << 30) / 1e9))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -378,6 +406,13 @@ def main():
             "ms_per_step_instrumented": None if ms_prof is None else round(ms_prof, 4),
             "kernels_schedule": kern_schedule if profile else None,
         }
+        if sched_ab is not None:
+            out["schedule_ab"] = {
+                "how": "same context, sm_set_schedule between rounds; 3 interleaved rounds of K bare steps each",
+                "default_num_streams": args.streams, "default_ms": sched_ab["default"],
+                "one_stream_ms": sched_ab["one_stream"]}
+            out["ms_per_step_one_stream"] = float(np.median(sched_ab["one_stream"]))
+            out["ms_per_step_default_ab"] = float(np.median(sched_ab["default"]))
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         if e2e is not None:

@@ -202,6 +202,10 @@ SM_API sm_status sm_run_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const
 SM_API sm_status sm_run_batch_multi(sm_ctx* const* ctxs, int32_t nctx, int32_t n, const uint8_t* lbgr,
                                     const uint8_t* rbgr, const uint8_t* lgray, const uint8_t* rgray,
                                     float reg_lambda, int16_t* disp_out);
+/* Change sm_params.num_streams / sub_batch of an existing context (same meaning and ranges as at
+ * sm_create); applies from the next sm_run.  Results are identical for every schedule; this lets
+ * one context (one set of device allocations) time schedules against each other. */
+SM_API sm_status sm_set_schedule(sm_ctx* ctx, int32_t num_streams, int32_t sub_batch);
 SM_API sm_status sm_synchronize(sm_ctx* ctx);
 SM_API void* sm_stream(sm_ctx* ctx);      /* the ctx's hipStream_t */
 
@@ -229,6 +233,10 @@ SM_API sm_status sm_get_census(sm_ctx* ctx, int32_t view, uint64_t* dst); /* H*W
  * dividend mantissa at binary exponent `exp2` (a in [2^exp2, 2^(exp2+1))) for every divisor
  * 1 <= b <= bmax; *mismatches receives the number of differing results. */
 SM_API sm_status sm_div_area_check(sm_ctx* ctx, int32_t exp2, int32_t bmax, uint64_t* mismatches);
+/* Measured HBM ceiling: a dwordx4 copy between two fresh device buffers of `bytes`
+ * each (rounded down to 16 KiB) on the ctx's device and stream, at three grid sizes, `reps` timed
+ * launches each; GB/s counts read + write bytes.  Best and median over the samples. */
+SM_API sm_status sm_copy_ceiling(sm_ctx* ctx, uint64_t bytes, int32_t reps, double* best_gbs, double* median_gbs);
 
 #ifdef __cplusplus
 }

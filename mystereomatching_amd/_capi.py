@@ -72,6 +72,7 @@ SIGNATURES = [
     ("sm_download_disp_async", C.c_int, [_P, C.c_int32, _P]),
     ("sm_run_batch", C.c_int, [_P, C.c_int32, _P, _P, _P, _P, C.c_float, _P]),
     ("sm_run_batch_multi", C.c_int, [C.POINTER(_P), C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_float, _P]),
+    ("sm_set_schedule", C.c_int, [_P, C.c_int32, C.c_int32]),
     ("sm_synchronize", C.c_int, [_P]),
     ("sm_stream", C.c_void_p, [_P]),
     ("sm_profile_enable", C.c_int, [_P, C.c_int32]),
@@ -81,6 +82,7 @@ SIGNATURES = [
     ("sm_expf_host", C.c_float, [C.c_float]),
     ("sm_expf_device_range", C.c_int, [_P, C.c_uint32, C.c_uint32, _P]),
     ("sm_div_area_check", C.c_int, [_P, C.c_int32, C.c_int32, _P]),
+    ("sm_copy_ceiling", C.c_int, [_P, C.c_uint64, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     ("sm_get_census", C.c_int, [_P, C.c_int32, _P]),
 ]
 

@@ -312,6 +312,27 @@ void build_luts(sm_ctx* c) {
     }
 }
 
+// sm_params.num_streams / sub_batch -> the schedule sm_run follows (sm_create, sm_set_schedule).
+// num_streams 0 (auto): two streams with CBCA at volumes >= 256 MiB per pair, where the next
+// group's prep, cost and H scan share the CUs with this group's LDS-bound NORM_SCAN sweep
+// (full resolution 37.8 -> 36.0 ms, 1080p x8 53.0 -> 50.3 ms, profiles/r4j); and for batches of
+// >= 8 smaller pairs with 4-path SGM and no refinement (Teddy x16 in two groups of 8: 2.60 ->
+// 2.54 ms, profiles/r4q; KITTI's 8-path SGM got slower, 8.27 -> 8.52 ms).  Side streams are
+// created on first use and kept.
+sm_status apply_schedule(sm_ctx* c, int num_streams, int sub_batch) {
+    const sm_params& p = c->p;
+    if (sub_batch < 0 || num_streams < 0 || num_streams > 4)
+        return fail(c, SM_EINVAL, "sub_batch >= 0 and num_streams in [0, 4] required");
+    c->sub_batch = sub_batch;
+    c->auto_groups = num_streams == 0 && p.aggregation == SM_AGG_CBCA && p.cbca_iterations > 0 &&
+                     (c->nvol * 4 >= ((size_t)1 << 28) ||
+                      (c->cap >= 8 && p.optimization == SM_OPT_SGM && p.sgm_paths == 4 && !p.do_refine));
+    c->nstreams = c->auto_groups ? 2 : (num_streams < 1 ? 1 : num_streams);
+    for (int i = 0; i + 1 < c->nstreams; i++)
+        if (!c->xst[i]) HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking));
+    return SM_OK;
+}
+
 template <typename T>
 sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
     if (count == 0) count = 1;
@@ -1076,17 +1097,7 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         // size (Teddy x16: 0.765 -> 0.692 ms, profiles/r4b/ab_teddy.txt)
         const bool nsv = cbca_lag(*p) == 34 && p->num_disparities % 64 == 0;
         c->fuse_norm_scan = p->fuse_norm_scan == 1 || (p->fuse_norm_scan == -1 && (nsv || c->nvol * 4 >= ((size_t)1 << 28)));
-        c->sub_batch = p->sub_batch;
-        // num_streams 0 (auto): two streams with CBCA at volumes >= 256 MiB per pair, where the
-        // next group's prep, cost and H scan share the CUs with this group's LDS-bound NORM_SCAN
-        // sweep (full resolution 37.8 -> 36.0 ms, 1080p x8 53.0 -> 50.3 ms, profiles/r4j); and for
-        // batches of >= 8 smaller pairs with 4-path SGM and no refinement (Teddy x16 in two groups
-        // of 8: 2.60 -> 2.54 ms, profiles/r4q; KITTI's 8-path SGM got slower, 8.27 -> 8.52 ms)
-        c->auto_groups = p->num_streams == 0 && p->aggregation == SM_AGG_CBCA && p->cbca_iterations > 0 &&
-                         (c->nvol * 4 >= ((size_t)1 << 28) ||
-                          (cap >= 8 && p->optimization == SM_OPT_SGM && p->sgm_paths == 4 && !p->do_refine));
-        c->nstreams = c->auto_groups ? 2 : (p->num_streams < 1 ? 1 : p->num_streams);
-        for (int i = 0; i + 1 < c->nstreams; i++) HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking));
+        if ((s = apply_schedule(c, p->num_streams, p->sub_batch))) return s;
         for (int i = 0; i < 16; i++) {
             hipEvent_t e;
             HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1533,6 +1544,17 @@ sm_status sm_run_batch_multi(sm_ctx* const* ctxs, int32_t nctx, int32_t n, const
     return SM_OK;
 }
 
+sm_status sm_set_schedule(sm_ctx* c, int32_t num_streams, int32_t sub_batch) {
+    sm_status s = check(c);
+    if (s) return s;
+    // (the previous sm_run joined its side streams into the main stream, so the next run's
+    // groups are ordered after it whichever streams they use)
+    if ((s = apply_schedule(c, num_streams, sub_batch))) return s;
+    c->p.num_streams = num_streams;
+    c->p.sub_batch = sub_batch;
+    return SM_OK;
+}
+
 sm_status sm_synchronize(sm_ctx* c) {
     sm_status s = check(c);
     if (s) return s;
@@ -1636,6 +1658,47 @@ sm_status sm_expf_device_range(sm_ctx* c, uint32_t first_bits, uint32_t n, float
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);
     hipFree(dbuf);
     if (e != hipSuccess) return hip_fail(c, e, "sm_expf_device_range");
+    return SM_OK;
+}
+
+sm_status sm_copy_ceiling(sm_ctx* c, uint64_t bytes, int32_t reps, double* best_gbs, double* median_gbs) {
+    sm_status s = check(c);
+    if (s) return s;
+    if (!best_gbs || !median_gbs || reps < 1 || reps > 1000 || bytes < 16384) return fail(c, SM_EINVAL, "bad arguments");
+    bytes = bytes / 16384 * 16384;
+    char *src = nullptr, *dst = nullptr;
+    if ((s = dalloc(c, &src, bytes))) return s;
+    if ((s = dalloc(c, &dst, bytes))) {
+        hipFree(src);
+        return s;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::vector<double> gbs;
+    hipError_t e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipMemsetAsync(src, 1, bytes, c->st);
+    // grid sizes bracketing the volume sweeps' launch shapes; every (grid, repetition) is one sample
+    for (int grid : {4096, 16384, 65536}) {
+        for (int r = 0; r < reps + 1 && e == hipSuccess; r++) {
+            if ((e = hipEventRecord(e0, c->st)) != hipSuccess) break;
+            sm::launch_copy_x4(src, dst, bytes, grid, c->st);
+            if ((e = hipGetLastError()) != hipSuccess) break;
+            if ((e = hipEventRecord(e1, c->st)) != hipSuccess) break;
+            if ((e = hipEventSynchronize(e1)) != hipSuccess) break;
+            float ms = 0.f;
+            if ((e = hipEventElapsedTime(&ms, e0, e1)) != hipSuccess) break;
+            if (r > 0 && ms > 0.f) gbs.push_back(2.0 * (double)bytes / (ms * 1e-3) / 1e9);   // read + write
+        }
+    }
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    hipFree(src);
+    hipFree(dst);
+    if (e != hipSuccess) return hip_fail(c, e, "sm_copy_ceiling");
+    if (gbs.empty()) return fail(c, SM_EHIP, "sm_copy_ceiling: no timing samples");
+    std::sort(gbs.begin(), gbs.end());
+    *best_gbs = gbs.back();
+    *median_gbs = gbs[gbs.size() / 2];
     return SM_OK;
 }
 

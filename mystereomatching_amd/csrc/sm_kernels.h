@@ -195,6 +195,7 @@ int sgm_ck_seg(int D);
 void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st);
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);
+void launch_copy_x4(const void* in, void* out, size_t bytes, int grid, hipStream_t st);   // bytes % 16384 == 0
 void launch_div_check(int exp2, int bmax, unsigned long long* bad, hipStream_t st);
 float expf_host(float x);
 // refinement (sm_refine.hip)

@@ -1185,9 +1185,29 @@ __global__ void k_expf_range(uint32_t first, uint32_t n, float* __restrict__ out
         out[i] = dev_expf(__builtin_bit_cast(float, first + i));
 }
 
+// Measured HBM ceiling for the roofline: a dwordx4 copy, each workgroup moving
+// whole 16 KB blocks (256 lanes x 4 dwordx4 in flight per lane), non-temporal loads and stores
+// like the volume sweeps, XCD-ordered so that consecutive blocks share an XCD's L2.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_copy_x4(const u32x4* __restrict__ in, u32x4* __restrict__ out, size_t nblk) {
+    const size_t stride = gridDim.x;
+    for (size_t b = xcd_swizzle(blockIdx.x, gridDim.x); b < nblk; b += stride) {
+        const size_t i0 = b * 1024 + threadIdx.x;
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = __builtin_nontemporal_load(in + i0 + 256 * k);
+#pragma unroll
+        for (int k = 0; k < 4; k++) __builtin_nontemporal_store(v[k], out + i0 + 256 * k);
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
+void launch_copy_x4(const void* in, void* out, size_t bytes, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_copy_x4, dim3(grid), dim3(256), 0, st, (const u32x4*)in, (u32x4*)out, bytes / 16384);
+}
+
 template <int METHOD, bool LAM1, int CW, bool OORZ>
 static void launch_cost_z(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
     if (a.D <= 64)

@@ -355,6 +355,20 @@ class StereoBatch:
         self._async_out.append(out)
         return out
 
+    def copy_ceiling(self, nbytes: int, reps: int = 5):
+        """sm_copy_ceiling: (best, median) GB/s of a dwordx4 device copy of nbytes (read + write)."""
+        best, med = C.c_double(), C.c_double()
+        st = self._lib.sm_copy_ceiling(self._ctx, int(nbytes), int(reps), C.byref(best), C.byref(med))
+        _capi.check(self._lib, self._ctx, st, "copy_ceiling")
+        return best.value, med.value
+
+    def set_schedule(self, num_streams: int = 0, sub_batch: int = 0):
+        """sm_set_schedule: num_streams / sub_batch for the following runs on the same allocations
+        (0 / 0 = the auto default); maps are identical under every schedule."""
+        st = self._lib.sm_set_schedule(self._ctx, int(num_streams), int(sub_batch))
+        _capi.check(self._lib, self._ctx, st, "set_schedule")
+        self.params.num_streams, self.params.sub_batch = int(num_streams), int(sub_batch)
+
     def synchronize(self):
         _capi.check(self._lib, self._ctx, self._lib.sm_synchronize(self._ctx), "sync")
         self._async_out.clear()

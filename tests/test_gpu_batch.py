@@ -73,6 +73,37 @@ def test_multi_stream_sub_batches(oracle, sub_batch, num_streams):
         sb.close()
 
 
+def test_set_schedule_same_context(oracle):
+    """sm_set_schedule switches num_streams / sub_batch between runs of one context (the bench's
+    same-allocation schedule A/B): every schedule, including side streams created on first use and
+    a return to one stream, gives the oracle's maps; out-of-range schedules are refused."""
+    from mystereomatching_amd._capi import SMError
+    H, W, md, n = 29, 61, 31, 9
+    batch = S.make_batch(n, H, W, md + 1, first_index=560)
+    sb = StereoBatch(md, H, W, n, device=0, num_streams=1)
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        want = _oracle_maps(oracle, batch, H, W, md)
+        for ns, sub in ((1, 0), (0, 0), (3, 2), (1, 0), (2, 4), (0, 0)):
+            sb.set_schedule(ns, sub)
+            np.testing.assert_array_equal(sb.run(0.3), want, err_msg=f"num_streams {ns} sub_batch {sub}")
+        for ns, sub in ((5, 0), (-1, 0), (1, -2)):
+            with pytest.raises(SMError):
+                sb.set_schedule(ns, sub)
+    finally:
+        sb.close()
+
+
+def test_copy_ceiling_runs():
+    """sm_copy_ceiling returns a positive best >= median rate below the 8 TB/s spec (x1.1)."""
+    sb = StereoBatch(15, 16, 32, 1, device=0)
+    try:
+        best, med = sb.copy_ceiling(1 << 30, reps=2)
+        assert 0 < med <= best < 8800
+    finally:
+        sb.close()
+
+
 def test_auto_two_groups(oracle):
     """num_streams 0 (auto) with batch_capacity >= 8, CBCA and 4-path SGM: sm_run splits the 9
     pairs into groups of 5 and 4 on two streams, the second starting after the first's first CBCA

@@ -126,6 +126,12 @@ def parse():
                     help="time the product multi-GPU path instead of resident batches: rank 0 holds the global "
                          "batch on the host; each step broadcasts the header, scatters the pairs (RCCL), runs "
                          "them and gathers the int16 maps back (mystereomatching_amd.batch.DistributedBatchRunner)")
+    ap.add_argument("--e2e-sub-batch", default="0",
+                    help="--e2e: the sub-blocks of a rank's pairs (DistributedBatchRunner sub_batch): s pairs each, "
+                         "a comma list of sizes, or 0 = auto (batch.sub_sizes)")
+    ap.add_argument("--e2e-input", choices=["pinned", "numpy"], default="pinned",
+                    help="--e2e: rank 0's host batch as page-locked torch tensors (batch.pinned_batch) or numpy "
+                         "arrays (staged into page-locked buffers by the runner's copy threads)")
     ap.add_argument("--agg", default="CBCA", choices=["CBCA", "GF", "NL"],
                     help='aggregation selector (h:52): "CBCA" (default), "GF" guided filter (cpp:4492-4516, the shipped '
                          'ximgproc::guidedFilter form; sm_params.gf_mode = 1 for MY_GUIDE), '
@@ -433,8 +439,12 @@ def _e2e_batch(args, world, rank, local, dist, backend, batch, H, W, md, paths, 
     D = md + 1
     fn = None
     try:
-        glob = {k: np.ascontiguousarray(np.concatenate([batch[k]] * world)) for k in ("lbgr", "rbgr", "lgray", "rgray")} \
-            if rank == 0 else None
+        glob = None
+        if rank == 0:   # page-locked host batch (batch.pinned_batch): the runner's copies need no staging
+            from mystereomatching_amd.batch import pinned_batch
+            glob = pinned_batch(B * world, H, W)
+            for k in glob:
+                glob[k].numpy()[...] = np.concatenate([batch[k]] * world)
         fn = hip_compute_fn(md, H, W, B, local, sgm_paths=paths)
         runner = DistributedBatchRunner(fn)
         maps = runner.run(glob, md, 0.3)   # warm-up
@@ -456,10 +466,12 @@ def _e2e_batch(args, world, rank, local, dist, backend, batch, H, W, md, paths, 
                 and args.opt == "sgm" and not args.refine else None
             if fx is not None:
                 ok = ok and fx["bit_exact"]
+        runner.close()
         return {"value": round(world * B * H * W * D * steps / el / 1e6, 2), "unit": "Mdisp/s",
                 "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "global_batch": world * B,
-                "path": f"DistributedBatchRunner ({backend}): header broadcast, scatter of host pairs from rank 0, "
-                        "compute, gather of the int16 maps to rank 0 host memory",
+                "path": f"DistributedBatchRunner ({backend}): header broadcast, sub-blocks of pairs staged from "
+                        "page-locked host memory on rank 0 and scattered while the previous sub-block computes, "
+                        "int16 maps gathered to rank 0 host memory while the next one computes",
                 "maps_ok": ok}
     except Exception as e:   # noqa: BLE001 -- reported, not raised
         return {"error": f"{type(e).__name__}: {e}"[:300]}
@@ -474,15 +486,22 @@ def run_e2e(args, world, rank, local, dist, backend):
     second.  No roofline / CPU baseline here: the resident-batch line is the kernel measurement."""
     import torch
     from mystereomatching_amd import synthetic as S
-    from mystereomatching_amd.batch import DistributedBatchRunner, hip_compute_fn
+    from mystereomatching_amd.batch import DistributedBatchRunner, hip_compute_fn, sub_sizes
 
     H, W, md, paths, B0, desc = WORKLOADS[args.workload]
     B = args.batch or B0
     D = md + 1
     n = B * world
     batch = S.make_batch(n, H, W, D) if rank == 0 else None
+    if batch is not None and args.e2e_input == "pinned":
+        from mystereomatching_amd.batch import pinned_batch
+        pb = pinned_batch(n, H, W)
+        for k in pb:
+            pb[k].numpy()[...] = batch[k]
+        batch = pb
     fn = hip_compute_fn(md, H, W, B, local, sgm_paths=paths)
-    runner = DistributedBatchRunner(fn)
+    sub = [int(x) for x in args.e2e_sub_batch.split(",")] if "," in args.e2e_sub_batch else int(args.e2e_sub_batch)
+    runner = DistributedBatchRunner(fn, sub_batch=sub)
 
     def barrier():
         if dist is not None:
@@ -516,9 +535,12 @@ def run_e2e(args, world, rank, local, dist, backend):
             "data": "synthetic (seeded piecewise-planar pairs, mystereomatching_amd/synthetic.py), host-resident on rank 0",
             "config": {"workload": desc + " -- end to end: broadcast header, scatter pairs, compute, gather maps",
                        "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": n, "sgm_paths": paths,
-                       "parallelism": f"dp{world} via DistributedBatchRunner ({backend})", "e2e": True},
+                       "parallelism": f"dp{world} via DistributedBatchRunner ({backend})", "e2e": True,
+                       "e2e_input": args.e2e_input, "sub_blocks": sub_sizes(B, sub),
+                       "timed_region": "rank 0 host batch -> maps in rank 0 host memory"},
             "parity": parity,
         }))
+    runner.close()
     fn.close()
     if dist is not None:
         dist.destroy_process_group()

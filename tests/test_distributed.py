@@ -30,7 +30,7 @@ def _oracle_fn():
     return run
 
 
-def _worker(rank, world, port, n, out_path):
+def _worker(rank, world, port, n, out_path, sub_batch=0, tensor_in=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -39,9 +39,16 @@ def _worker(rank, world, port, n, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mystereomatching_amd import synthetic as S
-        runner = DistributedBatchRunner(_oracle_fn())
+        import torch
+        runner = DistributedBatchRunner(_oracle_fn(), sub_batch=sub_batch)
         batch = S.make_batch(n, H, W, MD + 1, first_index=50) if rank == 0 else None
+        if batch is not None and tensor_in:
+            batch = {k: torch.from_numpy(np.ascontiguousarray(batch[k])) for k in ("lbgr", "rbgr", "lgray", "rgray")}
         disp = runner.run(batch, max_disp=MD, reg_lambda=0.3)
+        disp2 = runner.run(batch, max_disp=MD, reg_lambda=0.3)   # reused staging buffers
+        if rank == 0:
+            np.testing.assert_array_equal(disp2, disp)
+        runner.close()
         if rank == 0:
             np.save(out_path, disp)
         else:
@@ -60,6 +67,43 @@ def test_two_rank_scatter_gather_matches_single(tmp_path, n):
     ref = _oracle_fn()({k: batch[k] for k in ("lbgr", "rbgr", "lgray", "rgray")}, 0.3)
     assert got.shape == (n, H, W)
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("n,sub_batch,tensor_in", [(7, 1, False), (7, 3, False), (5, 2, True), (8, 0, False),
+                                                    (11, (1, 3), False)])
+def test_two_rank_sub_blocks(tmp_path, n, sub_batch, tensor_in):
+    """Sub-blocks of s pairs per rank (scatter k + 1 and gather k - 1 in flight around compute k):
+    ragged blocks, a last sub-block shorter than s, torch inputs, the auto size; maps in order."""
+    out = str(tmp_path / "disp.npy")
+    mp.spawn(_worker, args=(2, _free_port(), n, out, sub_batch, tensor_in), nprocs=2, join=True)
+    got = np.load(out)
+    from mystereomatching_amd import synthetic as S
+    batch = S.make_batch(n, H, W, MD + 1, first_index=50)
+    ref = _oracle_fn()({k: batch[k] for k in ("lbgr", "rbgr", "lgray", "rgray")}, 0.3)
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_single_process_sub_blocks():
+    """No process group: the runner pipelines rank 0's own sub-blocks (host compute function)."""
+    from mystereomatching_amd import synthetic as S
+    n = 5
+    batch = S.make_batch(n, H, W, MD + 1, first_index=90)
+    ref = _oracle_fn()({k: batch[k] for k in ("lbgr", "rbgr", "lgray", "rgray")}, 0.3)
+    for sb in (0, 1, 2, 5):
+        r = DistributedBatchRunner(_oracle_fn(), sub_batch=sb)
+        np.testing.assert_array_equal(r.run(batch, max_disp=MD, reg_lambda=0.3), ref)
+        r.close()
+
+
+def test_sub_sizes():
+    from mystereomatching_amd.batch import sub_sizes
+    assert [sub_sizes(p) for p in (0, 1, 2, 3, 4, 8, 9, 16)] == \
+        [[], [1], [1, 1], [1, 1, 1], [1, 2, 1], [1, 6, 1], [1, 7, 1], [2, 12, 2]]
+    for p in range(0, 40):
+        for sb in (0, 1, 3, 7, [2, 4], (1, 6, 1), [50]):
+            z = sub_sizes(p, sb)
+            assert sum(z) == p and all(q > 0 for q in z)
+    assert sub_sizes(8, 3) == [3, 3, 2] and sub_sizes(8, [1, 6]) == [1, 6, 1]
 
 
 def test_shard_bounds_cover_exactly_once():

@@ -171,22 +171,51 @@ def _rccl_world_one():
         dist.destroy_process_group()
 
 
-def test_runner_rccl_world_one(oracle):
+@pytest.mark.parametrize("sub_batch,inp", [(0, "numpy"), (1, "pinned"), (2, "numpy"), (2, "device")])
+def test_runner_rccl_world_one(oracle, sub_batch, inp):
     """DistributedBatchRunner over an initialised `nccl` (RCCL) process group of size 1: header
     broadcast, scatter and gather run as RCCL collectives on device tensors, as on the 8-GPU node
-    (configs[4]); the maps must equal the oracle's."""
-    H, W, md, n = 30, 52, 15, 3
+    (configs[4]), in sub-blocks (scatter k + 1 and gather k - 1 in flight around compute k) from
+    numpy, page-locked or device inputs; the maps must equal the oracle's."""
+    import torch
+    from mystereomatching_amd.batch import pinned_batch
+    H, W, md, n = 30, 52, 15, 5
     batch = S.make_batch(n, H, W, md + 1, first_index=440)
+    src = batch
+    if inp == "pinned":
+        src = pinned_batch(n, H, W)
+        for k in KEYS:
+            src[k].numpy()[...] = batch[k]
+    elif inp == "device":
+        src = {k: torch.from_numpy(np.ascontiguousarray(batch[k])).cuda() for k in KEYS}
     with _rccl_world_one():
         fn = hip_compute_fn(md, H, W, n, device=0)
         try:
-            runner = DistributedBatchRunner(fn)
+            runner = DistributedBatchRunner(fn, sub_batch=sub_batch)
             assert runner.collective and runner.device.type == "cuda"
             want = _oracle_maps(oracle, batch, H, W, md)
-            for _ in range(2):
-                np.testing.assert_array_equal(runner.run(batch, max_disp=md, reg_lambda=0.3), want)
+            for _ in range(3):
+                np.testing.assert_array_equal(runner.run(src, max_disp=md, reg_lambda=0.3), want)
+            runner.close()
         finally:
             fn.close()
+
+
+@pytest.mark.parametrize("sub_batch", [1, 3])
+def test_runner_single_process_sub_blocks(oracle, sub_batch):
+    """No process group, device compute: sub-block k + 1's inputs are copied on the copy stream
+    while sub-block k computes and its maps copied out after; maps in order, runs repeatable."""
+    H, W, md, n = 30, 52, 15, 7
+    batch = S.make_batch(n, H, W, md + 1, first_index=480)
+    fn = hip_compute_fn(md, H, W, n, device=0)
+    try:
+        runner = DistributedBatchRunner(fn, sub_batch=sub_batch)
+        want = _oracle_maps(oracle, batch, H, W, md)
+        for _ in range(2):
+            np.testing.assert_array_equal(runner.run(batch, max_disp=md, reg_lambda=0.3), want)
+        runner.close()
+    finally:
+        fn.close()
 
 
 def test_runner_rccl_hd1080_rank_shard():

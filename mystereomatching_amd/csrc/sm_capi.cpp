@@ -1006,8 +1006,8 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->gx, cap * 2 * c->npix))) return s;
     if ((s = dalloc(c, &c->gy, cap * 2 * c->npix))) return s;
     {
-        // front pad: V sweeps read rows i - lag >= -2 lag; tail pad: the fast V sweep's loads run
-        // up to 2 lag + 3 T rows past the last plane's end (sm_cbca.hip NsV)
+        // front pad: V sweeps read rows i - lag >= -2 lag; tail pad: the fast V sweep's arm loads
+        // run up to lag + T rows past the last plane's end (sm_cbca.hip NsV clamps later tiles)
         const size_t pad = ((size_t)2 * cbca_lag(*p) * p->cols * 4 + 255) / 256 * 256;
         const size_t tail = (size_t)(2 * cbca_lag(*p) + 64) * p->cols * 4;
         c->arms_bytes = cap * 2 * 2 * c->npix * 4;

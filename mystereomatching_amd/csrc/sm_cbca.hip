@@ -452,16 +452,29 @@ struct CbLine {
 // V NORM_SCAN at the reference's lag (LAG = cbca_crossL_out = 34, h:266): the fused sweep that
 // runs iteration 0's V normalisation and iteration 1's V scan (full resolution, 1080p).  Same
 // arithmetic, order and ring contents as CbLine<false, CB_NORM_SCAN, ...>; what differs is the
-// instruction budget of a position (the sweep issues at under one wave per SIMD, so every
-// instruction of a position is on the critical path):
+// instruction budget of a position and the order the stages of neighbouring tiles are issued in
+// (the sweep runs at one wave per SIMD: its rings allow three waves per CU, so every LDS round
+// trip a wave waits for is lost issue time):
+//  * a tile's work is four stages: A (rows j0 .. j0+T-1 into the S1 / area rings, the tile's
+//    pass intersections), B1 (the window slots and S1 / area reads of the normalised outputs at
+//    i = j - LAG), B2 (division, S2 prefix and ring writes) and C (the scan outputs at
+//    i2 = j - 2 LAG: S2 reads, differences, stores).  They are software-pipelined over
+//    tiles: body n issues A(n + 1) while B1(n)'s reads are in flight, and B1(n + 1)'s slot
+//    arithmetic and reads while C(n)'s reads are in flight, so each wait for an LDS read
+//    finds the reads long returned.  LDS accesses of one wave complete in issue order, so
+//    A(n + 1)'s ring writes cannot overtake B1(n)'s reads of the slots they reuse: the rings
+//    keep their size (2 LAG + T + 1 slots);
 //  * ring reads take the tile position k from the LDS instruction's immediate offset.  The slot
 //    pair of a window is computed once per position against the tile's uniform base C (one
 //    v_pk_mad_u16 + a packed wrap), and C-relative slot + k may pass the ring's end by up to
 //    T - 2 slots: the first T - 1 slots are mirrored past the end (written again by the tile that
 //    writes ring slot 0), so no position needs scalar slot arithmetic;
+//  * S2 holds position p at slot p mod R like S1, so the scan stage's window at i2 = j - 2 LAG
+//    sits at the very slots the norm stage's window at i = (j - LAG) - LAG read LAG positions
+//    earlier: the loop keeps those S1 read addresses (head, tail) of the last NH tiles, and the
+//    scan stage reads S2 at them plus the ring distance (an LDS immediate);
 //  * T = 7, so that the two S rings, the u16 area ring and their mirrors still fit three waves
-//    per CU (83 slots x 10 B x 64 lanes); two tiles of loads in flight; a six-tile loop whose
-//    registers hold the last five tiles' pass intersections (the scan stage's, REUSE2 above);
+//    per CU (83 slots x 10 B x 64 lanes); three tiles of loads in flight; a six-tile loop;
 //  * tile resources advance incrementally: the volume base by T rows (tiles past the line read
 //    nothing; the allocations carry tail pads for the tiles that straddle the end), the arm
 //    gathers and own-arm loads through fixed per-plane resources with a uniform row offset;
@@ -471,12 +484,12 @@ struct CbLine {
 #ifndef SM_CB_T_NSV
 #define SM_CB_T_NSV 7
 #endif
-#ifndef SM_CB_NSV
-#define SM_CB_NSV 1   // 0: the generic REUSE2 sweep (A/B builds)
+#ifndef SM_CB_NSV_VMWAIT
+#define SM_CB_NSV_VMWAIT 1   // one explicit vmcnt wait per tile for the stage-A inputs
 #endif
-#ifndef SM_CB_NSV_AH
-#define SM_CB_NSV_AH 1   // 1: the scan stage reads at the norm stage's saved addresses (S2 at slot p mod R)
-#endif
+// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= n only
+__host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (0xf << 8) | (0x7 << 4) | (n & 0xf); }
+static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
 constexpr int cbca_nsv_ring() { return (2 * NSV_LAG + SM_CB_T_NSV + 1 + SM_CB_T_NSV - 1) / SM_CB_T_NSV * SM_CB_T_NSV; }
 constexpr int cbca_nsv_phys() { return cbca_nsv_ring() + SM_CB_T_NSV - 1; }
@@ -489,9 +502,10 @@ struct NsV {
     static constexpr int LAG = NSV_LAG;
     static constexpr int R = cbca_nsv_ring();            // logical ring slots (multiple of T)
     static constexpr int P = cbca_nsv_phys();            // physical slots: R + the mirror of 0 .. T-2
-    static constexpr int DTMIN = -((LAG + T - 1) / T);   // oldest tile a pass intersection is reused from
+    static constexpr int DTMIN = -((LAG + T - 1) / T);   // oldest tile a saved address is reused from
     static constexpr int NH = -DTMIN + 1;                // tiles in the loop = history depth
-    static_assert(NH % 3 == 0, "two tiles in flight rotate three load buffers through the loop");
+    static constexpr int SHIFT = (T - (2 * LAG) % T) % T;   // the tile grid starts at row -SHIFT
+    static_assert(NH % 3 == 0, "three load buffers rotate through the loop");
     static_assert(2 * LAG + T + 1 <= R && R % T == 0, "ring");
     static_assert((T + (LAG + T - 1)) / T <= NH, "history");
 
@@ -500,10 +514,14 @@ struct NsV {
         uint32_t a0[2];       // lane k < T: own arm pair, set 0 at row j0 + k - LAG, set 1 at row j0 + k
         uint32_t a1[2][T];    // the other image's pair at (row, u -/+ d)
     };
+    struct Norm {             // B1 -> B2: the S1 and area window ends of a tile's outputs
+        float sh[T], st[T];
+        us2 ah[(T + 1) / 2], at[(T + 1) / 2];   // position k in half k % 2 of word k / 2
+    };
 
     // volume
     const char* xld;          // (pair, row jld, column u, chunk): the next tile to load
-    const char* xst;          // (pair, row j0 - 2 LAG, ...): the scan outputs of the next tile to process
+    const char* xst;          // (pair, row j0 - 2 LAG, ...): the scan outputs of the next tile to store
     int jld;                  // first row of the next tile to load
     uint32_t vsb;             // bytes per row
     int rows_avail;           // rows from row 0 that lie inside the allocation (+ tail pad)
@@ -512,37 +530,36 @@ struct NsV {
     __amdgpu_buffer_rsrc_t A0r[2], A1r[2];
     uint32_t rowb;            // bytes per arm row (W * 4)
     uint32_t rld;             // (jld + pad rows) * rowb: row offset of the next tile's set-1 arms
+    uint32_t rld_max;         // its clamp: tiles past the line end re-read rows inside the tail pad
     uint32_t aown;            // own loads: lane k < T -> row k of the tile (else out of range)
     uint32_t ao[T];           // gathers: column u -/+ d of tile row k (out of range outside the image)
     int lane, len;
+    int jst;                  // first scan-output row of the next tile to store (j0 - 2 LAG)
+    int jnm;                  // first normalised-output row of the next tile's stage B2 (j0 - LAG)
     // rings
-    uint32_t o1, o2, oa;      // LDS byte address of this lane's slot-0 entry in r1, r2, ra
+    uint32_t o1, oa;          // LDS byte address of this lane's slot-0 entry in r1, ra
     float* r1;
     float* r2;
     uint16_t* ra;
     uint32_t RR;              // (R, -R) mod 2^16
     float S1, S2;
     uint32_t Acc;
-    int ws;                   // ring slot of the tile's first input row (multiple of T)
-#if SM_CB_NSV_AH
-    // S2 holds position p at slot p mod R like S1, so the scan stage's window at i2 = j - 2 LAG
-    // sits at the very slots the norm stage's window at i = (j - LAG) - LAG read LAG positions
-    // earlier: the history keeps those S1 read addresses (head, tail) of the last NH tiles, and
-    // the scan stage reads S2 at them plus the ring distance, with no slot arithmetic of its own
-    uint32_t hh[NH][T], ht[NH][T];
-#else
-    uint32_t ph[NH][T];       // pass intersections of the last NH tiles (slot = tile index mod NH)
-#endif
+    int wsa;                  // ring slot of the next stage-A tile's first input row (multiple of T)
+    uint32_t hh[NH][T], ht[NH][T];   // S1 head / tail addresses read by the last NH tiles' B1
 
-    // loads the next tile (tiles are loaded in order, T rows apart)
+    // loads the next tile (tiles are loaded in order, T rows apart); FIRST: the tile at row
+    // -SHIFT, whose rows before the line read 0 (out-of-range offsets)
+    template <bool FIRST = false>
     __device__ __forceinline__ void load(Tile& t) {
         // tiles whose rows pass the allocation (only ever past the line end) read 0
         const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xld, jld + T <= rows_avail ? 0x7fffffff : 0);
 #pragma unroll
-        for (int k = 0; k < T; k++) t.x[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, (int)xo[k], 0, 2));
+        for (int k = 0; k < T; k++)
+            t.x[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, (FIRST && k < SHIFT) ? (int)0x80000000 : (int)xo[k], 0, 2));
 #pragma unroll
         for (int s = 0; s < 2; s++) {
-            const uint32_t roff = s == 0 ? rld - (uint32_t)LAG * rowb : rld;   // rows >= -2 LAG: >= 0
+            const uint32_t rl = min(rld, rld_max);
+            const uint32_t roff = s == 0 ? rl - (uint32_t)LAG * rowb : rl;   // rows >= -2 LAG: >= 0
             t.a0[s] = __builtin_amdgcn_raw_buffer_load_b32(A0r[s], (int)aown, (int)roff, 0);
 #pragma unroll
             for (int k = 0; k < T; k++) t.a1[s][k] = __builtin_amdgcn_raw_buffer_load_b32(A1r[s], (int)ao[k], (int)roff, 0);
@@ -554,34 +571,22 @@ struct NsV {
 
     // (C - 1 - tail, C + head) of pair p wrapped into [0, R): the window's tail and head slots
     // relative to the tile's first output (tile position k adds k, served by the mirror)
-    __device__ __forceinline__ uint32_t slots(uint32_t p, uint32_t cc) const {
+    // (ccr = cc + (R, -R): two independent v_pk_mad_u16 and a v_pk_min_u16; a dependent
+    // v_pk_add_u16 between them costs an s_nop pair per position on gfx950)
+    __device__ __forceinline__ uint32_t slots(uint32_t p, uint32_t cc, uint32_t ccr) const {
         // (a v_pk_mad_u16: tail * 0xffff + C - 1, head * 1 + C)
         const us2 q = __builtin_bit_cast(us2, p) * us2{0xffff, 1} + __builtin_bit_cast(us2, cc);
-        const us2 w = q + __builtin_bit_cast(us2, RR);
+        const us2 w = __builtin_bit_cast(us2, p) * us2{0xffff, 1} + __builtin_bit_cast(us2, ccr);
         return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, w));
     }
-    template <int H_, typename E>
-    __device__ __forceinline__ E rd(uint32_t sp, uint32_t o, int k) const {
-        typedef __attribute__((address_space(3))) const E lds_e;
-        return ((lds_e*)(size_t)mad_u32_u16<H_>(sp, 64u * (uint32_t)sizeof(E), o))[k * 64];
-    }
-    __device__ __forceinline__ void store(const __amdgpu_buffer_rsrc_t& r, int k, float v) const {
-        buf_st(r, xo[k], 0, v);
-    }
+    // ring slot of output row i0 = j0 - LAG of the tile whose first input row sits at slot ws
+    __device__ __forceinline__ static int out_slot(int ws) { return ws - LAG < 0 ? ws - LAG + R : ws - LAG; }
 
-#if SM_CB_NSV_AH
-    // One code copy for every tile: the two line ends differ only in uniform branches around the
-    // zeroing of pre-line inputs and the stores' offsets, so the saved addresses need no copies
-    // at a merge of two tile variants.
-    template <int RT>   // RT: the tile's slot in the NH-tile loop
-    __device__ __forceinline__ void tile(const Tile& t, int j0, bool guard) {
-        const int C = ws - LAG < 0 ? ws - LAG + R : ws - LAG;   // ring slot of output row i0 = j0 - LAG
-        const uint32_t cc = ((uint32_t)(C - 1) & 0xffffu) | ((uint32_t)C << 16);
-        const bool mirror = ws == 0;
-        float* w1 = r1 + ws * 64 + lane;
-        uint16_t* wa = ra + ws * 64 + lane;
-        // phase A: rows j0 .. j0+T-1 into the S1 / area rings; pass intersections at i = j - LAG
-        uint32_t pi[T];
+    // stage A: rows j0 .. j0+T-1 into the S1 / area rings at slot wsa; pass intersections pi
+    __device__ __forceinline__ void stage_a(const Tile& t, uint32_t (&pi)[T]) {
+        const bool mirror = __builtin_expect(wsa == 0, 0);
+        float* w1 = r1 + wsa * 64 + lane;
+        uint16_t* wa = ra + wsa * 64 + lane;
         float s1v[T];
         uint16_t acv[T];
 #pragma unroll
@@ -602,28 +607,65 @@ struct NsV {
                 ra[(R + k) * 64 + lane] = acv[k];
             }
         }
-        // phase B: normalised outputs at i = j - LAG; their prefix S2 (iteration k+1's scan input)
-        const __amdgpu_buffer_rsrc_t ob2 = buf_rsrc(xst);
-        xst += (long)T * (long)vsb;
+        wsa = wsa + T == R ? 0 : wsa + T;
+    }
+
+    // stage B1: window slots of the normalised outputs at i = j - LAG (C: their first slot) and
+    // their S1 / area reads; the S1 addresses are kept for the scan stage LAG positions later
+    template <int RT>
+    __device__ __forceinline__ void stage_b1(const uint32_t (&pi)[T], int C, Norm& nm) {
         typedef __attribute__((address_space(3))) const float lds_f;
         typedef __attribute__((address_space(3))) const uint16_t lds_h;
-        float qv[T], dv[T], shv[T], stv[T];
-        uint32_t ahv[T], atv[T];
+        const uint32_t cc = ((uint32_t)(C - 1) & 0xffffu) | ((uint32_t)C << 16);
+        const uint32_t ccr = __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, cc) + __builtin_bit_cast(us2, RR));
+        // (all slot pairs first: the dependent packed ops of one position are not adjacent,
+        // which would cost s_nop wait states)
+        uint32_t spv[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) spv[k] = slots(pi[k], cc, ccr);
 #pragma unroll
         for (int k = 0; k < T; k++) {
-            const uint32_t sp = slots(pi[k], cc);
+            const uint32_t sp = spv[k];
             const uint32_t a1h = mad_u32_u16<1>(sp, 256u, o1), a1t = mad_u32_u16<0>(sp, 256u, o1);
             hh[RT][k] = a1h;
             ht[RT][k] = a1t;
-            shv[k] = ((lds_f*)(size_t)a1h)[k * 64];
-            stv[k] = ((lds_f*)(size_t)a1t)[k * 64];
-            ahv[k] = rd<1, uint16_t>(sp, oa, k);
-            atv[k] = rd<0, uint16_t>(sp, oa, k);
+            nm.sh[k] = ((lds_f*)(size_t)a1h)[k * 64];
+            nm.st[k] = ((lds_f*)(size_t)a1t)[k * 64];
+            // (two positions' u16 ends share a register: the second a d16-hi read)
+            nm.ah[k / 2][k % 2] = ((lds_h*)(size_t)mad_u32_u16<1>(sp, 128u, oa))[k * 64];
+            nm.at[k / 2][k % 2] = ((lds_h*)(size_t)mad_u32_u16<0>(sp, 128u, oa))[k * 64];
         }
+    }
+
+    // stage B2: genfinalVm_cbca's division (cpp:3969-3992) of the outputs of tile j0, their
+    // prefix S2 (iteration k+1's scan input) into the S2 ring at slots C .. C+T-1
+    __device__ __forceinline__ void stage_b2(const Norm& nm, int C) {
+        float qv[T], dv[T];
+        uint32_t av[T];
+        // div_area (sm_device.h) on position pairs as packed f32 / u16 ops: the same
+        // operations element by element (v_pk_add_f32, v_pk_sub_u16, v_pk_mul_f32, v_pk_fma_f32)
+        typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int k = 0; k < T; k++) {
-            dv[k] = shv[k] - stv[k];
-            qv[k] = div_area(dv[k], (ahv[k] - atv[k]) & 0xffffu);
+        for (int j = 0; j < T / 2; j++) {
+            const f2 d = f2{nm.sh[2 * j], nm.sh[2 * j + 1]} - f2{nm.st[2 * j], nm.st[2 * j + 1]};
+            const us2 a = nm.ah[j] - nm.at[j];                     // areas modulo 2^16
+            const f2 bf = f2{(float)a.x, (float)a.y};
+            const f2 y = f2{__builtin_amdgcn_rcpf(bf.x), __builtin_amdgcn_rcpf(bf.y)};
+            const f2 q0 = d * y;
+            const f2 r = __builtin_elementwise_fma(-q0, bf, d);
+            const f2 q = __builtin_elementwise_fma(r, y, q0);
+            dv[2 * j] = d.x;
+            dv[2 * j + 1] = d.y;
+            qv[2 * j] = q.x;
+            qv[2 * j + 1] = q.y;
+            av[2 * j] = a.x;
+            av[2 * j + 1] = a.y;
+        }
+        if constexpr (T % 2) {
+            dv[T - 1] = nm.sh[T - 1] - nm.st[T - 1];
+            const us2 a = nm.ah[T / 2] - nm.at[T / 2];
+            av[T - 1] = a.x;
+            qv[T - 1] = div_area(dv[T - 1], av[T - 1]);
         }
         if constexpr (CHECK) {
             // dividends are >= +0, so "0 < dv < 2^-110" is "bits(dv) - 1 < 0x087fffff" (unsigned)
@@ -632,33 +674,40 @@ struct NsV {
             for (int k = 0; k < T; k++) tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
             if (__ballot(tmin < 0x087fffffu)) {
 #pragma unroll
-                for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)((ahv[k] - atv[k]) & 0xffffu);
+                for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)av[k];
             }
         }
-        // S2 of positions i0 .. i0+T-1 at slots C .. C+T-1 (C + k may pass R: the mirror slots;
-        // a logical slot below T - 1 is kept in both copies)
+        // nothing accumulates before the line: outputs at rows < 0 read the arm rows before their
+        // plane (the previous plane's last rows, not a zero pad) and are set to +0 -- a uniform
+        // branch taken by the first tiles only, out of line, with no memory operation in it
+        if (__builtin_expect(jnm < 0, 0)) {
+#pragma unroll
+            for (int k = 0; k < T; k++) qv[k] = (jnm + k >= 0) ? qv[k] : 0.f;
+        }
+        jnm += T;
+        // (C + k may pass R: the mirror slots; a logical slot below T - 1 is kept in both copies)
         float s2v[T];
         float* w2 = r2 + C * 64 + lane;
-        if (guard) {   // nothing accumulates before the line (one uniform branch per tile)
-#pragma unroll
-            for (int k = 0; k < T; k++) qv[k] = (j0 - LAG + k >= 0) ? qv[k] : 0.f;
-        }
 #pragma unroll
         for (int k = 0; k < T; k++) {
             S2 = S2 + qv[k];
             s2v[k] = S2;
             w2[k * 64] = S2;
         }
-        if (C + T - 1 >= R || C <= T - 2) {   // two of the R / T tile positions
+        if (__builtin_expect(C + T - 1 >= R || C <= T - 2, 0)) {   // two of the R / T tile positions
 #pragma unroll
             for (int k = 0; k < T; k++) {
                 if (C + k >= R) r2[(C + k - R) * 64 + lane] = s2v[k];
                 if (C + k <= T - 2) r2[(C + k + R) * 64 + lane] = s2v[k];
             }
         }
-        // phase C: scan outputs at i2 = j - 2 LAG, read at the norm stage's S1 addresses of
-        // position j - LAG (tile RT + dt, index q - dt T) plus the ring distance P slots
-        float s2h[T], s2t[T];
+    }
+
+    // stage C reads: the scan outputs at i2 = j - 2 LAG, read at the norm stage's S1 addresses
+    // of position j - LAG (tile RT + dt, index q - dt T) plus the ring distance P slots
+    template <int RT>
+    __device__ __forceinline__ void stage_c_read(float (&s2h)[T], float (&s2t)[T]) const {
+        typedef __attribute__((address_space(3))) const float lds_f;
 #pragma unroll
         for (int k = 0; k < T; k++) {
             const int q = k - LAG;
@@ -667,141 +716,58 @@ struct NsV {
             s2h[k] = ((lds_f*)(size_t)hh[src][idx])[(idx + P) * 64];
             s2t[k] = ((lds_f*)(size_t)ht[src][idx])[(idx + P) * 64];
         }
-        // (outside the line: an out-of-range offset; both branches issue the same vector-memory
-        // sequence, so the loop's vmcnt waits stay exact)
-        if (guard) {
-#pragma unroll
-            for (int k = 0; k < T; k++) {
-                const bool in = (unsigned)(j0 - 2 * LAG + k) < (unsigned)len;
-                buf_st(ob2, in ? xo[k] : 0x80000000u, 0, s2h[k] - s2t[k]);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < T; k++) buf_st(ob2, xo[k], 0, s2h[k] - s2t[k]);
-        }
-        ws = ws + T == R ? 0 : ws + T;
     }
-
-    template <int RT>
-    __device__ __forceinline__ void process(const Tile& t, int j0) {
-        // (stage-1 outputs past the line end only feed S2 positions no stored window reaches)
-        tile<RT>(t, j0, !(j0 - 2 * LAG >= 0 && j0 + T - 1 - 2 * LAG < len));
-    }
-#else
-    template <bool GUARD, int RT>   // RT: the tile's slot in the NH-tile loop
-    __device__ __forceinline__ void tile(const Tile& t, int j0) {
-        const int C = ws - LAG < 0 ? ws - LAG + R : ws - LAG;   // ring slot of output row i0 = j0 - LAG
-        const uint32_t cc = ((uint32_t)(C - 1) & 0xffffu) | ((uint32_t)C << 16);
-        const bool mirror = ws == 0;
-        float* w1 = r1 + ws * 64 + lane;
-        float* w2 = r2 + ws * 64 + lane;
-        uint16_t* wa = ra + ws * 64 + lane;
-        // phase A: rows j0 .. j0+T-1 into the S1 / area rings; pass intersections at i = j - LAG
-        uint32_t pi[T], pi2[T];
-        float s1v[T];
-        uint16_t acv[T];
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            S1 = S1 + t.x[k];
-            s1v[k] = S1;
-            w1[k * 64] = S1;
-            pi[k] = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[0], k), t.a1[0][k]);
-            const uint32_t pp = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[1], k), t.a1[1][k]);
-            Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
-            acv[k] = (uint16_t)Acc;
-            wa[k * 64] = acv[k];
-        }
-        if (mirror) {
-#pragma unroll
-            for (int k = 0; k < T - 1; k++) {
-                r1[(R + k) * 64 + lane] = s1v[k];
-                ra[(R + k) * 64 + lane] = acv[k];
-            }
-        }
-        // the scan stage's pass intersection at j is the norm stage's at j - LAG
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            const int q = k - LAG;
-            const int dt = -((-q + T - 1) / T);
-            pi2[k] = ph[(RT + dt + 4 * NH) % NH][q - dt * T];
-        }
-#pragma unroll
-        for (int k = 0; k < T; k++) ph[RT][k] = pi[k];
-        // phase B: normalised outputs at i = j - LAG; their prefix S2 (iteration k+1's scan input)
-        const __amdgpu_buffer_rsrc_t ob2 = buf_rsrc(xst);
+    // stage C stores: the tile's rows jst .. jst+T-1 through a resource whose range ends at the
+    // line end (rows past it are dropped by the range check) and is empty for tiles before the
+    // line (the tile grid starts SHIFT rows early so that no tile straddles row 0 of the scan
+    // outputs): every tile issues the same T stores and no branch
+    __device__ __forceinline__ void stage_c_store(const float (&s2h)[T], const float (&s2t)[T]) {
+        // (jst < 0 or jst >= len: nothing of the tile is in the line -- the tiles that run past
+        // the line end must not store into the rows after it, the next pair's or past the
+        // allocation; a tile with 0 < len - jst < T keeps only its rows before the end)
+        const int left = len - jst;
+        const int range = (unsigned)jst >= (unsigned)len ? 0 : (left >= T ? 0x7fffffff : left * (int)vsb);
+        const __amdgpu_buffer_rsrc_t ob2 = buf_rsrc(xst, range);
         xst += (long)T * (long)vsb;
-        // (reads batched in program order, then the arithmetic: inline asm addresses keep the
-        // scheduler from hoisting later positions' reads over earlier positions' arithmetic)
-        float qv[T], dv[T], shv[T], stv[T];
-        uint32_t ahv[T], atv[T];
+        jst += T;
 #pragma unroll
-        for (int k = 0; k < T; k++) {
-            const uint32_t sp = slots(pi[k], cc);
-            shv[k] = rd<1, float>(sp, o1, k);
-            stv[k] = rd<0, float>(sp, o1, k);
-            ahv[k] = rd<1, uint16_t>(sp, oa, k);
-            atv[k] = rd<0, uint16_t>(sp, oa, k);
-        }
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            dv[k] = shv[k] - stv[k];
-            qv[k] = div_area(dv[k], (ahv[k] - atv[k]) & 0xffffu);
-        }
-        if constexpr (CHECK) {
-            // dividends are >= +0, so "0 < dv < 2^-110" is "bits(dv) - 1 < 0x087fffff" (unsigned)
-            uint32_t tmin = 0xffffffffu;
-#pragma unroll
-            for (int k = 0; k < T; k++) tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
-            if (__ballot(tmin < 0x087fffffu)) {
-#pragma unroll
-                for (int k = 0; k < T; k++) {
-                    const uint32_t sp = slots(pi[k], cc);
-                    const uint32_t av = (rd<1, uint16_t>(sp, oa, k) - rd<0, uint16_t>(sp, oa, k)) & 0xffffu;
-                    qv[k] = dv[k] / (float)av;
-                }
-            }
-        }
-        float s2v[T];
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            float y = qv[k];
-            if (GUARD) y = (j0 - LAG + k >= 0) ? y : 0.f;   // nothing accumulates before the line
-            S2 = S2 + y;
-            s2v[k] = S2;
-            w2[k * 64] = S2;
-        }
-        if (mirror) {
-#pragma unroll
-            for (int k = 0; k < T - 1; k++) r2[(R + k) * 64 + lane] = s2v[k];
-        }
-        // phase C: scan outputs at i2 = j - 2 LAG
-        float s2h[T], s2t[T];
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            const uint32_t sp = slots(pi2[k], cc);
-            s2h[k] = rd<1, float>(sp, o2, k);
-            s2t[k] = rd<0, float>(sp, o2, k);
-        }
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            // (outside the line: an out-of-range offset, so that both tile forms issue the same
-            // vector-memory sequence and the loop's vmcnt waits stay exact)
-            const bool in = !GUARD || (unsigned)(j0 - 2 * LAG + k) < (unsigned)len;
-            buf_st(ob2, in ? xo[k] : 0x80000000u, 0, s2h[k] - s2t[k]);
-        }
-        ws = ws + T == R ? 0 : ws + T;
+        for (int k = 0; k < T; k++) buf_st(ob2, xo[k], 0, s2h[k] - s2t[k]);
     }
 
+    __device__ __forceinline__ static void launder(Tile& t) {
+        static_assert(T == 7, "launder lists the 23 registers of a T = 7 tile");
+        asm volatile("" : "+v"(t.x[0]), "+v"(t.x[1]), "+v"(t.x[2]), "+v"(t.x[3]), "+v"(t.x[4]), "+v"(t.x[5]),
+                          "+v"(t.x[6]), "+v"(t.a0[0]), "+v"(t.a0[1]), "+v"(t.a1[0][0]), "+v"(t.a1[0][1]),
+                          "+v"(t.a1[0][2]), "+v"(t.a1[0][3]), "+v"(t.a1[0][4]), "+v"(t.a1[0][5]), "+v"(t.a1[0][6]),
+                          "+v"(t.a1[1][0]), "+v"(t.a1[1][1]), "+v"(t.a1[1][2]), "+v"(t.a1[1][3]), "+v"(t.a1[1][4]),
+                          "+v"(t.a1[1][5]), "+v"(t.a1[1][6]));
+    }
+    // T stores that store nothing (out-of-range offsets)
+    __device__ __forceinline__ void dummy_stores() const {
+        const __amdgpu_buffer_rsrc_t r = buf_rsrc(xst, 0);
+#pragma unroll
+        for (int k = 0; k < T; k++) buf_st(r, 0x80000000u + 4u * k, 0, 0.f);   // (distinct: not merged)
+    }
+
+    // body of tile n (loop slot RT = n mod NH): on entry A(n) has run and B1(n)'s reads are in
+    // flight (nm); `next` holds tile n + 1's loads, `fill` receives tile n + 3's
     template <int RT>
-    __device__ __forceinline__ void process(const Tile& t, int j0) {
-        // (stage-1 outputs past the line end only feed S2 positions no stored window reaches)
-        if (j0 - 2 * LAG >= 0 && j0 + T - 1 - 2 * LAG < len)
-            tile<false, RT>(t, j0);
-        else
-            tile<true, RT>(t, j0);
-    }
+    __device__ __forceinline__ void body(Tile& fill, Tile& next, Norm& nm, int& C) {
+        load(fill);
+#if SM_CB_NSV_VMWAIT
+        // one wait for all of tile n + 1's loads (instead of one per register): an empty asm
+        // that reads and redefines all of them, so the compiler's wait sits in front of it
+        launder(next);
 #endif
-
+        uint32_t pi[T];
+        stage_a(next, pi);                                        // A(n + 1)
+        stage_b2(nm, C);                                          // B2(n)
+        float s2h[T], s2t[T];
+        stage_c_read<RT>(s2h, s2t);                               // C(n) reads
+        C = C + T >= R ? C + T - R : C + T;
+        stage_b1<(RT + 1) % NH>(pi, C, nm);                       // B1(n + 1)
+        stage_c_store(s2h, s2t);                                  // C(n) stores
+    }
 };
 
 template <bool RV, bool CHECK>
@@ -818,9 +784,12 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
     const size_t npix = (size_t)a.H * a.W;
     L.vsb = (uint32_t)(a.W * a.D * 4);
     const char* xbase = (const char*)(a.vm + ((size_t)b * npix + u) * a.D + (size_t)chunk * 64);
-    L.xld = xbase;
-    L.jld = 0;
-    L.xst = xbase - (long)(2 * L_t::LAG) * (long)L.vsb;
+    constexpr int J0 = -L_t::SHIFT;                 // first tile row
+    L.xld = xbase + (long)J0 * (long)L.vsb;
+    L.jld = J0;
+    L.jst = J0 - 2 * L_t::LAG;
+    L.jnm = J0 - L_t::LAG;
+    L.xst = xbase + (long)(J0 - 2 * L_t::LAG) * (long)L.vsb;
     {
         const long room = (const char*)a.vm_end - xbase;   // bytes from row 0 to the allocation end
         const long rows = room / (long)L.vsb;
@@ -830,7 +799,11 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
     for (int k = 0; k < T; k++) L.xo[k] = (uint32_t)L.lane * 4u + (uint32_t)k * L.vsb;
     L.len = a.H;
     L.rowb = (uint32_t)a.W * 4u;
-    L.rld = (uint32_t)a.arm_pad_rows * L.rowb;
+    L.rld = (uint32_t)(a.arm_pad_rows + J0) * L.rowb;   // (the pad holds 2 LAG rows: J0 - LAG >= -2 LAG)
+    // the arm allocation's tail pad holds 2 LAG + 64 rows after the last plane; a tile starting
+    // past row len + LAG has all its arm rows (set 0: rows - LAG, set 1: rows) at or past the line
+    // end, where no stored output reads them: such tiles re-read the rows of the tile at len + LAG
+    L.rld_max = (uint32_t)(a.arm_pad_rows + L.len + L_t::LAG) * L.rowb;
     const int dl = chunk * 64 + L.lane;
     const int own = RV ? 2 : 0, other = RV ? 0 : 2;
     const long pad = (long)a.arm_pad_rows * L.rowb;
@@ -855,7 +828,6 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
     {
         typedef __attribute__((address_space(3))) char lds_c;
         L.o1 = (uint32_t)(size_t)(lds_c*)L.r1 + 4u * (uint32_t)L.lane;
-        L.o2 = (uint32_t)(size_t)(lds_c*)L.r2 + 4u * (uint32_t)L.lane;
         L.oa = (uint32_t)(size_t)(lds_c*)L.ra + 2u * (uint32_t)L.lane;
     }
     L.RR = (uint32_t)L_t::R | ((uint32_t)(65536 - L_t::R) << 16);
@@ -863,41 +835,49 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
 #pragma unroll
     for (int r = 0; r < L_t::NH; r++)
 #pragma unroll
-        for (int k = 0; k < T; k++) {
-#if SM_CB_NSV_AH
-            L.hh[r][k] = L.ht[r][k] = L.o1;   // rows before the line: any in-ring address (outputs < 0 are not stored)
-#else
-            L.ph[r][k] = 0u;
-#endif
-        }
+        for (int k = 0; k < T; k++) L.hh[r][k] = L.ht[r][k] = L.o1;   // rows before the line: any in-ring address (outputs < 0 are not stored)
     __syncthreads();
     L.S1 = L.S2 = 0.f;
     L.Acc = 0;
-    L.ws = 0;
-    const int nst = L.len + 2 * L_t::LAG;
+    L.wsa = 0;
+    int C = L_t::out_slot(0);
+    const int nst = L.len + 2 * L_t::LAG;   // (tiles start at J0; the last stored row is len - 1)
     typename L_t::Tile ta, tb, tc;
+    typename L_t::Norm nm;
     static_assert(L_t::NH == 6, "the loop below is written for six tiles");
-    // (the scheduler must not interleave the two prologue tiles' loads, and the loop has no exit
-    // but its condition: otherwise the compiler's vmcnt waits at the loop head are conservative
-    // and every sixth tile waits for the next tile's loads too.  Up to five tiles past the line
-    // end run: their loads read the zeroed tail pads, their stores are out of range.)
-    L.load(ta);
+    // Prologue: tiles 0 .. 2 loaded in order, A(0), B1(0).  (The scheduler must not interleave
+    // the prologue tiles' loads, and the loop has no exit but its condition: otherwise the
+    // compiler's vmcnt waits at the loop head are conservative.  Up to eight tiles past the line
+    // end are loaded and up to five run: their loads read the zeroed tail pads or nothing, their
+    // stores are out of range.)
+    L.template load<true>(ta);
     __builtin_amdgcn_sched_barrier(0);
     L.load(tb);
     __builtin_amdgcn_sched_barrier(0);
-    for (int j0 = 0; j0 < nst; j0 += 6 * T) {
-        L.load(tc);
-        L.template process<0>(ta, j0);
-        L.load(ta);
-        L.template process<1>(tb, j0 + T);
-        L.load(tb);
-        L.template process<2>(tc, j0 + 2 * T);
-        L.load(tc);
-        L.template process<3>(ta, j0 + 3 * T);
-        L.load(ta);
-        L.template process<4>(tb, j0 + 4 * T);
-        L.load(tb);
-        L.template process<5>(tc, j0 + 5 * T);
+#if SM_CB_NSV_VMWAIT
+    L.dummy_stores();   // the stores of "C(-2)": body 0 then sees the steady-state sequence
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    L.load(tc);
+    __builtin_amdgcn_sched_barrier(0);
+#if SM_CB_NSV_VMWAIT
+    L.dummy_stores();   // "C(-1)"
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    {
+        uint32_t pi[T];
+        L.stage_a(ta, pi);
+        L.template stage_b1<0>(pi, C, nm);
+    }
+    // body n: load tile n + 3 into the buffer of tile n (A(n) ran in body n - 1), A(n + 1) from
+    // the buffer of tile n + 1
+    for (int j0 = J0; j0 < nst; j0 += 6 * T) {
+        L.template body<0>(ta, tb, nm, C);
+        L.template body<1>(tb, tc, nm, C);
+        L.template body<2>(tc, ta, nm, C);
+        L.template body<3>(ta, tb, nm, C);
+        L.template body<4>(tb, tc, nm, C);
+        L.template body<5>(tc, ta, nm, C);
     }
 }
 
@@ -908,7 +888,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     extern __shared__ float smem[];
     cbca_run_nsv<RV, CHECK>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
 }
-
 template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int LAGC>
 __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
     CbLine<HORIZ, MODE, FULL, SCALE, RV, LAGC> L;
@@ -1083,7 +1062,7 @@ static void launch_lag(const CbcaArgs& a, int n, hipStream_t st) {
 
 // NsV's prerequisites: the reference's lag, whole 64-disparity chunks, arm-plane offsets in 31 bits
 static bool nsv_ok(const CbcaArgs& a) {
-    return SM_CB_NSV && a.lag == NSV_LAG && a.D % 64 == 0 && a.arm_pad_rows == 2 * NSV_LAG &&
+    return a.lag == NSV_LAG && a.D % 64 == 0 && a.arm_pad_rows == 2 * NSV_LAG &&
            (double)(a.H + 4 * NSV_LAG + 64) * a.W * 4.0 < 2147483647.0;
 }
 

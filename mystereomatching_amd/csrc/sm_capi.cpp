@@ -113,6 +113,11 @@ struct sm_ctx {
     int sub_batch = 0;          // sm_params.sub_batch: run sm_run in groups of k pairs (0 = all)
     int nstreams = 1;           // sm_params.num_streams: groups alternate over s streams (see sm_run)
     bool auto_groups = false;   // num_streams = 0 chose two streams: sm_run splits n pairs into two groups
+    bool pipelined = false;     // auto_groups with CBCA + SGM: the two groups run as a pipeline across calls
+    bool pipe_live = false;     // the side stream still runs the second group of the last sm_run (not joined)
+    int pipe_g = 0;             // pairs in the first group of the last pipelined sm_run
+    hipEvent_t ev_copy2 = nullptr;   // async copy of a pipelined run's second group done (cst)
+    bool copy_split = false;    // the pending async copy is two copies (ev_copy: group 0, ev_copy2: group 1)
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
     hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
     hipEvent_t ev_run = nullptr, ev_copy = nullptr;     // run done (c->st) / async copy done (cst)
@@ -328,6 +333,9 @@ sm_status apply_schedule(sm_ctx* c, int num_streams, int sub_batch) {
                      (c->nvol * 4 >= ((size_t)1 << 28) ||
                       (c->cap >= 8 && p.optimization == SM_OPT_SGM && p.sgm_paths == 4 && !p.do_refine));
     c->nstreams = c->auto_groups ? 2 : (num_streams < 1 ? 1 : num_streams);
+    // the pipelined form of the two groups (sm_run): CBCA + SGM without refinement, where the
+    // groups touch only their own pairs' buffers
+    c->pipelined = c->auto_groups && p.optimization == SM_OPT_SGM && !p.do_refine;
     for (int i = 0; i + 1 < c->nstreams; i++)
         if (!c->xst[i]) HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking));
     return SM_OK;
@@ -382,7 +390,8 @@ void free_all(sm_ctx* c) {
     }
     if (c->ev_run) hipEventDestroy(c->ev_run);
     if (c->ev_copy) hipEventDestroy(c->ev_copy);
-    c->ev_run = c->ev_copy = nullptr;
+    if (c->ev_copy2) hipEventDestroy(c->ev_copy2);
+    c->ev_run = c->ev_copy = c->ev_copy2 = nullptr;
     for (auto& x : c->xst)
         if (x) {
             hipStreamDestroy(x);
@@ -891,14 +900,36 @@ sm_status upload(sm_ctx* c, int n, const uint8_t* lbgr, const uint8_t* rbgr, siz
 // the maps are about to be written: an asynchronous copy of the previous maps must be done
 sm_status wait_copy(sm_ctx* c) {
     if (c->copy_pending) HIP_TRY(c, hipStreamWaitEvent(c->st, c->ev_copy, 0));
+    if (c->copy_pending && c->copy_split) HIP_TRY(c, hipStreamWaitEvent(c->st, c->ev_copy2, 0));
     return SM_OK;
 }
 
-sm_status check(sm_ctx* c) {
+sm_status check_nojoin(sm_ctx* c) {
     if (!c) return SM_EINVAL;
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) return hip_fail(c, e, "hipSetDevice");
     return SM_OK;
+}
+
+// A pipelined sm_run leaves its second group running on the side stream; every other entry point
+// first orders the main stream after it (one event), so that it sees (and may overwrite) the state
+// of the whole call.
+sm_status join_all(sm_ctx* c) {
+    if (!c->pipe_live) return SM_OK;
+    c->pipe_live = false;
+    hipError_t e = hipEventRecord(c->xev[9], c->xst[0]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->st, c->xev[9], 0);
+    if (e != hipSuccess) {
+        hipStreamSynchronize(c->xst[0]);   // a failed join: drain on the host
+        return hip_fail(c, e, "stream join");
+    }
+    return SM_OK;
+}
+
+sm_status check(sm_ctx* c) {
+    sm_status s = check_nojoin(c);
+    if (s) return s;
+    return join_all(c);
 }
 
 }  // namespace
@@ -1114,6 +1145,7 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
 sm_status sm_destroy(sm_ctx* c) {
     if (!c) return SM_OK;
     hipSetDevice(c->device);
+    if (c->pipe_live) join_all(c);
     if (c->st) hipStreamSynchronize(c->st);
     free_all(c);
     delete c;
@@ -1383,7 +1415,7 @@ sm_status sm_upload_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8
 #define SM_STAGGER_STAGE 1   // 0: CBCA groups also start after the previous group's whole CBCA (A/B)
 #endif
 sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
-    sm_status s = check(c);
+    sm_status s = check_nojoin(c);   // (a pipelined run continues from the previous one's streams)
     if (s) return s;
     if (c->stage < 1) return fail(c, SM_ESTATE, "sm_run before images were uploaded");
     if (n < 1 || n > c->n_loaded) return fail(c, SM_EINVAL, "n must be in [1, pairs uploaded]");
@@ -1400,11 +1432,26 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     // prep, cost and first sweep then share the CUs with this group's LDS-bound NORM_SCAN
     // sweep: profiles/r4j, 1.5-5 % faster than starting after the whole CBCA), else after group
     // k's aggregation
-    const bool early = SM_STAGGER_STAGE == 1 && c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0;
+    //
+    // Pipelined (num_streams 0 with CBCA + SGM, two groups): group 0 on the main stream, group 1 on
+    // the side stream, and the call returns WITHOUT joining them: the next call's group 0 follows
+    // this call's group 0 on the main stream and its group 1 this call's group 1 on the side
+    // stream, so group 1 keeps running about half a call behind group 0 -- its LDS- and
+    // issue-bound CBCA sweeps (NsV: three waves per CU, one SIMD idle, 3 TB/s) beside group 0's SGM
+    // passes, which use no LDS and stream HBM.  Two single-pair pipelines offset by half a call:
+    // 36.1 -> 35.2 ms per two full-resolution pairs in the bench (profiles/r5l); the placement of an
+    // instance's allocations moves both by up to 2 ms (tools/overlap_probe2.py).  Only
+    // a pipeline start staggers group 1 (after group 0's CBCA); every other entry point joins
+    // first (check -> join_all), and the asynchronous map copy waits for both groups.
+    const bool piped = c->pipelined && ns == 2 && n >= 2 && (n + g - 1) / g == 2;
+    const bool early = !piped && SM_STAGGER_STAGE == 1 && c->p.aggregation == SM_AGG_CBCA && c->p.cbca_iterations > 0;
+    // (a different split of the pairs would let the groups of two calls share a pair: join first)
+    if ((!piped || g != c->pipe_g) && (s = join_all(c))) return s;
+    const bool start = !(piped && c->pipe_live);   // groups start from a joined state
     hipStream_t main_st = c->st;
     int k = 0;
     sm_status s_out = SM_OK;
-    if (ns > 1) {   // the side streams start after everything queued so far on the main stream
+    if (ns > 1 && start) {   // the side streams start after everything queued so far on the main stream
         HIP_TRY(c, hipEventRecord(c->xev[0], main_st));
         for (int i = 0; i + 1 < ns; i++) HIP_TRY(c, hipStreamWaitEvent(c->xst[i], c->xev[0], 0));
     }
@@ -1413,7 +1460,7 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
         const Bufs B = at(c, off);
         c->st = (ns > 1 && k % ns) ? c->xst[k % ns - 1] : main_st;
         hipError_t e = hipSuccess;
-        if (ns > 1 && k > 0 && (e = hipStreamWaitEvent(c->st, c->xev[1 + (k - 1) % 8], 0)) != hipSuccess) {
+        if (ns > 1 && k > 0 && start && (e = hipStreamWaitEvent(c->st, c->xev[1 + (k - 1) % 8], 0)) != hipSuccess) {
             s_out = hip_fail(c, e, "hipStreamWaitEvent (group stagger)");
             break;
         }
@@ -1437,7 +1484,7 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
         if (s_out) break;
         // the maps are written from here on: an asynchronous copy of the previous run's maps
         // (sm_download_disp_async) must be done reading them
-        if (c->copy_pending && (e = hipStreamWaitEvent(c->st, c->ev_copy, 0)) != hipSuccess) {
+        if (c->copy_pending && (e = hipStreamWaitEvent(c->st, (c->copy_split && k == 1) ? c->ev_copy2 : c->ev_copy, 0)) != hipSuccess) {
             s_out = hip_fail(c, e, "hipStreamWaitEvent (async map copy)");
             break;
         }
@@ -1456,7 +1503,10 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     }
     c->st = main_st;
     c->stagger_ev = nullptr;
-    if (ns > 1) {   // the join runs on the error path too: nothing stays queued behind the main stream
+    if (piped && !s_out) {
+        c->pipe_live = true;   // group 1 stays on the side stream (joined by the next other call)
+        c->pipe_g = g;
+    } else if (ns > 1) {   // the join runs on the error path too: nothing stays queued behind the main stream
         for (int i = 0; i + 1 < ns; i++) {
             hipError_t e = hipEventRecord(c->xev[9 + i], c->xst[i]);
             if (e == hipSuccess) e = hipStreamWaitEvent(main_st, c->xev[9 + i], 0);
@@ -1484,7 +1534,7 @@ sm_status sm_download_disp(sm_ctx* c, int32_t n, int16_t* disp_out) {
 }
 
 sm_status sm_download_disp_async(sm_ctx* c, int32_t n, int16_t* disp_out) {
-    sm_status s = check(c);
+    sm_status s = check_nojoin(c);   // (keeps a pipelined run's groups apart)
     if (s) return s;
     if (!disp_out || n < 1 || n > c->cap) return fail(c, SM_EINVAL, "bad arguments");
     if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
@@ -1493,10 +1543,30 @@ sm_status sm_download_disp_async(sm_ctx* c, int32_t n, int16_t* disp_out) {
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_run, hipEventDisableTiming));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
     }
+    if (!c->ev_copy2) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_copy2, hipEventDisableTiming));
     HIP_TRY(c, hipEventRecord(c->ev_run, c->st));
     HIP_TRY(c, hipStreamWaitEvent(c->cst, c->ev_run, 0));
-    HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDefault, c->cst));
-    HIP_TRY(c, hipEventRecord(c->ev_copy, c->cst));
+    c->copy_split = c->pipe_live && n > c->pipe_g;
+    if (c->copy_split) {
+        // a pipelined run: the first group's maps once the main stream is there, the second's once
+        // the side stream is (waited for, not joined), so that the next run's group k waits for
+        // its own maps' copy only
+        const size_t g = (size_t)c->pipe_g;
+        HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, g * c->npix * 2, hipMemcpyDefault, c->cst));
+        HIP_TRY(c, hipEventRecord(c->ev_copy, c->cst));
+        HIP_TRY(c, hipEventRecord(c->xev[10], c->xst[0]));
+        HIP_TRY(c, hipStreamWaitEvent(c->cst, c->xev[10], 0));
+        HIP_TRY(c, hipMemcpyAsync(disp_out + g * c->npix, c->disp + g * c->npix, ((size_t)n - g) * c->npix * 2,
+                                  hipMemcpyDefault, c->cst));
+        HIP_TRY(c, hipEventRecord(c->ev_copy2, c->cst));
+    } else {
+        if (c->pipe_live) {   // (n within the first group: its maps only)
+            HIP_TRY(c, hipEventRecord(c->xev[10], c->xst[0]));
+            HIP_TRY(c, hipStreamWaitEvent(c->cst, c->xev[10], 0));
+        }
+        HIP_TRY(c, hipMemcpyAsync(disp_out, c->disp, (size_t)n * c->npix * 2, hipMemcpyDefault, c->cst));
+        HIP_TRY(c, hipEventRecord(c->ev_copy, c->cst));
+    }
     c->copy_pending = true;
     return SM_OK;
 }

@@ -120,6 +120,46 @@ def test_auto_two_groups(oracle):
         sb.close()
 
 
+def test_pipelined_runs(oracle):
+    """num_streams 0 with CBCA + SGM: sm_run returns with its second group still running on the
+    side stream (no join), the next run's groups follow their own stream, download_async copies
+    each group's maps after that group.  Back-to-back runs with async copies, a run over fewer
+    pairs (a different split: joined first), new images uploaded mid-pipeline, DP[0] read mid-
+    pipeline: every map must equal the oracle's."""
+    import torch
+    H, W, md, n = 29, 61, 31, 9
+    a = S.make_batch(n, H, W, md + 1, first_index=600)
+    b = S.make_batch(n, H, W, md + 1, first_index=620)
+    wa, wb = _oracle_maps(oracle, a, H, W, md), _oracle_maps(oracle, b, H, W, md)
+    sb = StereoBatch(md, H, W, n, device=0)
+    try:
+        sb.upload(*(a[k] for k in KEYS))
+        outs = [torch.empty((n, H, W), dtype=torch.int16, pin_memory=True).numpy() for _ in range(4)]
+        for i in range(4):
+            sb.run(0.3, download=False)
+            sb.download_async(outs[i])
+        sb.synchronize()
+        for o in outs:
+            np.testing.assert_array_equal(o, wa)
+        sb.run(0.3, download=False)   # pipeline live
+        np.testing.assert_array_equal(sb.get_disp(0), wa[0])
+        sb.n = 7                      # fewer pairs: another split of the groups
+        part = sb.run(0.3)
+        np.testing.assert_array_equal(part, wa[:7])
+        sb.n = n
+        sb.run(0.3, download=False)   # live again, then new images
+        sb.upload(*(b[k] for k in KEYS))
+        for i in range(3):
+            sb.run(0.3, download=False)
+            sb.download_async(outs[i])
+        sb.synchronize()
+        for o in outs[:3]:
+            np.testing.assert_array_equal(o, wb)
+        np.testing.assert_array_equal(sb.run(0.3), wb)
+    finally:
+        sb.close()
+
+
 @pytest.mark.parametrize("n,caps", [(5, (3, 3)), (4, (2, 2, 2)), (1, (1, 1))])
 def test_run_batch_multi_contexts(oracle, n, caps):
     """sm_run_batch_multi over several contexts on device 0 (one host thread each): contiguous

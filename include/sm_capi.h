@@ -120,11 +120,15 @@ typedef struct sm_params {
     int32_t sub_batch;           /* run the n pairs in groups of k (0 = one group), stages back to back */
     int32_t num_streams;         /* 0 (default): auto -- with CBCA and a volume >= 256 MiB per pair (or
                                   * batch_capacity >= 8 with 4-path SGM and no refinement), two
-                                  * streams and (sub_batch 0) two groups of n / 2 pairs, each group
-                                  * starting after the previous one's first CBCA sweep; else one
-                                  * stream; 1: one stream; 2-4: groups alternate over that many
-                                  * streams (group k + 1 starts after group k's first CBCA sweep, or
-                                  * its aggregation without CBCA) */
+                                  * streams and (sub_batch 0) two groups of n / 2 pairs; with SGM
+                                  * and no refinement the groups are pipelined ACROSS calls: sm_run
+                                  * returns with the second group still queued on the side stream
+                                  * (about half a call behind the first), the next sm_run's groups
+                                  * follow on their own streams, sm_download_disp_async copies each
+                                  * group's maps after that group, and every other call first waits
+                                  * for both; else one stream; 1: one stream; 2-4: groups alternate
+                                  * over that many streams (group k + 1 starts after group k's first
+                                  * CBCA sweep, or its aggregation without CBCA), joined per call */
     int32_t fuse_norm_scan;      /* CBCA: iteration k's normalising sweep fused with iteration k+1's
                                   * scan (one sweep, 8 B per element less): 1 = always, 0 = never,
                                   * -1 (default) = when the dedicated sweep for the reference's lag

@@ -170,6 +170,12 @@ struct CbLine {
     // drops the third set's own-arm load, readlane, pkmin and 64-word gather per position
     // (full resolution 11.15 -> 9.91 ms, profiles/r3l, r3m).
     static constexpr bool REUSE2 = LAGC > 0 && !HORIZ && MODE == CB_NORM_SCAN;
+    // RING8 (H NORM at the reference's lag, a compile-time LAGC): the ring holds 8 tiles
+    // (2 lag + T + 1 = 79 -> 80 slots at T = 10), so an 8-tile loop knows every tile's ring slots at
+    // compile time: the window slots of position k are (constant - tail - 1, constant + head),
+    // with no per-position scalar wrap (4 SALU per position) and no ws bookkeeping
+    static constexpr bool RING8 = LAGC > 0 && HORIZ && MODE == CB_NORM &&
+                                  (2 * LAGC + T + 1 + T - 1) / T * T == 8 * T;
     static_assert(!REUSE2 || (CbCfg<HORIZ, MODE>::PF == 3 && LAGC + T - 1 <= 4 * T),
                   "the history is the last four tiles of the four-tile loop");
 
@@ -308,6 +314,14 @@ struct CbLine {
         const us2 w = q + us2{(unsigned short)ring, (unsigned short)(-ring)};
         return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, w));
     }
+    // slot_pair for a compile-time slot c < ring of an 8-tile ring (RING8): one packed add of the
+    // constant (c, c), the wrap of both ends as in slot_pair
+    __device__ __forceinline__ uint32_t slot_pair_c(uint32_t p, int c) const {
+        constexpr int RINGC = 8 * T;
+        const us2 q = __builtin_bit_cast(us2, p ^ 0xffffu) + us2{(unsigned short)c, (unsigned short)c};
+        const us2 w = q + us2{(unsigned short)RINGC, (unsigned short)(-RINGC)};
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, w));
+    }
     // LDS element of a ring of 4-byte / 2-byte entries at slot = half H_ of sp, for this lane;
     // RG: 0 = r1, 1 = r2 (floats), 2 = ra (u16).  One v_mad_u32_u16 of the half with the ring's
     // bytes per slot and the lane's slot-0 address.
@@ -330,13 +344,16 @@ struct CbLine {
     // start read the zeroed ring, which is exactly the reference's border case
     // out = S[i + head] (cal1DCost, h:1643-1715).  Only the two ends of a line (GUARD) test
     // whether an output position exists before storing it.
-    template <bool GUARD, int R>
+    template <bool GUARD, int R, int RC = -1>
     __device__ __forceinline__ void tile(const Tile& t, int j0) {
         uint32_t pi[T], pi2[T];
         // ring % T == 0 and ws % T == 0, so the tile's write slots ws .. ws+T-1 never wrap
-        float* w1 = r1 + ws * 64 + lane;
-        uint16_t* wa = ra + ws * 64 + lane;
-        const int si0 = uwrap(ws - lag);        // slot of i = j0 - lag
+        // (RC >= 0: the tile's slot in the 8-tile ring cycle, all slots compile-time constants)
+        constexpr int RINGC = 8 * T;
+        const int wsv = RC >= 0 ? RC * T : ws;
+        float* w1 = r1 + wsv * 64 + lane;
+        uint16_t* wa = ra + wsv * 64 + lane;
+        const int si0 = RC >= 0 ? (RC * T - LAGC + 2 * RINGC) % RINGC : uwrap(ws - lag);   // slot of i = j0 - lag
         // (NORM_SCAN: r2 holds position p's S2 at slot (p + lag) mod ring, so the tile's S2 writes
         // are slots ws .. ws + T - 1 and the slot of i2 = j0 - 2 lag in r2 is si0)
         const int i0 = j0 - lag;
@@ -373,7 +390,8 @@ struct CbLine {
         uint32_t ahv[T], atv[T];
 #pragma unroll
         for (int k = 0; k < T; k++) {
-            const uint32_t sp = slot_pair(pi[k], si0 + k);   // slots of i - tail - 1, i + head
+            const uint32_t sp = RC >= 0 ? slot_pair_c(pi[k], (si0 + k) % RINGC)
+                                        : slot_pair(pi[k], si0 + k);   // slots of i - tail - 1, i + head
             shv[k] = ring_at<1, 0>(sp);
             stv[k] = ring_at<0, 0>(sp);
             if (MODE != CB_SCAN) {
@@ -433,18 +451,18 @@ struct CbLine {
             for (int k = 0; k < T; k++)
                 store_tile(ob2, k, s2h[k] - s2t[k], !GUARD || (unsigned)(i20 + k) < (unsigned)len);
         }
-        ws = (ws + T == ring) ? 0 : ws + T;
+        if (RC < 0) ws = (ws + T == ring) ? 0 : ws + T;
         wrs = (wrs + T >= cbca_win_ring(T)) ? wrs + T - cbca_win_ring(T) : wrs + T;
     }
 
-    template <int R = 0>   // R: the tile's slot in the four-tile loop (REUSE2 history)
+    template <int R = 0, int RC = -1>   // R: the tile's slot in the four-tile loop (REUSE2 history)
     __device__ __forceinline__ void process(const Tile& t, int j0) {
         constexpr int stages = MODE == CB_NORM_SCAN ? 2 : 1;
         const int last_out = j0 + T - 1 - lag * stages;        // last output position of the tile
         if (j0 - lag >= 0 && last_out < len && (MODE != CB_NORM_SCAN || j0 - 2 * lag >= 0))
-            tile<false, R>(t, j0);
+            tile<false, R, RC>(t, j0);
         else
-            tile<true, R>(t, j0);
+            tile<true, R, RC>(t, j0);
     }
 };
 
@@ -491,6 +509,9 @@ struct CbLine {
 __host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (0xf << 8) | (0x7 << 4) | (n & 0xf); }
 static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
+#ifndef SM_CB_RING8
+#define SM_CB_RING8 1   // H NORM at lag 34 through CbLine::RING8 (0: the runtime-ring sweep, A/B builds)
+#endif
 constexpr int cbca_nsv_ring() { return (2 * NSV_LAG + SM_CB_T_NSV + 1 + SM_CB_T_NSV - 1) / SM_CB_T_NSV * SM_CB_T_NSV; }
 constexpr int cbca_nsv_phys() { return cbca_nsv_ring() + SM_CB_T_NSV - 1; }
 // dynamic LDS in 4-byte words: r1, r2 (P x 64 floats each), ra (P x 64 u16)
@@ -995,7 +1016,33 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     // otherwise the compiler's vmcnt waits at the loop head are conservative and the first tile
     // of every trip waits for later tiles' loads too.  Tiles past the line end run (up to PF of
     // them): their loads are bounded or read the next line, their stores are out of range.
-    if constexpr (CbCfg<HORIZ, MODE>::PF == 3) {
+    if constexpr (decltype(L)::RING8) {
+        // H NORM at lag 34: eight tiles per trip (one ring cycle), three tiles in flight
+        L.load(ta, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        L.load(tb, T);
+        __builtin_amdgcn_sched_barrier(0);
+        L.load(tc, 2 * T);
+        __builtin_amdgcn_sched_barrier(0);
+        for (int j0 = 0; j0 < nst; j0 += 8 * T) {
+            L.load(td, j0 + 3 * T);
+            L.template process<0, 0>(ta, j0);
+            L.load(ta, j0 + 4 * T);
+            L.template process<0, 1>(tb, j0 + T);
+            L.load(tb, j0 + 5 * T);
+            L.template process<0, 2>(tc, j0 + 2 * T);
+            L.load(tc, j0 + 6 * T);
+            L.template process<0, 3>(td, j0 + 3 * T);
+            L.load(td, j0 + 7 * T);
+            L.template process<0, 4>(ta, j0 + 4 * T);
+            L.load(ta, j0 + 8 * T);
+            L.template process<0, 5>(tb, j0 + 5 * T);
+            L.load(tb, j0 + 9 * T);
+            L.template process<0, 6>(tc, j0 + 6 * T);
+            L.load(tc, j0 + 10 * T);
+            L.template process<0, 7>(td, j0 + 7 * T);
+        }
+    } else if constexpr (CbCfg<HORIZ, MODE>::PF == 3) {
         L.load(ta, 0);
         __builtin_amdgcn_sched_barrier(0);
         L.load(tb, T);
@@ -1084,6 +1131,12 @@ static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
         }
         if (a.lag == 34) return launch_lag<HORIZ, MODE, SCALE, 34>(a, n, st);
     }
+#if SM_CB_RING8
+    // H NORM at the reference's lag: the compile-time 8-tile ring cycle (CbLine::RING8)
+    if constexpr (HORIZ && MODE == CB_NORM) {
+        if (a.lag == 34) return launch_lag<HORIZ, MODE, SCALE, 34>(a, n, st);
+    }
+#endif
     launch_lag<HORIZ, MODE, SCALE, 0>(a, n, st);
 }
 

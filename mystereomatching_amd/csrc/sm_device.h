@@ -33,6 +33,10 @@
 
 namespace sm {
 
+// entry ki % 32 of the 2^(i/32) table (overloaded for the cost kernel's LDS copy)
+template <typename Tab>
+__host__ __device__ inline uint64_t exp_tab_at(const Tab& tab, uint64_t ki) { return tab[ki % 32]; }
+
 // expf core; `tab` is the 32-entry 2^(i/32) table (device: __constant__, host: static).
 // Main path only: valid for -0x1.9fe368p6 <= x <= 0x1.62e42ep6 (callers that cannot be outside
 // that range, or that discard such results, skip the special cases).
@@ -56,7 +60,7 @@ __host__ __device__ inline float expf_glibc_core(float x, const Tab& tab) {
     uint64_t ki = __builtin_bit_cast(uint64_t, kd);
     kd -= SHIFT;
     double r = __builtin_fma(InvLn2N, xd, -kd);
-    const uint64_t t = tab[ki % 32];
+    const uint64_t t = exp_tab_at(tab, ki);
     // t += ki << 47: the shifted term's low word is 0, so only the high word changes (one
     // 32-bit add instead of a 64-bit shift and add); the words are assembled as a 2-vector so
     // that no 64-bit shift / or is emitted for the pair

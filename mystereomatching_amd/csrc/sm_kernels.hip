@@ -886,12 +886,51 @@ __host__ __device__ constexpr int cost_rec_u4() { return CW <= 2 ? 1 : 2; }
 // -17.5: expf_glibc_core is exact down to -103.9, and every value below 2^-25 leaves
 // fl(t - e) == t (see above).  Saves the range test, three selects and a min per element.
 constexpr int LUT_T_N = 260;   // >= 128 census bits + icd (<= 128) + 1
+// The out-of-range sentinel gradient (NOSEL): |f - S| for a real gradient f in [-255, 255] lies in
+// [S - 255, S + 255] = [295, 805]; with the truncation min(., T) the element's G is then >= 0.999
+// min(T, 295) (the host's NOSEL test), and unclamped (FAST below) G <= 677.5.
+constexpr float COST_OOR_GRAD = 550.0f;
+// FAST elements (NOSEL, lamG == 1, adaptive weights, T >= 382.5, focus pixel off the image border): the gradient
+// images are 0.5 (I[+1] - I[-1]) inside the image and full differences on its border rows and
+// columns (calGrad, cpp:271-350), so an interior focus pixel has |gx|, |gy| <= 127.5 and a
+// candidate in the same row |gx| <= 255, |gy| <= 127.5: |dx| <= 382.5 <= T and |dy| <= 255, the
+// truncation is the identity, and wa |dx| == |fl(wa dx)| (wa, wb > 0; round-to-nearest is
+// symmetric), so G = |fl(wa dx)| + |fl(wb dy)| takes one packed subtract, one packed multiply and
+// one add with both operands' abs modifiers.  With wa + wb = 1 (up to 2^-24), G <= 382.5 for real
+// candidates and <= 677.5 for the sentinel (unit weights could reach 1355), so -G >= -700 keeps expf_glibc_core's exponent field from wrapping without the -100
+// clamp (below -103.9 the core returns a double < 2^-149 that rounds to 0 or the least
+// subnormal, which fl(t - e) absorbs like the reference's exact value).  The census count
+// starts from the record's bias word and accumulates through three v_bcnt_u32_b32 (one chain).
+#ifndef SM_COST_FAST
+#define SM_COST_FAST 1
+#endif
+// The cost kernel's LDS copy of the 2^(i/32) table sits in static LDS (a link-time address), so
+// its byte offset (ki % 32) * 8 is one SDWA shift with a byte-0 destination select
+// ((ki << 3) & 0xff) and the table's address goes into the ds_read's offset field.
+struct LdsExpTab {
+    const uint64_t* p;
+};
+__device__ __forceinline__ uint64_t exp_tab_at(const LdsExpTab& t, uint64_t ki) {
+    uint32_t off;
+    asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
+        : "=v"(off) : "v"((uint32_t)ki));
+    return *(const uint64_t*)((const char*)t.p + off);
+}
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
 
 // ND > 0: D == 64 * ND, the element loop fully unrolled (LDS and store offsets become immediates;
 // no loop counter, compare or pointer increments: 35 -> ~29 VALU per element at D = 256)
 template <int METHOD, bool LAM1, int CW, bool ONE, bool OORZ, int ND = 0>
 __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     extern __shared__ __align__(16) unsigned char cs_raw[];
+    // static LDS (link-time addresses: table reads take the offset field): the 2^(i/32) table
+    // and the census / AD exponential LUTs
+    __shared__ uint64_t etab[32];
+    __shared__ float luts[LUT_A_N + LUT_B_N];
     constexpr int RW = cost_rec_u4<CW>();
     constexpr int COST_P = cost_p(ONE);
     constexpr bool NOSEL = METHOD == SM_M_CENSUS_GRAD && OORZ && CW >= 3;
@@ -921,13 +960,12 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     uint4* mrecB4 = mrec + (COST_P + D - 1);                     // plane B (SPLIT), CW = 4
     uint2* mrecB2 = (uint2*)mrecB4;                              // plane B (SPLIT), CW = 3
     auto recA = [&](int i) -> uint4& { return SPLIT ? mrec[i] : mrec[RW * i]; };
-    uint64_t* etab = (uint64_t*)(fcode + COST_P);               // [32] 2^(i/32)
-    float* fgx = (float*)(etab + 32);                            // [P]
+    float* fgx = (float*)(fcode + COST_P);                       // [P]
     float* fgy = fgx + COST_P;
     float* fwa = fgy + COST_P;                                   // adaptive weight a (1 if off)
     float* fwb = fwa + COST_P;                                   // 1 - a (1 if off)
     uint32_t* fbgr = (uint32_t*)(fwb + COST_P);                  // [P]
-    float* luta = (float*)(fbgr + COST_P);                       // [LUT_A_N]
+    float* luta = luts;                                          // [LUT_A_N]
     float* lutb = luta + LUT_A_N;                                // [LUT_B_N]
     const int tid = threadIdx.y * 64 + threadIdx.x;
     const float cd = a.census_default;
@@ -979,13 +1017,17 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 w2 = p[0] | (p[1] << 8) | (p[2] << 16);
             }
         } else if (NOSEL) {   // out-of-range candidate: see NOSEL above
-            w2 = w3 = __float_as_uint(1e30f);
+            w2 = w3 = __float_as_uint(COST_OOR_GRAD);
             bias = (uint32_t)icd;
         }
         if (CW == 4) {
             recA(i) = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, (uint32_t)(c.y >> 32));
             if (SPLIT) mrecB4[i] = make_uint4(w2, w3, bias, 0);
             else mrec[2 * i + 1] = make_uint4(w2, w3, bias, 0);
+        } else if (CW == 3 && NOSEL) {   // {census words, bias} and {gx, gy} (one 8-byte read)
+            recA(i) = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, bias);
+            if (SPLIT) mrecB2[i] = make_uint2(w2, w3);
+            else mrec[2 * i + 1] = make_uint4(w2, w3, 0, 0);
         } else if (CW == 3) {
             recA(i) = make_uint4((uint32_t)c.x, (uint32_t)(c.x >> 32), (uint32_t)c.y, w2);
             if (SPLIT) mrecB2[i] = make_uint2(w3, bias);
@@ -1001,8 +1043,12 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out, np * D * 4);
     // the wave's pixel index is uniform: loop control and the store's pixel offset stay scalar
     const int wy = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
-#pragma unroll SM_COST_UNROLL
-    for (int pl = wy; pl < np; pl += 4) {
+    // FAST: interior rows, T >= 382.5, adaptive weights (wa + wb <= 1 + 2^-24 bounds the sentinel's G)
+    const bool fast_rows = v > 0 && v < H - 1 && a.grad_trunc >= 382.5f && a.grad_adaptive;
+    // (ND > 0) the lane's record index at pl = 0: a pixel's records start pl records later
+    const int mil_lane = (sgn > 0 ? u0 - lane - 64 * (ND - 1) : u0 + lane) - mbase;
+    // one focus pixel (pl: its index in the segment) with FAST or general elements
+    auto one = [&](int pl, auto fastc) {
         const int u = u0 + pl;
         const ulonglong2 cf = CEN ? fcode[pl] : make_ulonglong2(0, 0);
         float fx = 0.f, fy = 0.f, wa = 0.f, wb = 0.f;
@@ -1016,35 +1062,39 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
         if (ADM) fc = fbgr[pl];
         // element at staged record mi (moving position q = mbase + mi = u - sgn * d, zeros when out
         // of range), stored at byte voff + soff of the pixel's row (voff = d * 4 - soff's part)
-        auto elem = [&](int mi, uint32_t voff, uint32_t soff) {
+        auto elem = [&](auto fastc, int mi, uint32_t voff, uint32_t soff) {
+            constexpr bool FAST = decltype(fastc)::value;
             const int q = mi + mbase;
             if constexpr (NOSEL) {
+                typedef float f2 __attribute__((ext_vector_type(2)));
                 const uint4 r0 = recA(mi);
-                uint32_t pc, gxm, gym;
+                uint32_t pc;
+                uint2 gw;
                 if constexpr (CW == 3) {
-                    const uint2 r1 = SPLIT ? mrecB2[mi] : *(const uint2*)&mrec[RW * mi + 1];
-                    pc = r1.y;                         // icd for out-of-range candidates, else 0
-                    gxm = r0.w;
-                    gym = r1.x;
+                    gw = SPLIT ? mrecB2[mi] : *(const uint2*)&mrec[RW * mi + 1];
+                    pc = r0.w;                         // icd for out-of-range candidates, else 0
                 } else {
                     const uint4 r1 = SPLIT ? mrecB4[mi] : mrec[RW * mi + 1];
                     pc = r1.z;
-                    gxm = r1.x;
-                    gym = r1.y;
+                    gw = make_uint2(r1.x, r1.y);
                 }
-                pc += __popc((uint32_t)cf.x ^ r0.x);
-                pc += __popc((uint32_t)(cf.x >> 32) ^ r0.y);
-                pc += __popc((uint32_t)cf.y ^ r0.z);
-                if (CW == 4) pc += __popc((uint32_t)(cf.y >> 32) ^ r0.w);
-                asm volatile("" : "+v"(pc));   // a v_bcnt accumulate chain, not a sum of scaled counts
-                const float dx = fminf(fabsf(fx - __uint_as_float(gxm)), a.grad_trunc);
-                const float dy = fminf(fabsf(fy - __uint_as_float(gym)), a.grad_trunc);
-                const float t1 = wa * dx;
-                const float t2 = wb * dy;
-                const float g = t1 + t2;
-                const float xg = LAM1 ? -g : -g / a.lam2;
+                pc = bcnt_acc((uint32_t)cf.x ^ r0.x, pc);
+                pc = bcnt_acc((uint32_t)(cf.x >> 32) ^ r0.y, pc);
+                pc = bcnt_acc((uint32_t)cf.y ^ r0.z, pc);
+                if (CW == 4) pc = bcnt_acc((uint32_t)(cf.y >> 32) ^ r0.w, pc);
+                const f2 dv = f2{fx, fy} - f2{__uint_as_float(gw.x), __uint_as_float(gw.y)};
+                float g;
+                if constexpr (FAST) {
+                    const f2 tv = f2{wa, wb} * dv;
+                    g = fabsf(tv.x) + fabsf(tv.y);
+                } else {
+                    const f2 tv = f2{wa, wb} * f2{fminf(fabsf(dv.x), a.grad_trunc), fminf(fabsf(dv.y), a.grad_trunc)};
+                    g = tv.x + tv.y;
+                }
+                // (-fminf(g, 100) == fmaxf(-g, -100): both paths end in a negated conversion)
+                const float xg = LAM1 ? (FAST ? -g : -fminf(g, 100.0f)) : fmaxf(-g / a.lam2, -100.0f);
                 const float t = luta[pc];                       // fl(2 - expf(-min(pc, icd) / lamCen))
-                const float ex = expf_glibc_core(fmaxf(xg, -100.0f), etab);
+                const float ex = expf_glibc_core(xg, LdsExpTab{etab});
                 const float res = t - ex;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, voff, soff,
                                                       SM_COST_STORE_AUX);
@@ -1081,7 +1131,7 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
                 const int ci = oor ? icd : min((int)pc, icd);
                 const float e0 = luta[ci];                // expf(-C / lamCen)
                 const float xg = LAM1 ? -g : -g / a.lam2;
-                const float ex = expf_glibc_core(xg, etab); // expf(-G / lamG)
+                const float ex = expf_glibc_core(xg, LdsExpTab{etab}); // expf(-G / lamG)
                 const float e1 = xg >= -17.5f ? ex : 0.f;
                 const float t = 2.0f - e0;
                 res = t - e1;
@@ -1102,30 +1152,46 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, res), ro, voff, soff,
                                                   SM_COST_STORE_AUX);
         };
-        if constexpr (ONE) {
-            elem(u - sgn * lane - mbase, lane * 4, pl * D * 4);
-        } else if constexpr (ND > 0) {
-            // element k takes disparity d = lane + 64 kk with kk = k (left view) or ND - 1 - k (right
-            // view), so that its record index is mil + 64 (ND - 1 - k) in both views: the LDS reads
-            // take non-negative immediate offsets from one per-lane base, the stores a uniform soffset
-            const int mil = (sgn > 0 ? u - lane - 64 * (ND - 1) : u + lane) - mbase;
+        auto pixel = [&](auto fastc) {
+            if constexpr (ONE) {
+                elem(fastc, u - sgn * lane - mbase, lane * 4, pl * D * 4);
+            } else if constexpr (ND > 0) {
+                // element k takes disparity d = lane + 64 kk with kk = k (left view) or ND - 1 - k (right
+                // view), so that its record index is mil + 64 (ND - 1 - k) in both views: the LDS reads
+                // take non-negative immediate offsets from one per-lane base, the stores a uniform soffset
+                const int mil = mil_lane + pl;
 #pragma unroll
-            for (int k = 0; k < ND; k++) {
-                const int kk = sgn > 0 ? k : ND - 1 - k;
-                elem(mil + 64 * (ND - 1 - k), lane * 4, (uint32_t)(pl * D * 4 + kk * 256));
+                for (int k = 0; k < ND; k++) {
+                    const int kk = sgn > 0 ? k : ND - 1 - k;
+                    elem(fastc, mil + 64 * (ND - 1 - k), lane * 4, (uint32_t)(pl * D * 4 + kk * 256));
+                }
+            } else {
+                const int qstep = sgn * 64;
+                int q = u - sgn * lane;
+                for (int d = lane; d < D; d += 64, q -= qstep) elem(fastc, q - mbase, d * 4, pl * D * 4);
             }
-        } else {
-            const int qstep = sgn * 64;
-            int q = u - sgn * lane;
-            for (int d = lane; d < D; d += 64, q -= qstep) elem(q - mbase, d * 4, pl * D * 4);
-        }
+        };
+        pixel(fastc);
+    };
+    // FAST (see COST_OOR_GRAD): a wave-uniform choice per focus pixel; the general elements are
+    // valid for every pixel.  (Two pixels per trip: no fewer instructions per element.)
+    // (not for ONE: one element per lane and pixel leaves the table read's latency exposed, Teddy
+    // x16 0.164 -> 0.178 ms, profiles/r5n/ab3_teddy.log)
+    constexpr bool FASTOK = SM_COST_FAST && NOSEL && LAM1 && !ONE;
+#pragma unroll SM_COST_UNROLL
+    for (int pl = wy; pl < np; pl += 4) {
+        const int u = u0 + pl;
+        if (FASTOK && fast_rows && u > 0 && u < W - 1)
+            one(pl, std::integral_constant<bool, FASTOK>{});
+        else
+            one(pl, std::false_type{});
     }
 }
 
 size_t cost_smem_bytes(int D, int cwords) {
     const int COST_P = cost_p(D <= 64);
     const size_t nm = COST_P + D - 1;
-    return 16 * (cwords > 2 ? 2 : 1) * nm + 16 * COST_P + 8 * 32 + 4 * 5 * COST_P + 4 * (LUT_A_N + LUT_B_N);
+    return 16 * (cwords > 2 ? 2 : 1) * nm + 16 * COST_P + 4 * 5 * COST_P;   // (+ the static tables)
 }
 
 // SolveAll with PY_LVL = 1 as a standalone pass (used by the reference-ordered API):
@@ -1226,11 +1292,12 @@ static void launch_cost_z(const CostArgs& a, dim3 grid, dim3 block, size_t shm, 
 
 template <int METHOD, bool LAM1, int CW>
 static void launch_cost_nw(const CostArgs& a, dim3 grid, dim3 block, size_t shm, hipStream_t st) {
-    // select-free elements (NOSEL in k_cost): an out-of-range pair's G is fl(wa T) + fl(wb T)
-    // >= 0.999 T there (T = grad_trunc, wa + fl(1 - wa) = 1 up to 2^-24), and its exponential
+    // select-free elements (NOSEL in k_cost): an out-of-range pair's G is at least
+    // fl(wa m) + fl(wb m) >= 0.999 m, m = min(T, COST_OOR_GRAD - 255) (T = grad_trunc,
+    // wa + fl(1 - wa) = 1 up to 2^-24), and its exponential
     // must still round away: xg = -G (lamG == 1) or -G / lamG below -17.5; the clamped
     // 2 - e0 table covers counts up to 128 + icd
-    const float gmin = 0.999f * a.grad_trunc;
+    const float gmin = 0.999f * fminf(a.grad_trunc, COST_OOR_GRAD - 255.0f);
     const float xg = LAM1 ? -gmin : -gmin / a.lam2;
     if constexpr (METHOD == SM_M_CENSUS_GRAD && CW >= 3) {
         if (xg < -17.5f && a.grad_trunc < 1e29f && (int)a.census_default <= 128 && (int)a.census_default >= 0)

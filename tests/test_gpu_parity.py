@@ -132,6 +132,47 @@ def test_grad_cost_constants(oracle, lam_g, trunc, adaptive, md):
         lib.sm_destroy(ctx)
 
 
+def _extreme_pair(H, W, md, seed):
+    """Gray levels 0 / 255 only (every gradient at its bound: +-127.5 inside, +-255 on the border
+    rows and columns), the right image a shifted copy with a few flipped pixels."""
+    rng = np.random.default_rng(seed)
+    lg = (rng.integers(0, 2, (H, W)) * 255).astype(np.uint8)
+    rg = np.roll(lg, -min(md, W - 1) // 3, axis=1)
+    flip = rng.random((H, W)) < 0.2
+    rg = np.where(flip, 255 - rg, rg).astype(np.uint8)
+    pair = {"lgray": lg, "rgray": rg,
+            "lbgr": np.repeat(lg[:, :, None], 3, axis=2).copy(), "rbgr": np.repeat(rg[:, :, None], 3, axis=2).copy()}
+    return pair
+
+
+@pytest.mark.parametrize("trunc,adaptive,md,W", [(500.0, 1, 255, 300), (382.5, 1, 255, 300), (382.0, 1, 255, 300),
+                                                  (700.0, 0, 255, 300), (900.0, 1, 191, 260), (500.0, 0, 127, 200),
+                                                  (500.0, 1, 70, 120), (383.0, 1, 23, 64), (500.0, 1, 255, 2)])
+def test_grad_cost_extremes(oracle, trunc, adaptive, md, W):
+    """censusGrad cost volume on 0 / 255 images, whose gradients sit at their bounds, around the
+    FAST elements' truncation bound (T >= 382.5, k_cost) and for T above the sentinel's range:
+    both views, the unrolled D = 128 / 192 / 256 kernels, D > 64 and D <= 64, and a 2-pixel row."""
+    H = 9
+    pair = _extreme_pair(H, W, md, 7 + md + W)
+    cfg = oracle.config(H, W, md, grad_trunc=trunc, grad_adaptive=adaptive)
+    lib = _capi.load()
+    p = _capi.default_params(md, H, W, aggregation=0, optimization=0, compute_right_view=1)
+    p.grad_trunc, p.grad_adaptive = trunc, adaptive
+    ctx = C.c_void_p()
+    _capi.check(lib, ctx, lib.sm_create(C.byref(ctx), C.byref(p), 0))
+    try:
+        a = {k: np.ascontiguousarray(pair[k]) for k in ("lbgr", "rbgr", "lgray", "rgray")}
+        _capi.check(lib, ctx, lib.sm_set_images(ctx, _capi.ptr(a["lbgr"]), _capi.ptr(a["rbgr"]), W * 3,
+                                                _capi.ptr(a["lgray"]), _capi.ptr(a["rgray"]), W))
+        _capi.check(lib, ctx, lib.sm_cost_calculate(ctx))
+        for view in (0, 1):
+            got = np.empty((H, W, md + 1), np.float32)
+            _capi.check(lib, ctx, lib.sm_get_volume(ctx, view, _capi.ptr(got)))
+            np.testing.assert_array_equal(bits(got), bits(oracle.cost_volume(pair, cfg, view=view)))
+    finally:
+        lib.sm_destroy(ctx)
+
+
 def test_right_view_volume(oracle):
     H, W, md = 33, 52, 19
     pair = S.make_pair(H, W, md + 1, 12)

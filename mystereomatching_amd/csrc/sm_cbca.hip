@@ -509,6 +509,9 @@ struct CbLine {
 __host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (0xf << 8) | (0x7 << 4) | (n & 0xf); }
 static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
+#ifndef SM_CB_RING8_LA
+#define SM_CB_RING8_LA 6   // RING8 tiles in flight (same-process A/B, profiles/r5q: LA 3 5.11-5.18, 4 5.10, 5 5.10, 6 5.02-5.10, 7 5.13 ms)
+#endif
 #ifndef SM_CB_RING8
 #define SM_CB_RING8 1   // H NORM at lag 34 through CbLine::RING8 (0: the runtime-ring sweep, A/B builds)
 #endif
@@ -1017,30 +1020,30 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     // of every trip waits for later tiles' loads too.  Tiles past the line end run (up to PF of
     // them): their loads are bounded or read the next line, their stores are out of range.
     if constexpr (decltype(L)::RING8) {
-        // H NORM at lag 34: eight tiles per trip (one ring cycle), three tiles in flight
-        L.load(ta, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        L.load(tb, T);
-        __builtin_amdgcn_sched_barrier(0);
-        L.load(tc, 2 * T);
-        __builtin_amdgcn_sched_barrier(0);
+        // H NORM at lag 34: eight tiles per trip (one ring cycle), tile k in buffer k, LA tiles in
+        // flight (the buffer a load fills was consumed LA - 8 tiles before, LA <= 7)
+        typename CbLine<HORIZ, MODE, FULL, SCALE, RV, LAGC>::Tile tq[8];
+        constexpr int LA = SM_CB_RING8_LA;
+        static_assert(LA >= 1 && LA <= 7, "RING8 look-ahead");
+#pragma unroll
+        for (int k = 0; k < LA; k++) {
+            L.load(tq[k], k * T);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         for (int j0 = 0; j0 < nst; j0 += 8 * T) {
-            L.load(td, j0 + 3 * T);
-            L.template process<0, 0>(ta, j0);
-            L.load(ta, j0 + 4 * T);
-            L.template process<0, 1>(tb, j0 + T);
-            L.load(tb, j0 + 5 * T);
-            L.template process<0, 2>(tc, j0 + 2 * T);
-            L.load(tc, j0 + 6 * T);
-            L.template process<0, 3>(td, j0 + 3 * T);
-            L.load(td, j0 + 7 * T);
-            L.template process<0, 4>(ta, j0 + 4 * T);
-            L.load(ta, j0 + 8 * T);
-            L.template process<0, 5>(tb, j0 + 5 * T);
-            L.load(tb, j0 + 9 * T);
-            L.template process<0, 6>(tc, j0 + 6 * T);
-            L.load(tc, j0 + 10 * T);
-            L.template process<0, 7>(td, j0 + 7 * T);
+            auto step = [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                L.load(tq[(k + LA) % 8], j0 + (k + LA) * T);
+                L.template process<0, k>(tq[k], j0 + k * T);
+            };
+            step(std::integral_constant<int, 0>{});
+            step(std::integral_constant<int, 1>{});
+            step(std::integral_constant<int, 2>{});
+            step(std::integral_constant<int, 3>{});
+            step(std::integral_constant<int, 4>{});
+            step(std::integral_constant<int, 5>{});
+            step(std::integral_constant<int, 6>{});
+            step(std::integral_constant<int, 7>{});
         }
     } else if constexpr (CbCfg<HORIZ, MODE>::PF == 3) {
         L.load(ta, 0);

@@ -509,6 +509,9 @@ struct CbLine {
 __host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (0xf << 8) | (0x7 << 4) | (n & 0xf); }
 static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
+#ifndef SM_CB_NSV_LA
+#define SM_CB_NSV_LA 3   // NsV tiles in flight (same-process A/B, profiles/r5r: 3 8.10-8.12, 4 8.18-8.20, 5 8.11-8.15 ms: issue-bound)
+#endif
 #ifndef SM_CB_RING8_LA
 #define SM_CB_RING8_LA 6   // RING8 tiles in flight (same-process A/B, profiles/r5q: LA 3 5.11-5.18, 4 5.10, 5 5.10, 6 5.02-5.10, 7 5.13 ms)
 #endif
@@ -774,7 +777,7 @@ struct NsV {
     }
 
     // body of tile n (loop slot RT = n mod NH): on entry A(n) has run and B1(n)'s reads are in
-    // flight (nm); `next` holds tile n + 1's loads, `fill` receives tile n + 3's
+    // flight (nm); `next` holds tile n + 1's loads, `fill` receives tile n + LA's
     template <int RT>
     __device__ __forceinline__ void body(Tile& fill, Tile& next, Norm& nm, int& C) {
         load(fill);
@@ -866,42 +869,42 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
     L.wsa = 0;
     int C = L_t::out_slot(0);
     const int nst = L.len + 2 * L_t::LAG;   // (tiles start at J0; the last stored row is len - 1)
-    typename L_t::Tile ta, tb, tc;
+    // six tile buffers, tile n in buffer n mod 6; LA tiles in flight (body n loads tile n + LA into
+    // the buffer of tile n + LA - 6, whose stage A ran in body n + LA - 7 <= n - 1)
+    constexpr int LA = SM_CB_NSV_LA;
+    static_assert(LA >= 2 && LA <= 6, "NsV look-ahead");
+    typename L_t::Tile tq[6];
     typename L_t::Norm nm;
     static_assert(L_t::NH == 6, "the loop below is written for six tiles");
-    // Prologue: tiles 0 .. 2 loaded in order, A(0), B1(0).  (The scheduler must not interleave
-    // the prologue tiles' loads, and the loop has no exit but its condition: otherwise the
-    // compiler's vmcnt waits at the loop head are conservative.  Up to eight tiles past the line
-    // end are loaded and up to five run: their loads read the zeroed tail pads or nothing, their
-    // stores are out of range.)
-    L.template load<true>(ta);
+    // Prologue: tiles 0 .. LA - 1 loaded in order, A(0), B1(0).  (The scheduler must not
+    // interleave the prologue tiles' loads, and the loop has no exit but its condition: otherwise
+    // the compiler's vmcnt waits at the loop head are conservative.  Up to LA + 5 tiles past the
+    // line end are loaded and up to five run: their loads read the zeroed tail pads or nothing,
+    // their stores are out of range.)
+    L.template load<true>(tq[0]);
     __builtin_amdgcn_sched_barrier(0);
-    L.load(tb);
-    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 1; k < LA; k++) {
+        L.load(tq[k]);
+        __builtin_amdgcn_sched_barrier(0);
 #if SM_CB_NSV_VMWAIT
-    L.dummy_stores();   // the stores of "C(-2)": body 0 then sees the steady-state sequence
-    __builtin_amdgcn_sched_barrier(0);
+        L.dummy_stores();   // the stores of "C(k - LA)": body 0 then sees the steady-state sequence
+        __builtin_amdgcn_sched_barrier(0);
 #endif
-    L.load(tc);
-    __builtin_amdgcn_sched_barrier(0);
-#if SM_CB_NSV_VMWAIT
-    L.dummy_stores();   // "C(-1)"
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    }
     {
         uint32_t pi[T];
-        L.stage_a(ta, pi);
+        L.stage_a(tq[0], pi);
         L.template stage_b1<0>(pi, C, nm);
     }
-    // body n: load tile n + 3 into the buffer of tile n (A(n) ran in body n - 1), A(n + 1) from
-    // the buffer of tile n + 1
+    // body n: load tile n + LA, A(n + 1) from the buffer of tile n + 1
     for (int j0 = J0; j0 < nst; j0 += 6 * T) {
-        L.template body<0>(ta, tb, nm, C);
-        L.template body<1>(tb, tc, nm, C);
-        L.template body<2>(tc, ta, nm, C);
-        L.template body<3>(ta, tb, nm, C);
-        L.template body<4>(tb, tc, nm, C);
-        L.template body<5>(tc, ta, nm, C);
+        L.template body<0>(tq[LA % 6], tq[1], nm, C);
+        L.template body<1>(tq[(1 + LA) % 6], tq[2], nm, C);
+        L.template body<2>(tq[(2 + LA) % 6], tq[3], nm, C);
+        L.template body<3>(tq[(3 + LA) % 6], tq[4], nm, C);
+        L.template body<4>(tq[(4 + LA) % 6], tq[5], nm, C);
+        L.template body<5>(tq[(5 + LA) % 6], tq[0], nm, C);
     }
 }
 

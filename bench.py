@@ -211,12 +211,6 @@ def main():
         if host_maps is not None:
             sb.download_async(host_maps)
 
-    # measured HBM ceiling next to the 8 TB/s spec (SURVEY §8d): a dwordx4 copy over a buffer the
-    # size of one pair's volume (at least 2 GiB, far past the 256 MB Infinity Cache)
-    ceiling = None
-    if not args.no_profile:
-        ceiling = sb.copy_ceiling(max(H * W * D * 4, 2 << 30), reps=5)
-
     for _ in range(args.warmup):
         step()
     sb.synchronize()
@@ -236,6 +230,14 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # measured HBM ceiling next to the 8 TB/s spec (SURVEY §8d): a dwordx4 copy over a buffer the
+    # size of one pair's volume (at least 2 GiB, far past the 256 MB Infinity Cache).  After the
+    # timed loop: run right before the warmup it slowed NL's first steps (Teddy x16 6.83 -> 7.32 ms
+    # with three warmup steps, profiles/r5t)
+    ceiling = None
+    if not args.no_profile:
+        ceiling = sb.copy_ceiling(max(H * W * D * 4, 2 << 30), reps=5)
 
     # Schedule A/B on the SAME context (same device allocations, sm_set_schedule): the default
     # schedule and one stream, timed bare in interleaved rounds (order alternating), so the

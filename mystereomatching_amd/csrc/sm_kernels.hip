@@ -845,6 +845,12 @@ void launch_prep(const PrepArgs& a, int n, hipStream_t st) {
 #ifndef SM_COST_SPLIT
 #define SM_COST_SPLIT 1
 #endif
+#ifndef SM_COST_ONE_PAIR
+#define SM_COST_ONE_PAIR 1   // D <= 64: two focus pixels per trip (profiles/r5t/ab_one.log)
+#endif
+#ifndef SM_COST_ONE_FAST
+#define SM_COST_ONE_FAST 1   // D <= 64: FAST elements too, with two pixels per trip (Teddy x16 0.169 -> 0.166 ms)
+#endif
 #ifndef SM_COST_UNROLL
 #define SM_COST_UNROLL 1
 #endif
@@ -1175,11 +1181,25 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
     };
     // FAST (see COST_OOR_GRAD): a wave-uniform choice per focus pixel; the general elements are
     // valid for every pixel.  (Two pixels per trip: no fewer instructions per element.)
-    // (not for ONE: one element per lane and pixel leaves the table read's latency exposed, Teddy
-    // x16 0.164 -> 0.178 ms, profiles/r5n/ab3_teddy.log)
-    constexpr bool FASTOK = SM_COST_FAST && NOSEL && LAM1 && !ONE;
+    // (for ONE only with two pixels per trip: one element per lane and pixel leaves the table
+    // read's latency exposed, Teddy x16 0.164 -> 0.178 ms, profiles/r5n/ab3_teddy.log)
+    constexpr bool FASTOK = SM_COST_FAST && NOSEL && LAM1 && (!ONE || SM_COST_ONE_FAST);
+    int pl = wy;
+    if constexpr (ONE && SM_COST_ONE_PAIR) {
+        // D <= 64: pixels pl and pl + 4 per trip, two independent elements per lane
+        for (; pl + 4 < np; pl += 8) {
+            const int u = u0 + pl;
+            if (FASTOK && fast_rows && u > 0 && u + 4 < W - 1) {
+                one(pl, std::integral_constant<bool, FASTOK>{});
+                one(pl + 4, std::integral_constant<bool, FASTOK>{});
+            } else {
+                one(pl, std::false_type{});
+                one(pl + 4, std::false_type{});
+            }
+        }
+    }
 #pragma unroll SM_COST_UNROLL
-    for (int pl = wy; pl < np; pl += 4) {
+    for (; pl < np; pl += 4) {
         const int u = u0 + pl;
         if (FASTOK && fast_rows && u > 0 && u < W - 1)
             one(pl, std::integral_constant<bool, FASTOK>{});

@@ -509,6 +509,12 @@ struct CbLine {
 __host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (0xf << 8) | (0x7 << 4) | (n & 0xf); }
 static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
+#ifndef SM_CB_NSV2
+#define SM_CB_NSV2 1   // V NORM_SCAN at lag 34 as two waves per line (k_cbca_nsv2; 0: k_cbca_nsv)
+#endif
+#ifndef SM_CB_NSV2_AEARLY
+#define SM_CB_NSV2_AEARLY 1   // NsV2: stage A's prefixes before the B1 barrier, only its writes after
+#endif
 #ifndef SM_CB_NSV_LA
 #define SM_CB_NSV_LA 3   // NsV tiles in flight (same-process A/B, profiles/r5r: 3 8.10-8.12, 4 8.18-8.20, 5 8.11-8.15 ms: issue-bound)
 #endif
@@ -576,15 +582,19 @@ struct NsV {
 
     // loads the next tile (tiles are loaded in order, T rows apart); FIRST: the tile at row
     // -SHIFT, whose rows before the line read 0 (out-of-range offsets)
-    template <bool FIRST = false>
+    // (MASK: 1 = the volume rows, 2 = arm set 0, 4 = arm set 1; NsV2's waves load their parts)
+    template <bool FIRST = false, int MASK = 7>
     __device__ __forceinline__ void load(Tile& t) {
         // tiles whose rows pass the allocation (only ever past the line end) read 0
-        const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xld, jld + T <= rows_avail ? 0x7fffffff : 0);
+        if constexpr (MASK & 1) {
+            const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xld, jld + T <= rows_avail ? 0x7fffffff : 0);
 #pragma unroll
-        for (int k = 0; k < T; k++)
-            t.x[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, (FIRST && k < SHIFT) ? (int)0x80000000 : (int)xo[k], 0, 2));
+            for (int k = 0; k < T; k++)
+                t.x[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, (FIRST && k < SHIFT) ? (int)0x80000000 : (int)xo[k], 0, 2));
+        }
 #pragma unroll
         for (int s = 0; s < 2; s++) {
+            if (!(MASK & (2 << s))) continue;
             const uint32_t rl = min(rld, rld_max);
             const uint32_t roff = s == 0 ? rl - (uint32_t)LAG * rowb : rl;   // rows >= -2 LAG: >= 0
             t.a0[s] = __builtin_amdgcn_raw_buffer_load_b32(A0r[s], (int)aown, (int)roff, 0);
@@ -610,6 +620,7 @@ struct NsV {
     __device__ __forceinline__ static int out_slot(int ws) { return ws - LAG < 0 ? ws - LAG + R : ws - LAG; }
 
     // stage A: rows j0 .. j0+T-1 into the S1 / area rings at slot wsa; pass intersections pi
+    template <bool PI = true>
     __device__ __forceinline__ void stage_a(const Tile& t, uint32_t (&pi)[T]) {
         const bool mirror = __builtin_expect(wsa == 0, 0);
         float* w1 = r1 + wsa * 64 + lane;
@@ -621,7 +632,7 @@ struct NsV {
             S1 = S1 + t.x[k];
             s1v[k] = S1;
             w1[k * 64] = S1;
-            pi[k] = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[0], k), t.a1[0][k]);
+            if constexpr (PI) pi[k] = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[0], k), t.a1[0][k]);
             const uint32_t pp = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[1], k), t.a1[1][k]);
             Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
             acv[k] = (uint16_t)Acc;
@@ -776,6 +787,45 @@ struct NsV {
         for (int k = 0; k < T; k++) buf_st(r, 0x80000000u + 4u * k, 0, 0.f);   // (distinct: not merged)
     }
 
+    // NsV2's second wave: the pass intersections of a tile (stage A's pi without the rings)
+    __device__ __forceinline__ void pass_isect(const Tile& t, uint32_t (&pi)[T]) const {
+#pragma unroll
+        for (int k = 0; k < T; k++) pi[k] = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[0], k), t.a1[0][k]);
+    }
+    // NsV2's first wave: stage A as its register part (the S1 and area prefixes of the tile's
+    // rows) and its ring writes, so that the writes alone wait for the second wave's B1 reads
+    struct AVals {
+        float s1v[T];
+        uint16_t acv[T];
+    };
+    __device__ __forceinline__ void stage_a_values(const Tile& t, AVals& v) {
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            S1 = S1 + t.x[k];
+            v.s1v[k] = S1;
+            const uint32_t pp = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[1], k), t.a1[1][k]);
+            Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
+            v.acv[k] = (uint16_t)Acc;
+        }
+    }
+    __device__ __forceinline__ void stage_a_write(const AVals& v) {
+        float* w1 = r1 + wsa * 64 + lane;
+        uint16_t* wa = ra + wsa * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            w1[k * 64] = v.s1v[k];
+            wa[k * 64] = v.acv[k];
+        }
+        if (__builtin_expect(wsa == 0, 0)) {
+#pragma unroll
+            for (int k = 0; k < T - 1; k++) {
+                r1[(R + k) * 64 + lane] = v.s1v[k];
+                ra[(R + k) * 64 + lane] = v.acv[k];
+            }
+        }
+        wsa = wsa + T == R ? 0 : wsa + T;
+    }
+
     // body of tile n (loop slot RT = n mod NH): on entry A(n) has run and B1(n)'s reads are in
     // flight (nm); `next` holds tile n + 1's loads, `fill` receives tile n + LA's
     template <int RT>
@@ -797,12 +847,11 @@ struct NsV {
     }
 };
 
+// the line's state (both NsV forms); the caller zeroes the rings
 template <bool RV, bool CHECK>
-__device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, float* smem) {
+__device__ __forceinline__ void nsv_setup(NsV<RV, CHECK>& L, const CbcaArgs& a, const int blk, float* smem) {
     using L_t = NsV<RV, CHECK>;
     constexpr int T = L_t::T;
-    L_t L;
-    L.lane = (int)threadIdx.x;
     const int nchunks = a.D / 64;
     const int per_pair = a.W * nchunks;
     const int b = blk / per_pair;
@@ -858,15 +907,25 @@ __device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, f
         L.oa = (uint32_t)(size_t)(lds_c*)L.ra + 2u * (uint32_t)L.lane;
     }
     L.RR = (uint32_t)L_t::R | ((uint32_t)(65536 - L_t::R) << 16);
-    for (int w = L.lane; w < cbca_nsv_smem_words(); w += 64) smem[w] = 0.f;   // rows before the line: S = 0, area = 0
 #pragma unroll
     for (int r = 0; r < L_t::NH; r++)
 #pragma unroll
         for (int k = 0; k < T; k++) L.hh[r][k] = L.ht[r][k] = L.o1;   // rows before the line: any in-ring address (outputs < 0 are not stored)
-    __syncthreads();
     L.S1 = L.S2 = 0.f;
     L.Acc = 0;
     L.wsa = 0;
+}
+
+template <bool RV, bool CHECK>
+__device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, float* smem) {
+    using L_t = NsV<RV, CHECK>;
+    constexpr int T = L_t::T;
+    constexpr int J0 = -L_t::SHIFT;
+    L_t L;
+    L.lane = (int)threadIdx.x;
+    nsv_setup(L, a, blk, smem);
+    for (int w = L.lane; w < cbca_nsv_smem_words(); w += 64) smem[w] = 0.f;   // rows before the line: S = 0, area = 0
+    __syncthreads();
     int C = L_t::out_slot(0);
     const int nst = L.len + 2 * L_t::LAG;   // (tiles start at J0; the last stored row is len - 1)
     // six tile buffers, tile n in buffer n mod 6; LA tiles in flight (body n loads tile n + LA into
@@ -914,6 +973,126 @@ template <bool RV, bool CHECK>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_cbca_nsv(const CbcaArgs a) {
     extern __shared__ float smem[];
     cbca_run_nsv<RV, CHECK>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
+}
+
+// NsV2: the same sweep as two waves per line sharing the line's rings (one workgroup of 128).
+// A single NsV wave is issue-bound at one wave per SIMD (its rings allow three lines per CU);
+// two waves per line double the issuing waves without more LDS.  Wave 0 runs stage A (volume
+// rows and perpendicular arms -> S1 / area rings), wave 1 the pass intersections, B1, B2 and C.
+// Per tile n two workgroup barriers: after A(n) (its ring writes done) and after B1(n) (its ring
+// reads done, the only reads A(n + 1) can overwrite: B1(n) spans rows j0 - 2 lag - 1 .. j0 + T - 1
+// of the R-slot ring).  The first wave computes A(n + 1)'s prefixes beside B1(n) and only its
+// ring writes wait for B1(n)'s barrier, so the second wave's B1, B2, C are the critical path.
+// Both waves run the same tiles and one extra barrier each (the first wave's at the end, the
+// second's at the start), so they pass the same barriers in the same order.
+__device__ __forceinline__ void nsv2_bar_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void nsv2_bar() { asm volatile("s_barrier" ::: "memory"); }
+
+template <bool RV, bool CHECK>
+__device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, float* smem) {
+    using L_t = NsV<RV, CHECK>;
+    using Tile = typename L_t::Tile;
+    constexpr int T = L_t::T;
+    constexpr int J0 = -L_t::SHIFT;
+    constexpr int LA = SM_CB_NSV_LA;
+    static_assert(LA >= 2 && LA <= 6, "NsV look-ahead");
+    static_assert(L_t::NH == 6, "the loops below are written for six tiles");
+    L_t L;
+    L.lane = (int)threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    nsv_setup(L, a, blk, smem);
+    for (int w = (int)threadIdx.x; w < cbca_nsv_smem_words(); w += 128) smem[w] = 0.f;   // rows before the line
+    __syncthreads();
+    const int nst = L.len + 2 * L_t::LAG;
+    Tile tq[6];
+    if (wid == 0) {
+        // stage A: tile n's rows into the rings, then the two barriers of tile n
+        L.template load<true, 5>(tq[0]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 1; k < LA; k++) {
+            L.template load<false, 5>(tq[k]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        for (int j0 = J0; j0 < nst; j0 += 6 * T) {
+            auto step = [&](auto rc) {
+                constexpr int n = decltype(rc)::value;
+                L.template load<false, 5>(tq[(n + LA) % 6]);
+#if SM_CB_NSV_VMWAIT
+                L_t::launder(tq[n]);
+#endif
+#if SM_CB_NSV2_AEARLY
+                typename L_t::AVals v;
+                L.stage_a_values(tq[n], v);
+                nsv2_bar();        // B1(n - 1) read
+                L.stage_a_write(v);
+                nsv2_bar_lgkm();   // A(n) written
+#else
+                uint32_t pi[T];
+                L.template stage_a<false>(tq[n], pi);
+                nsv2_bar_lgkm();   // A(n) written
+                nsv2_bar();        // B1(n) read
+#endif
+            };
+            step(std::integral_constant<int, 0>{});
+            step(std::integral_constant<int, 1>{});
+            step(std::integral_constant<int, 2>{});
+            step(std::integral_constant<int, 3>{});
+            step(std::integral_constant<int, 4>{});
+            step(std::integral_constant<int, 5>{});
+        }
+#if SM_CB_NSV2_AEARLY
+        nsv2_bar();   // (pairs with the second wave's last "B1 read")
+#endif
+    } else {
+        typename L_t::Norm nm;
+        int C = L_t::out_slot(0);
+        L.template load<false, 2>(tq[0]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 1; k < LA; k++) {
+            L.template load<false, 2>(tq[k]);
+            __builtin_amdgcn_sched_barrier(0);
+#if SM_CB_NSV_VMWAIT
+            L.dummy_stores();   // the stores of "C(k - LA)": step 0 sees the steady-state sequence
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+#if SM_CB_NSV2_AEARLY
+        nsv2_bar();   // (pairs with the first wave's "B1(-1) read")
+#endif
+        for (int j0 = J0; j0 < nst; j0 += 6 * T) {
+            auto step = [&](auto rc) {
+                constexpr int n = decltype(rc)::value;
+                L.template load<false, 2>(tq[(n + LA) % 6]);
+#if SM_CB_NSV_VMWAIT
+                L_t::launder(tq[n]);
+#endif
+                uint32_t pi[T];
+                L.pass_isect(tq[n], pi);
+                nsv2_bar();                                   // A(n) written
+                L.template stage_b1<n>(pi, C, nm);            // B1(n)
+                nsv2_bar_lgkm();                              // B1(n) read
+                L.stage_b2(nm, C);                            // B2(n)
+                float s2h[T], s2t[T];
+                L.template stage_c_read<n>(s2h, s2t);         // C(n)
+                C = C + T >= L_t::R ? C + T - L_t::R : C + T;
+                L.stage_c_store(s2h, s2t);
+            };
+            step(std::integral_constant<int, 0>{});
+            step(std::integral_constant<int, 1>{});
+            step(std::integral_constant<int, 2>{});
+            step(std::integral_constant<int, 3>{});
+            step(std::integral_constant<int, 4>{});
+            step(std::integral_constant<int, 5>{});
+        }
+    }
+}
+
+template <bool RV, bool CHECK>
+__global__ __launch_bounds__(128) void k_cbca_nsv2(const CbcaArgs a) {
+    extern __shared__ float smem[];
+    cbca_run_nsv2<RV, CHECK>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
 }
 template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int LAGC>
 __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
@@ -1126,6 +1305,17 @@ static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
         if (nsv_ok(a)) {
             dim3 grid(a.W * (a.D / 64) * n), block(64);
             const size_t shm = 4 * (size_t)cbca_nsv_smem_words();
+#if SM_CB_NSV2
+            block = dim3(128);
+            if (a.view == 0) {
+                if (a.div_safe) hipLaunchKernelGGL((k_cbca_nsv2<false, false>), grid, block, shm, st, a);
+                else hipLaunchKernelGGL((k_cbca_nsv2<false, true>), grid, block, shm, st, a);
+            } else {
+                if (a.div_safe) hipLaunchKernelGGL((k_cbca_nsv2<true, false>), grid, block, shm, st, a);
+                else hipLaunchKernelGGL((k_cbca_nsv2<true, true>), grid, block, shm, st, a);
+            }
+            return;
+#endif
             if (a.view == 0) {
                 if (a.div_safe) hipLaunchKernelGGL((k_cbca_nsv<false, false>), grid, block, shm, st, a);
                 else hipLaunchKernelGGL((k_cbca_nsv<false, true>), grid, block, shm, st, a);

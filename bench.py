@@ -115,8 +115,7 @@ def parse():
                          "int16 maps in pinned host memory, SURVEY §8d's `disp_out` ready)")
     ap.add_argument("--sub-batch", type=int, default=0, help="sm_params.sub_batch: run the pairs in groups of k")
     ap.add_argument("--streams", type=int, default=0,
-                    help="sm_params.num_streams: 0 = auto (two streams, two pair groups: CBCA batches of >= 8 pairs with "
-                         "4-path SGM, or >= 256 MiB per pair without the two-wave lag-34 V sweep), "
+                    help="sm_params.num_streams: 0 = auto (two streams, two groups for CBCA at >= 256 MiB per pair), "
                          "1 = one stream, s = groups alternate over s streams")
     ap.add_argument("--fuse-norm-scan", choices=["auto", "on", "off"], default="auto",
                     help="CBCA: fuse iteration k's normalising sweep with iteration k+1's scan (sm_params.fuse_norm_scan; "
@@ -272,8 +271,8 @@ def main():
     kernels, ms_prof = {}, None
     kern_schedule = "one stream: the timed loop's own context" if args.streams == 1 else \
         "one stream (the timed loop's own context switched by sm_set_schedule): each kernel alone; the timed " \
-        "loop runs sm_params.num_streams = %d (0 = auto: two pair groups on two streams for CBCA batches of >= 8 " \
-        "pairs with 4-path SGM, or >= 256 MiB per pair without the two-wave V sweep)" % args.streams
+        "loop runs sm_params.num_streams = %d (0 = auto: two pair groups on two streams for CBCA >= 256 MiB " \
+        "per pair)" % args.streams
     if profile:
         sbk = sb
         if args.streams != 1:

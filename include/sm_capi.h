@@ -118,8 +118,7 @@ typedef struct sm_params {
     int32_t do_last_median_blur; /* Do_lastMedianBlur = 1 (h:80) */
     /* scheduling of sm_run (results are identical for every setting): */
     int32_t sub_batch;           /* run the n pairs in groups of k (0 = one group), stages back to back */
-    int32_t num_streams;         /* 0 (default): auto -- with CBCA and a volume >= 256 MiB per pair
-                                  * whose V NORM_SCAN is not the two-wave lag-34 sweep (or
+    int32_t num_streams;         /* 0 (default): auto -- with CBCA and a volume >= 256 MiB per pair (or
                                   * batch_capacity >= 8 with 4-path SGM and no refinement), two
                                   * streams and (sub_batch 0) two groups of n / 2 pairs; with SGM
                                   * and no refinement the groups are pipelined ACROSS calls: sm_run

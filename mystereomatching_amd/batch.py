@@ -44,11 +44,13 @@ def shard_bounds(n: int, world: int, rank: int):
 def sub_sizes(per: int, sub_batch=0) -> list:
     """Sub-block sizes of a rank's block of `per` pairs.  sub_batch: an int s > 0 (blocks of s,
     the last one short), a sequence of sizes (used while they fit, the rest in one block), or 0
-    (auto): a small first and last block around one large one (8 pairs: 1, 6, 1; 16: 2, 12, 2), so
-    the transfers that cannot overlap compute -- the first block's inputs and the last block's
-    maps -- are small while most pairs run in one batched call (configs[4]'s 8 pairs of 1080p per
-    rank, RCCL world 1: 1, 6, 1 ran 54.7 ms per step against 55.5 for 4, 4, 56.2 for 2, 4, 2 and
-    56.0 for one block, resident 52.1 ms; profiles/r5c)."""
+    (auto): a small first block, then one large one (8 pairs: 1, 7; 16: 2, 14), so the transfer
+    that cannot overlap compute at the start -- the first block's inputs -- is small while most
+    pairs run in one batched call, whose two pair groups then pipeline as in a resident run
+    (configs[4]'s 8 pairs of 1080p per rank, RCCL world 1, with the two-wave V sweep: 1, 7 ran
+    52.9 ms per step against 53.4 for 1, 6, 1, 53.6 for 2, 6, 54.3 for 1, 3, 3, 1 and 54.4 for
+    one block, resident 50.0 ms, profiles/r5z; with the one-wave sweep 1, 6, 1 had been best,
+    profiles/r5c)."""
     if per <= 0:
         return []
     if isinstance(sub_batch, (list, tuple)):
@@ -64,7 +66,7 @@ def sub_sizes(per: int, sub_batch=0) -> list:
         if per < 4:
             return [1] * per
         h = max(1, per // 8)
-        return [h, per - 2 * h, h]
+        return [h, per - h]
     return [min(s, per - i) for i in range(0, per, s)]
 
 

@@ -122,7 +122,6 @@ struct sm_ctx {
     hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
     hipEvent_t ev_run = nullptr, ev_copy = nullptr;     // run done (c->st) / async copy done (cst)
     bool copy_pending = false;  // an async copy may still read the maps
-    bool nsv_sweep = false;     // CBCA's V NORM_SCAN runs as the two-wave lag-34 sweep (schedule rule)
     std::vector<hipEvent_t> xev;                        // stagger / join events
     hipEvent_t stagger_ev = nullptr;                    // SM_STAGGER_STAGE 1: recorded after the first CBCA sweep
     // profiling
@@ -319,21 +318,21 @@ void build_luts(sm_ctx* c) {
 }
 
 // sm_params.num_streams / sub_batch -> the schedule sm_run follows (sm_create, sm_set_schedule).
-// num_streams 0 (auto): two streams with CBCA at volumes >= 256 MiB per pair whose V NORM_SCAN
-// is not the two-wave lag-34 sweep, where the next group's prep, cost and H scan share the CUs
-// with this group's LDS-bound sweep (full resolution 37.8 -> 36.0 ms, 1080p x8 53.0 -> 50.3 ms
-// with the one-wave sweeps, profiles/r4j; with the two-wave sweep, which keeps all four SIMDs
-// busy, full resolution is as fast on one stream: 36.04 vs 35.99 ms on one context,
-// profiles/r5_final2); and for batches of >= 8 pairs with 4-path SGM and no refinement (Teddy
-// x16 in two groups of 8: 2.48 -> 2.37 ms, 1080p x8 47.3 -> 47.1 ms, profiles/r5y; KITTI's
-// 8-path SGM got slower, 8.27 -> 8.52 ms).  Side streams are created on first use and kept.
+// num_streams 0 (auto): two streams with CBCA at volumes >= 256 MiB per pair, where the next
+// group's prep, cost and H scan share the CUs with this group's LDS-bound NORM_SCAN sweep
+// (full resolution 37.8 -> 36.0 ms, 1080p x8 53.0 -> 50.3 ms, profiles/r4j; since the groups are
+// pipelined across calls, round 5: KITTI x4 8.22 -> 7.58 ms, profiles/r5_final_wl; with the
+// two-wave V sweep full resolution is as fast on one stream, 36.04 vs 35.99 ms, and KITTI still
+// gains, 8.09 -> 7.58 ms, so the rule stays); and for batches of >= 8 smaller pairs with 4-path
+// SGM and no refinement (Teddy x16 in two groups of 8: 2.48 -> 2.37 ms, profiles/r5_final3).
+// Side streams are created on first use and kept.
 sm_status apply_schedule(sm_ctx* c, int num_streams, int sub_batch) {
     const sm_params& p = c->p;
     if (sub_batch < 0 || num_streams < 0 || num_streams > 4)
         return fail(c, SM_EINVAL, "sub_batch >= 0 and num_streams in [0, 4] required");
     c->sub_batch = sub_batch;
     c->auto_groups = num_streams == 0 && p.aggregation == SM_AGG_CBCA && p.cbca_iterations > 0 &&
-                     ((c->nvol * 4 >= ((size_t)1 << 28) && !c->nsv_sweep) ||
+                     (c->nvol * 4 >= ((size_t)1 << 28) ||
                       (c->cap >= 8 && p.optimization == SM_OPT_SGM && p.sgm_paths == 4 && !p.do_refine));
     c->nstreams = c->auto_groups ? 2 : (num_streams < 1 ? 1 : num_streams);
     // the pipelined form of the two groups (sm_run): CBCA + SGM without refinement, where the
@@ -1131,7 +1130,6 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         // size (Teddy x16: 0.765 -> 0.692 ms, profiles/r4b/ab_teddy.txt)
         const bool nsv = cbca_lag(*p) == 34 && p->num_disparities % 64 == 0;
         c->fuse_norm_scan = p->fuse_norm_scan == 1 || (p->fuse_norm_scan == -1 && (nsv || c->nvol * 4 >= ((size_t)1 << 28)));
-        c->nsv_sweep = nsv && c->fuse_norm_scan && p->cbca_iterations > 1;
         if ((s = apply_schedule(c, p->num_streams, p->sub_batch))) return s;
         for (int i = 0; i < 16; i++) {
             hipEvent_t e;

@@ -98,7 +98,7 @@ def test_single_process_sub_blocks():
 def test_sub_sizes():
     from mystereomatching_amd.batch import sub_sizes
     assert [sub_sizes(p) for p in (0, 1, 2, 3, 4, 8, 9, 16)] == \
-        [[], [1], [1, 1], [1, 1, 1], [1, 2, 1], [1, 6, 1], [1, 7, 1], [2, 12, 2]]
+        [[], [1], [1, 1], [1, 1, 1], [1, 3], [1, 7], [1, 8], [2, 14]]
     for p in range(0, 40):
         for sb in (0, 1, 3, 7, [2, 4], (1, 6, 1), [50]):
             z = sub_sizes(p, sb)

@@ -509,12 +509,6 @@ struct CbLine {
 __host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (0xf << 8) | (0x7 << 4) | (n & 0xf); }
 static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
-#ifndef SM_CB_NSV2
-#define SM_CB_NSV2 1   // V NORM_SCAN at lag 34 as two waves per line (k_cbca_nsv2; 0: k_cbca_nsv)
-#endif
-#ifndef SM_CB_NSV2_AEARLY
-#define SM_CB_NSV2_AEARLY 1   // NsV2: stage A's prefixes before the B1 barrier, only its writes after
-#endif
 #ifndef SM_CB_NSV_LA
 #define SM_CB_NSV_LA 3   // NsV tiles in flight (same-process A/B, profiles/r5r: 3 8.10-8.12, 4 8.18-8.20, 5 8.11-8.15 ms: issue-bound)
 #endif
@@ -618,35 +612,6 @@ struct NsV {
     }
     // ring slot of output row i0 = j0 - LAG of the tile whose first input row sits at slot ws
     __device__ __forceinline__ static int out_slot(int ws) { return ws - LAG < 0 ? ws - LAG + R : ws - LAG; }
-
-    // stage A: rows j0 .. j0+T-1 into the S1 / area rings at slot wsa; pass intersections pi
-    template <bool PI = true>
-    __device__ __forceinline__ void stage_a(const Tile& t, uint32_t (&pi)[T]) {
-        const bool mirror = __builtin_expect(wsa == 0, 0);
-        float* w1 = r1 + wsa * 64 + lane;
-        uint16_t* wa = ra + wsa * 64 + lane;
-        float s1v[T];
-        uint16_t acv[T];
-#pragma unroll
-        for (int k = 0; k < T; k++) {
-            S1 = S1 + t.x[k];
-            s1v[k] = S1;
-            w1[k * 64] = S1;
-            if constexpr (PI) pi[k] = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[0], k), t.a1[0][k]);
-            const uint32_t pp = pkmin((uint32_t)__builtin_amdgcn_readlane((int)t.a0[1], k), t.a1[1][k]);
-            Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
-            acv[k] = (uint16_t)Acc;
-            wa[k * 64] = acv[k];
-        }
-        if (mirror) {
-#pragma unroll
-            for (int k = 0; k < T - 1; k++) {
-                r1[(R + k) * 64 + lane] = s1v[k];
-                ra[(R + k) * 64 + lane] = acv[k];
-            }
-        }
-        wsa = wsa + T == R ? 0 : wsa + T;
-    }
 
     // stage B1: window slots of the normalised outputs at i = j - LAG (C: their first slot) and
     // their S1 / area reads; the S1 addresses are kept for the scan stage LAG positions later
@@ -825,26 +790,6 @@ struct NsV {
         }
         wsa = wsa + T == R ? 0 : wsa + T;
     }
-
-    // body of tile n (loop slot RT = n mod NH): on entry A(n) has run and B1(n)'s reads are in
-    // flight (nm); `next` holds tile n + 1's loads, `fill` receives tile n + LA's
-    template <int RT>
-    __device__ __forceinline__ void body(Tile& fill, Tile& next, Norm& nm, int& C) {
-        load(fill);
-#if SM_CB_NSV_VMWAIT
-        // one wait for all of tile n + 1's loads (instead of one per register): an empty asm
-        // that reads and redefines all of them, so the compiler's wait sits in front of it
-        launder(next);
-#endif
-        uint32_t pi[T];
-        stage_a(next, pi);                                        // A(n + 1)
-        stage_b2(nm, C);                                          // B2(n)
-        float s2h[T], s2t[T];
-        stage_c_read<RT>(s2h, s2t);                               // C(n) reads
-        C = C + T >= R ? C + T - R : C + T;
-        stage_b1<(RT + 1) % NH>(pi, C, nm);                       // B1(n + 1)
-        stage_c_store(s2h, s2t);                                  // C(n) stores
-    }
 };
 
 // the line's state (both NsV forms); the caller zeroes the rings
@@ -916,65 +861,6 @@ __device__ __forceinline__ void nsv_setup(NsV<RV, CHECK>& L, const CbcaArgs& a, 
     L.wsa = 0;
 }
 
-template <bool RV, bool CHECK>
-__device__ __forceinline__ void cbca_run_nsv(const CbcaArgs& a, const int blk, float* smem) {
-    using L_t = NsV<RV, CHECK>;
-    constexpr int T = L_t::T;
-    constexpr int J0 = -L_t::SHIFT;
-    L_t L;
-    L.lane = (int)threadIdx.x;
-    nsv_setup(L, a, blk, smem);
-    for (int w = L.lane; w < cbca_nsv_smem_words(); w += 64) smem[w] = 0.f;   // rows before the line: S = 0, area = 0
-    __syncthreads();
-    int C = L_t::out_slot(0);
-    const int nst = L.len + 2 * L_t::LAG;   // (tiles start at J0; the last stored row is len - 1)
-    // six tile buffers, tile n in buffer n mod 6; LA tiles in flight (body n loads tile n + LA into
-    // the buffer of tile n + LA - 6, whose stage A ran in body n + LA - 7 <= n - 1)
-    constexpr int LA = SM_CB_NSV_LA;
-    static_assert(LA >= 2 && LA <= 6, "NsV look-ahead");
-    typename L_t::Tile tq[6];
-    typename L_t::Norm nm;
-    static_assert(L_t::NH == 6, "the loop below is written for six tiles");
-    // Prologue: tiles 0 .. LA - 1 loaded in order, A(0), B1(0).  (The scheduler must not
-    // interleave the prologue tiles' loads, and the loop has no exit but its condition: otherwise
-    // the compiler's vmcnt waits at the loop head are conservative.  Up to LA + 5 tiles past the
-    // line end are loaded and up to five run: their loads read the zeroed tail pads or nothing,
-    // their stores are out of range.)
-    L.template load<true>(tq[0]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 1; k < LA; k++) {
-        L.load(tq[k]);
-        __builtin_amdgcn_sched_barrier(0);
-#if SM_CB_NSV_VMWAIT
-        L.dummy_stores();   // the stores of "C(k - LA)": body 0 then sees the steady-state sequence
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-    }
-    {
-        uint32_t pi[T];
-        L.stage_a(tq[0], pi);
-        L.template stage_b1<0>(pi, C, nm);
-    }
-    // body n: load tile n + LA, A(n + 1) from the buffer of tile n + 1
-    for (int j0 = J0; j0 < nst; j0 += 6 * T) {
-        L.template body<0>(tq[LA % 6], tq[1], nm, C);
-        L.template body<1>(tq[(1 + LA) % 6], tq[2], nm, C);
-        L.template body<2>(tq[(2 + LA) % 6], tq[3], nm, C);
-        L.template body<3>(tq[(3 + LA) % 6], tq[4], nm, C);
-        L.template body<4>(tq[(4 + LA) % 6], tq[5], nm, C);
-        L.template body<5>(tq[(5 + LA) % 6], tq[0], nm, C);
-    }
-}
-
-// (at most three waves per CU fit the rings: tell the scheduler so that it schedules for latency,
-// not for registers)
-template <bool RV, bool CHECK>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_cbca_nsv(const CbcaArgs a) {
-    extern __shared__ float smem[];
-    cbca_run_nsv<RV, CHECK>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
-}
-
 // NsV2: the same sweep as two waves per line sharing the line's rings (one workgroup of 128).
 // A single NsV wave is issue-bound at one wave per SIMD (its rings allow three lines per CU);
 // two waves per line double the issuing waves without more LDS.  Wave 0 runs stage A (volume
@@ -1021,18 +907,11 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
 #if SM_CB_NSV_VMWAIT
                 L_t::launder(tq[n]);
 #endif
-#if SM_CB_NSV2_AEARLY
                 typename L_t::AVals v;
                 L.stage_a_values(tq[n], v);
                 nsv2_bar();        // B1(n - 1) read
                 L.stage_a_write(v);
                 nsv2_bar_lgkm();   // A(n) written
-#else
-                uint32_t pi[T];
-                L.template stage_a<false>(tq[n], pi);
-                nsv2_bar_lgkm();   // A(n) written
-                nsv2_bar();        // B1(n) read
-#endif
             };
             step(std::integral_constant<int, 0>{});
             step(std::integral_constant<int, 1>{});
@@ -1041,9 +920,7 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
             step(std::integral_constant<int, 4>{});
             step(std::integral_constant<int, 5>{});
         }
-#if SM_CB_NSV2_AEARLY
         nsv2_bar();   // (pairs with the second wave's last "B1 read")
-#endif
     } else {
         typename L_t::Norm nm;
         int C = L_t::out_slot(0);
@@ -1058,9 +935,7 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
             __builtin_amdgcn_sched_barrier(0);
 #endif
         }
-#if SM_CB_NSV2_AEARLY
         nsv2_bar();   // (pairs with the first wave's "B1(-1) read")
-#endif
         for (int j0 = J0; j0 < nst; j0 += 6 * T) {
             auto step = [&](auto rc) {
                 constexpr int n = decltype(rc)::value;
@@ -1303,25 +1178,14 @@ static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
     // V NORM_SCAN at the reference's cbca_crossL_out (h:266): NsV, else the REUSE2 instantiation
     if constexpr (!HORIZ && MODE == CB_NORM_SCAN) {
         if (nsv_ok(a)) {
-            dim3 grid(a.W * (a.D / 64) * n), block(64);
+            dim3 grid(a.W * (a.D / 64) * n), block(128);   // two waves per line
             const size_t shm = 4 * (size_t)cbca_nsv_smem_words();
-#if SM_CB_NSV2
-            block = dim3(128);
             if (a.view == 0) {
                 if (a.div_safe) hipLaunchKernelGGL((k_cbca_nsv2<false, false>), grid, block, shm, st, a);
                 else hipLaunchKernelGGL((k_cbca_nsv2<false, true>), grid, block, shm, st, a);
             } else {
                 if (a.div_safe) hipLaunchKernelGGL((k_cbca_nsv2<true, false>), grid, block, shm, st, a);
                 else hipLaunchKernelGGL((k_cbca_nsv2<true, true>), grid, block, shm, st, a);
-            }
-            return;
-#endif
-            if (a.view == 0) {
-                if (a.div_safe) hipLaunchKernelGGL((k_cbca_nsv<false, false>), grid, block, shm, st, a);
-                else hipLaunchKernelGGL((k_cbca_nsv<false, true>), grid, block, shm, st, a);
-            } else {
-                if (a.div_safe) hipLaunchKernelGGL((k_cbca_nsv<true, false>), grid, block, shm, st, a);
-                else hipLaunchKernelGGL((k_cbca_nsv<true, true>), grid, block, shm, st, a);
             }
             return;
         }

@@ -510,7 +510,7 @@ __host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (
 static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
 #ifndef SM_CB_NSV_LA
-#define SM_CB_NSV_LA 3   // NsV tiles in flight (same-process A/B, profiles/r5r: 3 8.10-8.12, 4 8.18-8.20, 5 8.11-8.15 ms: issue-bound)
+#define SM_CB_NSV_LA 3   // NsV tiles in flight (same-process A/B of the two-wave sweep, profiles/r5la: 2 7.09-7.14, 3 7.03-7.04, 4 9.79-9.81 ms)
 #endif
 #ifndef SM_CB_RING8_LA
 #define SM_CB_RING8_LA 6   // RING8 tiles in flight (same-process A/B, profiles/r5q: LA 3 5.11-5.18, 4 5.10, 5 5.10, 6 5.02-5.10, 7 5.13 ms)

@@ -509,6 +509,9 @@ struct CbLine {
 __host__ __device__ constexpr int nsv_vmcnt(int n) { return ((n >> 4) << 14) | (0xf << 8) | (0x7 << 4) | (n & 0xf); }
 static_assert(nsv_vmcnt(60) == 0xCF7C, "s_waitcnt encoding");
 constexpr int NSV_LAG = 34;
+#ifndef SM_CB_NSV2_PRIO
+#define SM_CB_NSV2_PRIO 2   // NsV2: s_setprio of the second wave (full res 7.12-7.46 -> 7.05-7.17 ms, Teddy 0.543 -> 0.540, profiles/r5pr)
+#endif
 #ifndef SM_CB_NSV_LA
 #define SM_CB_NSV_LA 3   // NsV tiles in flight (same-process A/B of the two-wave sweep, profiles/r5la: 2 7.09-7.14, 3 7.03-7.04, 4 9.79-9.81 ms)
 #endif
@@ -922,6 +925,9 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
         }
         nsv2_bar();   // (pairs with the second wave's last "B1 read")
     } else {
+#if SM_CB_NSV2_PRIO
+        __builtin_amdgcn_s_setprio(SM_CB_NSV2_PRIO);   // the second wave carries the critical chain
+#endif
         typename L_t::Norm nm;
         int C = L_t::out_slot(0);
         L.template load<false, 2>(tq[0]);

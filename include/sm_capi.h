@@ -211,7 +211,12 @@ SM_API sm_status sm_run_batch_multi(sm_ctx* const* ctxs, int32_t nctx, int32_t n
  * one context (one set of device allocations) time schedules against each other. */
 SM_API sm_status sm_set_schedule(sm_ctx* ctx, int32_t num_streams, int32_t sub_batch);
 SM_API sm_status sm_synchronize(sm_ctx* ctx);
-SM_API void* sm_stream(sm_ctx* ctx);      /* the ctx's hipStream_t */
+SM_API void* sm_stream(sm_ctx* ctx);      /* the ctx's main hipStream_t, joined first: after a
+                                             pipelined sm_run (num_streams 0, the default) the
+                                             call's second group runs on a side stream until the
+                                             next entry point joins it; sm_stream joins it, so work
+                                             ordered after the returned stream sees the whole call.
+                                             NULL on error (sm_last_error) */
 
 /* Per-kernel timing with HIP events on the ctx stream. */
 SM_API sm_status sm_profile_enable(sm_ctx* ctx, int32_t on);

@@ -194,6 +194,10 @@ class DistributedBatchRunner:
                 sizes0 = sub_sizes(per0, cap)
             if len(sizes0) > _MAX_SUB:
                 sizes0 = sub_sizes(per0, -(-per0 // _MAX_SUB))
+            # (after the header-size clamp, which can make blocks larger again)
+            if cap and max(sizes0, default=0) > cap:
+                raise ValueError(f"{per0} pairs per rank need sub-blocks of at most {cap} pairs (the compute "
+                                 f"function's capacity) in at most {_MAX_SUB} blocks: raise the capacity or the world size")
             header = [n, H, W, max_disp, reg_lambda, len(sizes0)] + sizes0 + [0] * (_MAX_SUB - len(sizes0))
         hd = self._bcast_header(header)
         n, H, W, max_disp, reg_lambda, nsub = int(hd[0]), int(hd[1]), int(hd[2]), int(hd[3]), hd[4], int(hd[5])
@@ -295,6 +299,10 @@ class DistributedBatchRunner:
                     if gpu:
                         ev_out[b].record()
 
+        # inputs on rank 0's GPU may have been produced on the caller's stream (decode, augment):
+        # the copy stream that reads them starts after it
+        if gpu and self.rank == 0 and not host_in:
+            self._copy.wait_stream(torch.cuda.current_stream(dev))
         # prologue: stage sub-blocks 0 and 1, post the first scatter
         fut = {0: stage_future(0), 1: stage_future(1)}
         if nsub:

@@ -118,6 +118,7 @@ struct sm_ctx {
     int pipe_g = 0;             // pairs in the first group of the last pipelined sm_run
     hipEvent_t ev_copy2 = nullptr;   // async copy of a pipelined run's second group done (cst)
     bool copy_split = false;    // the pending async copy is two copies (ev_copy: group 0, ev_copy2: group 1)
+    int copy_g = 0;             // with copy_split: pairs [0, copy_g) are ev_copy's, ev_copy2 covers all n
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
     hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
     hipEvent_t ev_run = nullptr, ev_copy = nullptr;     // run done (c->st) / async copy done (cst)
@@ -1486,7 +1487,11 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
         if (s_out) break;
         // the maps are written from here on: an asynchronous copy of the previous run's maps
         // (sm_download_disp_async) must be done reading them
-        if (c->copy_pending && (e = hipStreamWaitEvent(c->st, (c->copy_split && k == 1) ? c->ev_copy2 : c->ev_copy, 0)) != hipSuccess) {
+        // (a split copy: ev_copy covers pairs [0, copy_g) only; a group reaching past them -- the
+        // second group, or any group of a different split or schedule -- waits for ev_copy2,
+        // recorded after both copies)
+        const bool past = c->copy_split && off + m2 > c->copy_g;
+        if (c->copy_pending && (e = hipStreamWaitEvent(c->st, past ? c->ev_copy2 : c->ev_copy, 0)) != hipSuccess) {
             s_out = hip_fail(c, e, "hipStreamWaitEvent (async map copy)");
             break;
         }
@@ -1549,6 +1554,7 @@ sm_status sm_download_disp_async(sm_ctx* c, int32_t n, int16_t* disp_out) {
     HIP_TRY(c, hipEventRecord(c->ev_run, c->st));
     HIP_TRY(c, hipStreamWaitEvent(c->cst, c->ev_run, 0));
     c->copy_split = c->pipe_live && n > c->pipe_g;
+    c->copy_g = c->pipe_g;
     if (c->copy_split) {
         // a pipelined run: the first group's maps once the main stream is there, the second's once
         // the side stream is (waited for, not joined), so that the next run's group k waits for
@@ -1638,7 +1644,12 @@ sm_status sm_synchronize(sm_ctx* c) {
     return SM_OK;
 }
 
-void* sm_stream(sm_ctx* c) { return c ? (void*)c->st : nullptr; }
+// (a pipelined sm_run leaves its second group on a side stream: the main stream is made to wait
+// for it first, so work ordered after the returned stream sees the whole call)
+void* sm_stream(sm_ctx* c) {
+    if (!c || check(c) != SM_OK) return nullptr;
+    return (void*)c->st;
+}
 
 sm_status sm_profile_enable(sm_ctx* c, int32_t on) {
     if (!c) return SM_EINVAL;

@@ -95,6 +95,28 @@ def test_single_process_sub_blocks():
         r.close()
 
 
+def test_capacity_exceeded_is_refused_at_the_header():
+    """More pairs per rank than 32 sub-blocks of the compute function's capacity cannot be
+    scheduled: run() refuses at the header instead of failing inside the compute call; a batch
+    that fits runs as capacity-sized blocks."""
+    from mystereomatching_amd import synthetic as S
+    calls = []
+
+    def fn(block, lam):
+        calls.append(block["lgray"].shape[0])
+        return np.zeros(block["lgray"].shape, np.int16)
+    fn.capacity = 1
+    r = DistributedBatchRunner(fn, sub_batch=0)
+    big = {k: np.zeros((33,) + v.shape[1:], v.dtype) for k, v in S.make_batch(1, H, W, MD + 1).items()}
+    with pytest.raises(ValueError, match="capacity"):
+        r.run(big, max_disp=MD, reg_lambda=0.3)
+    assert calls == []
+    ok = {k: v[:5] for k, v in big.items()}
+    assert r.run(ok, max_disp=MD, reg_lambda=0.3).shape == (5, H, W)
+    assert calls == [1] * 5
+    r.close()
+
+
 def test_sub_sizes():
     from mystereomatching_amd.batch import sub_sizes
     assert [sub_sizes(p) for p in (0, 1, 2, 3, 4, 8, 9, 16)] == \

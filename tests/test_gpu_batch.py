@@ -160,6 +160,75 @@ def test_pipelined_runs(oracle):
         sb.close()
 
 
+def test_pipelined_d256_kernels(oracle):
+    """The bench's timed schedule on the kernels the headline uses: D = 256 with the reference's
+    lag, so the V NORM_SCAN sweep is the two-wave k_cbca_nsv2 and 4-path SGM the checkpointed
+    k_sgm_ck pairs; batch_capacity 16 and num_streams 0, so sm_run pipelines two groups across
+    calls (group 1 left running on the side stream).  Two image sets alternate between calls, so
+    a map overwritten while its asynchronous copy still reads it, or a group reading the other
+    set's inputs, shows up as a wrong map; then n changes between a download_async and the next
+    run (a different group split: the copy-split race of sm_run's map-copy waits), and the one-
+    stream schedule is switched in mid-pipeline.  Every map is compared with the oracle's."""
+    import torch
+    H, W, md, n, cap = 72, 96, 255, 8, 16
+    sets = [S.make_batch(cap, H, W, md + 1, first_index=700 + 40 * s) for s in range(2)]
+    want = [_oracle_maps(oracle, b, H, W, md) for b in sets]
+    sb = StereoBatch(md, H, W, cap, device=0)
+    try:
+        # the kernels this shape reaches (one-stream pass with per-kernel events)
+        sb.upload(*(sets[0][k] for k in KEYS))
+        sb.set_schedule(1, 0)
+        sb.profile(True)
+        sb.profile_reset()
+        sb.n = n
+        np.testing.assert_array_equal(sb.run(0.3), want[0][:n])
+        names = set(sb.profile_read())
+        sb.profile(False)
+        assert {"cbca_v_norm_scan", "sgm_ck_a01", "sgm_ck_b01", "sgm_ck_a23", "sgm_last_wta"} <= names, names
+        sb.set_schedule(0, 0)
+        outs = [torch.full((cap, H, W), -7, dtype=torch.int16, pin_memory=True).numpy() for _ in range(6)]
+        # back-to-back pipelined calls, the image set alternating every call (upload joins)
+        for i in range(6):
+            s = i % 2
+            sb.upload(*(sets[s][k] for k in KEYS))
+            sb.n = n
+            sb.run(0.3, download=False)
+            sb.download_async(outs[i][:n])
+        sb.synchronize()
+        for i in range(6):
+            np.testing.assert_array_equal(outs[i][:n], want[i % 2][:n], err_msg=f"call {i}")
+        # the same set, no upload in between: the steady pipelined state the bench times
+        sb.upload(*(sets[1][k] for k in KEYS))
+        sb.n = n
+        for i in range(4):
+            sb.run(0.3, download=False)
+            sb.download_async(outs[i][:n])
+        sb.synchronize()
+        for i in range(4):
+            np.testing.assert_array_equal(outs[i][:n], want[1][:n], err_msg=f"steady call {i}")
+        # n = 10 (groups 5 + 5), async copy, then n = 16 (groups 8 + 8) on the other set: the new
+        # group 0 writes pairs 5-7, which the previous call's SECOND copy reads
+        sb.upload(*(sets[0][k] for k in KEYS))
+        sb.n = 10
+        sb.run(0.3, download=False)
+        sb.download_async(outs[0][:10])
+        sb.upload(*(sets[1][k] for k in KEYS))
+        sb.n = cap
+        sb.run(0.3, download=False)
+        sb.download_async(outs[1])
+        sb.synchronize()
+        np.testing.assert_array_equal(outs[0][:10], want[0][:10])
+        np.testing.assert_array_equal(outs[1], want[1])
+        # one stream switched in while the pipeline is live, then back
+        sb.run(0.3, download=False)
+        sb.set_schedule(1, 0)
+        np.testing.assert_array_equal(sb.run(0.3), want[1])
+        sb.set_schedule(0, 0)
+        np.testing.assert_array_equal(sb.run(0.3), want[1])
+    finally:
+        sb.close()
+
+
 @pytest.mark.parametrize("n,caps", [(5, (3, 3)), (4, (2, 2, 2)), (1, (1, 1))])
 def test_run_batch_multi_contexts(oracle, n, caps):
     """sm_run_batch_multi over several contexts on device 0 (one host thread each): contiguous

@@ -106,3 +106,37 @@ def test_fuse_norm_scan_matches_oracle_fixture(name):
         sb.close()
     want = z["disp"]
     assert np.array_equal(got, want), _diff_msg(got, want)
+
+
+BENCH_MAPS = sorted(glob.glob(os.path.join(HERE, "golden", "bench_maps_*.npz")))
+
+
+@pytest.mark.parametrize("path", BENCH_MAPS, ids=[os.path.basename(p)[11:-4] for p in BENCH_MAPS])
+def test_bench_batch_default_schedule_every_pair(path):
+    """A bench workload's whole batch (tests/golden/bench_maps_<workload>.npz: the oracle map of
+    every pair, made by make_bench_maps.py) through the schedule bench.py times: the default
+    (num_streams 0: at these sizes two pair groups pipelined across calls), three back-to-back
+    runs with asynchronous map copies into page-locked memory, the last two without anything
+    joining the pipeline in between.  Every pair of every call must equal its oracle map."""
+    import torch
+    z = np.load(path)
+    H, W, md, B, paths = (int(z[k]) for k in ("H", "W", "max_disp", "pairs", "sgm_paths"))
+    batch = S.make_batch(B, H, W, md + 1)
+    for i in range(B):
+        for k in KEYS:
+            got = hashlib.sha256(np.ascontiguousarray(batch[k][i]).tobytes()).hexdigest()
+            assert got == str(z[f"sha_{k}_{i}"]), f"synthetic {k} of pair {i} no longer regenerates the fixture"
+    want = z["disp"]
+    sb = StereoBatch(md, H, W, B, device=0, sgm_paths=paths)
+    try:
+        sb.upload(*(batch[k] for k in KEYS))
+        outs = [torch.full((B, H, W), -9, dtype=torch.int16, pin_memory=True).numpy() for _ in range(3)]
+        for o in outs:
+            sb.run(0.3, download=False)
+            sb.download_async(o)
+        sb.synchronize()
+        for c, o in enumerate(outs):
+            for i in range(B):
+                assert np.array_equal(o[i], want[i]), f"call {c} pair {i}: " + _diff_msg(o[i], want[i])
+    finally:
+        sb.close()

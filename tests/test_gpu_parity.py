@@ -18,7 +18,7 @@ from mystereomatching_amd import synthetic as S
 pytestmark = pytest.mark.gpu
 
 GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
-                if not os.path.basename(p).startswith("large_"))   # large_*: test_gpu_large_fixtures.py
+                if not os.path.basename(p).startswith(("large_", "bench_maps_")))   # those: test_gpu_large_fixtures.py
 
 
 def bits(a):
@@ -512,7 +512,13 @@ def test_fuse_norm_scan_batch_and_right_view(oracle):
 
 @pytest.mark.parametrize("H,W,md,iters,fuse,refine", [
     (200, 90, 63, 2, 1, 0), (200, 90, 63, 1, 1, 0), (160, 150, 127, 3, 1, 0), (150, 120, 63, 4, 1, 0),
-    (130, 110, 63, 4, 0, 0), (90, 140, 191, 2, 1, 1), (70, 75, 255, 2, 0, 1), (40, 300, 63, 2, 1, 0)])
+    (130, 110, 63, 4, 0, 0), (90, 140, 191, 2, 1, 1), (70, 75, 255, 2, 0, 1), (40, 300, 63, 2, 1, 0),
+    # the shipping two-wave V sweep (k_cbca_nsv2, both views through Do_refine) on lines shorter
+    # than 2 lag + T = 75 rows: every tile's arm rows run past the line end into the tail pad
+    # (the round-5 work-in-progress fault), D = 256 and 128, iteration 0 (no
+    # tiny-dividend test) and iteration 2 (with it)
+    (2, 96, 255, 2, 1, 1), (8, 96, 255, 3, 1, 1), (40, 96, 255, 2, 1, 1), (68, 96, 255, 3, 1, 1),
+    (2, 80, 127, 3, 1, 1), (8, 80, 127, 2, 1, 1), (40, 80, 127, 3, 1, 1), (68, 80, 127, 2, 1, 1)])
 def test_fast_sweeps_lag34(oracle, H, W, md, iters, fuse, refine):
     """The dedicated CBCA sweeps at the reference's lag (34) and whole 64-disparity chunks: the V
     NORM_SCAN sweep (NsV: iteration 0 without the tiny-dividend test, later iterations with it)

@@ -142,6 +142,15 @@ typedef struct sm_params {
     int32_t lr_consis;           /* Do_LRConsis = 1 (h:72): "so" optimises both views, DP[1] = so(vm[1])
                                   * (num = Do_LRConsis ? 2 : 1, cpp:1093); 0: "so" builds and optimises
                                   * the left view only */
+    int32_t placement_trials;    /* volume placement (results are identical for every setting): the
+                                  * same kernels run 5-8 % apart on different device allocations of
+                                  * the volumes -- same request counts, more DRAM credit stalls
+                                  * (TCC_EA0_RDREQ_DRAM_CREDIT_STALL) -- so the first
+                                  * sm_run of a context may time its own pipeline on k candidate
+                                  * volume sets held at once and keep the fastest (k - 1 extra sets
+                                  * of memory during that call only; fewer if they do not fit).
+                                  * -1 (default) = 3 with CBCA + SGM and a volume >= 256 MiB per
+                                  * pair, else off; 0 / 1 = off; 2-8 = k */
 } sm_params;
 
 typedef struct sm_ctx sm_ctx;
@@ -210,6 +219,10 @@ SM_API sm_status sm_run_batch_multi(sm_ctx* const* ctxs, int32_t nctx, int32_t n
  * sm_create); applies from the next sm_run.  Results are identical for every schedule; this lets
  * one context (one set of device allocations) time schedules against each other. */
 SM_API sm_status sm_set_schedule(sm_ctx* ctx, int32_t num_streams, int32_t sub_batch);
+/* placement trials of the first sm_run (sm_params.placement_trials): the number of volume sets
+ * timed (0: none ran), their pipeline times in ms (up to max), and the index of the set kept */
+SM_API int32_t sm_placement_trials_ms(sm_ctx* ctx, double* ms, int32_t max);
+SM_API int32_t sm_placement_kept(const sm_ctx* ctx);
 SM_API sm_status sm_synchronize(sm_ctx* ctx);
 SM_API void* sm_stream(sm_ctx* ctx);      /* the ctx's main hipStream_t, joined first: after a
                                              pipelined sm_run (num_streams 0, the default) the

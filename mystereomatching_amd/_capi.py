@@ -42,6 +42,7 @@ class sm_params(C.Structure):
         ("sub_batch", C.c_int32), ("num_streams", C.c_int32), ("fuse_norm_scan", C.c_int32),
         ("gf_eps", C.c_float), ("gf_mode", C.c_int32), ("nl_sigma", C.c_double),
         ("lr_consis", C.c_int32),
+        ("placement_trials", C.c_int32),
     ]
 
 
@@ -73,6 +74,8 @@ SIGNATURES = [
     ("sm_run_batch", C.c_int, [_P, C.c_int32, _P, _P, _P, _P, C.c_float, _P]),
     ("sm_run_batch_multi", C.c_int, [C.POINTER(_P), C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_float, _P]),
     ("sm_set_schedule", C.c_int, [_P, C.c_int32, C.c_int32]),
+    ("sm_placement_trials_ms", C.c_int32, [_P, C.POINTER(C.c_double), C.c_int32]),
+    ("sm_placement_kept", C.c_int32, [_P]),
     ("sm_synchronize", C.c_int, [_P]),
     ("sm_stream", C.c_void_p, [_P]),
     ("sm_profile_enable", C.c_int, [_P, C.c_int32]),

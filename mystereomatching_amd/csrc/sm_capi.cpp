@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <map>
@@ -123,6 +124,9 @@ struct sm_ctx {
     hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
     hipEvent_t ev_run = nullptr, ev_copy = nullptr;     // run done (c->st) / async copy done (cst)
     bool copy_pending = false;  // an async copy may still read the maps
+    int place_trials = 0;       // > 1: the first sm_run chooses among that many volume sets (place_volumes)
+    std::vector<double> place_ms;   // the trials' pipeline times (sm_placement_trials_ms)
+    int place_best = -1;
     std::vector<hipEvent_t> xev;                        // stagger / join events
     hipEvent_t stagger_ev = nullptr;                    // SM_STAGGER_STAGE 1: recorded after the first CBCA sweep
     // profiling
@@ -282,6 +286,7 @@ sm_status validate(const sm_params& p, std::string& why) {
     if (p.batch_capacity < 1) return bad("batch_capacity must be >= 1");
     if (p.sub_batch < 0 || p.num_streams < 0 || p.num_streams > 4) return bad("sub_batch >= 0 and num_streams in [0, 4] required");
     if (p.fuse_norm_scan < -1 || p.fuse_norm_scan > 1) return bad("fuse_norm_scan must be -1 (auto), 0 or 1");
+    if (p.placement_trials < -1 || p.placement_trials > 8) return bad("placement_trials must be in [-1, 8]");
     // The kernels rely on every cost and path cost being >= +0 (SGM and WTA minima compare float
     // bit patterns as unsigned integers, sm_device.h), which these constants guarantee: fusion
     // terms 2 - exp(-C / lam) - exp(-G / lam) with C, G >= 0, truncations >= 0, P1, P2 >= 0.
@@ -990,6 +995,7 @@ void sm_params_default(sm_params* p, int32_t max_disp, int32_t rows, int32_t col
     p->gf_mode = SM_GF_XIMGPROC;  // `//#define MY_GUIDE` (h:38): the shipped build calls ximgproc::guidedFilter
     p->nl_sigma = 0.1;          // NLCCA::aggreCV (NL/NLCCA.cpp:33)
     p->lr_consis = 1;           // Do_LRConsis (h:72)
+    p->placement_trials = -1;   // auto (see sm_capi.h)
 }
 
 const char* sm_status_string(sm_status s) {
@@ -1119,6 +1125,12 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         const double sg = p->nl_sigma < 0.01 ? 0.01 : p->nl_sigma;   // update_table (qx_tree_filter.cpp:23-24)
         for (int i = 0; i < 256; i++) table[i] = exp(-(double)i / (255 * sg));
         HIP_TRY(c, hipMemcpy(c->nl_table, table, 256 * sizeof(double), hipMemcpyHostToDevice));
+    }
+    {
+        const bool plain = p->aggregation == SM_AGG_CBCA && p->cbca_iterations > 0 && p->optimization == SM_OPT_SGM;
+        c->place_trials = p->placement_trials >= 0 ? p->placement_trials
+                                                   : (plain && c->nvol * 4 >= ((size_t)1 << 28) ? 3 : 0);
+        if (!(p->aggregation == SM_AGG_CBCA || p->aggregation == SM_AGG_NONE)) c->place_trials = 0;   // (GF / NL scratch not moved)
     }
     if (getenv("SM_TRACE_ALLOC"))   // diagnostics: where the large buffers landed
         fprintf(stderr, "[alloc] vm0 %p vm1 %p acc %p arms %p code %p gx %p px %p\n", (void*)c->vm0, (void*)c->vm1,
@@ -1417,11 +1429,18 @@ sm_status sm_upload_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8
 #ifndef SM_STAGGER_STAGE
 #define SM_STAGGER_STAGE 1   // 0: CBCA groups also start after the previous group's whole CBCA (A/B)
 #endif
+static sm_status place_volumes(sm_ctx* c, int k, int n, float reg_lambda);
+
 sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     sm_status s = check_nojoin(c);   // (a pipelined run continues from the previous one's streams)
     if (s) return s;
     if (c->stage < 1) return fail(c, SM_ESTATE, "sm_run before images were uploaded");
     if (n < 1 || n > c->n_loaded) return fail(c, SM_EINVAL, "n must be in [1, pairs uploaded]");
+    if (c->place_trials > 1) {   // the first run: choose the volume placement (place_volumes)
+        const int k = c->place_trials;
+        c->place_trials = 0;
+        if ((s = join_all(c)) || (s = place_volumes(c, k, n, reg_lambda))) return s;
+    }
     const float m = 1 + reg_lambda;
     const float w = (float)(1. / (double)m);
     // Sub-batches: all stages of a group of pairs run back to back so that one pass's output is
@@ -1530,6 +1549,75 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
     return SM_OK;
 }
 
+// Volume placement trials (sm_params.placement_trials).  One library, one process: the
+// same kernels on different device allocations of the volumes run 5-8 % apart, stably per
+// allocation -- with identical request counts (TCC_EA0_RDREQ / WRREQ) and no more translation
+// misses (TCP_UTCL1_TRANSLATION_MISS ~1e3 of 4e8 requests), but more DRAM credit stalls
+// (TCC_EA0_RDREQ_DRAM_CREDIT_STALL, TCC_TAG_STALL), i.e. the physical pages' spread over the HBM
+// channels (profiles/r6g).  No allocation flag selects that, so the first sm_run holds k candidate
+// sets of the large volumes at once (distinct pages), times the call's own pipeline on each (one
+// warm-up, then the best of two) and keeps the fastest; the others are freed.  The maps are the
+// same on every set; the trial runs' maps are overwritten by the real run that follows.
+static sm_status place_volumes(sm_ctx* c, int k, int n, float reg_lambda) {
+    float** slot[4] = {&c->vm0, &c->vm1, &c->acc, &c->ck};
+    const size_t vol = (c->cap * c->nvol + c->vtail) * sizeof(float);
+    const size_t bytes[4] = {vol, vol, vol, c->cap * c->ck_pair * sizeof(float)};
+    std::vector<std::array<float*, 4>> sets(1);
+    for (int i = 0; i < 4; i++) sets[0][i] = *slot[i];
+    for (int t = 1; t < k; t++) {
+        std::array<float*, 4> v{};
+        bool ok = true;
+        for (int i = 0; i < 4 && ok; i++)
+            if (sets[0][i] && hipMalloc((void**)&v[i], bytes[i]) != hipSuccess) {
+                v[i] = nullptr;
+                ok = false;
+            }
+        if (!ok) {   // (no room for another set: try the ones held)
+            for (float* q : v)
+                if (q) hipFree(q);
+            (void)hipGetLastError();
+            break;
+        }
+        sets.push_back(v);
+    }
+    if (sets.size() < 2) return SM_OK;
+    const bool prof = c->prof;
+    c->prof = false;
+    sm_status s = SM_OK;
+    size_t best = 0;
+    double best_t = 1e30;
+    c->place_ms.clear();
+    for (size_t i = 0; i < sets.size() && !s; i++) {
+        for (int j = 0; j < 4; j++) *slot[j] = sets[i][j];
+        double tmin = 1e30;
+        for (int r = 0; r < 3 && !s; r++) {   // (r = 0 touches the set's pages first)
+            const auto t0 = std::chrono::steady_clock::now();
+            s = sm_run(c, n, reg_lambda, nullptr);
+            if (!s) s = sm_synchronize(c);
+            const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (r > 0) tmin = std::min(tmin, t);
+        }
+        c->place_ms.push_back(tmin * 1e3);
+        if (tmin < best_t) {
+            best_t = tmin;
+            best = i;
+        }
+    }
+    c->prof = prof;
+    for (size_t i = 0; i < sets.size(); i++)
+        if (i != best)
+            for (float* q : sets[i])
+                if (q) hipFree(q);
+    for (int j = 0; j < 4; j++) *slot[j] = sets[best][j];
+    c->place_best = (int)best;
+    if (getenv("SM_TRACE_ALLOC")) {
+        fprintf(stderr, "[place] %zu volume sets, kept %zu:", sets.size(), best);
+        for (double t : c->place_ms) fprintf(stderr, " %.3f", t);
+        fprintf(stderr, " ms\n");
+    }
+    return s;
+}
+
 sm_status sm_download_disp(sm_ctx* c, int32_t n, int16_t* disp_out) {
     sm_status s = check(c);
     if (s) return s;
@@ -1621,6 +1709,15 @@ sm_status sm_run_batch_multi(sm_ctx* const* ctxs, int32_t nctx, int32_t n, const
         if (st[i] != SM_OK) return st[i];
     return SM_OK;
 }
+
+int32_t sm_placement_trials_ms(sm_ctx* c, double* ms, int32_t max) {
+    if (!c) return -1;
+    const int32_t nt = (int32_t)c->place_ms.size();
+    for (int32_t i = 0; ms && i < nt && i < max; i++) ms[i] = c->place_ms[i];
+    return nt;
+}
+
+int32_t sm_placement_kept(const sm_ctx* c) { return c ? c->place_best : -1; }
 
 sm_status sm_set_schedule(sm_ctx* c, int32_t num_streams, int32_t sub_batch) {
     sm_status s = check(c);

@@ -512,6 +512,13 @@ constexpr int NSV_LAG = 34;
 #ifndef SM_CB_NSV2_PRIO
 #define SM_CB_NSV2_PRIO 2   // NsV2: s_setprio of the second wave (full res 7.12-7.46 -> 7.05-7.17 ms, Teddy 0.543 -> 0.540, profiles/r5pr)
 #endif
+#ifndef SM_CB_NSV2_PIPE
+#define SM_CB_NSV2_PIPE 1   // NsV2's second wave software-pipelined over tiles (cbca_run_nsv2; same-process A/B
+                            // with placement trials, profiles/r6i: 7.10-7.19 -> 6.87-7.09 ms at like placements)
+#endif
+#ifndef SM_CB_NSV2_SPLIT
+#define SM_CB_NSV2_SPLIT 2   // (pipelined) B1 positions read before C(n-1)'s stores: 4 reads each, <= 15 in flight
+#endif
 #ifndef SM_CB_NSV_LA
 #define SM_CB_NSV_LA 3   // NsV tiles in flight (same-process A/B of the two-wave sweep, profiles/r5la: 2 7.09-7.14, 3 7.03-7.04, 4 9.79-9.81 ms)
 #endif
@@ -592,6 +599,7 @@ struct NsV {
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             if (!(MASK & (2 << s))) continue;
+            // (stage C's set 0 lies LAG rows further back: its clamp LAG rows further on)
             const uint32_t rl = min(rld, rld_max);
             const uint32_t roff = s == 0 ? rl - (uint32_t)LAG * rowb : rl;   // rows >= -2 LAG: >= 0
             t.a0[s] = __builtin_amdgcn_raw_buffer_load_b32(A0r[s], (int)aown, (int)roff, 0);
@@ -709,6 +717,40 @@ struct NsV {
         }
     }
 
+    // NsV2 pipelined (SM_CB_NSV2_PIPE): B1's window addresses are formed a tile ahead (they need
+    // only the pass arms and the slot base), so that after the barrier "A(n) written" the reads
+    // issue back to back; the S1 ends go to the saved-address history hh / ht[RT] as in stage_b1
+    struct B1Addr {
+        uint32_t ah[T], at[T];   // the area ring's head / tail addresses
+    };
+    template <int RT>
+    __device__ __forceinline__ void b1_addr(const uint32_t (&pi)[T], int C, B1Addr& ad) {
+        const uint32_t cc = ((uint32_t)(C - 1) & 0xffffu) | ((uint32_t)C << 16);
+        const uint32_t ccr = __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, cc) + __builtin_bit_cast(us2, RR));
+        uint32_t spv[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) spv[k] = slots(pi[k], cc, ccr);
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            hh[RT][k] = mad_u32_u16<1>(spv[k], 256u, o1);
+            ht[RT][k] = mad_u32_u16<0>(spv[k], 256u, o1);
+            ad.ah[k] = mad_u32_u16<1>(spv[k], 128u, oa);
+            ad.at[k] = mad_u32_u16<0>(spv[k], 128u, oa);
+        }
+    }
+    template <int RT, int K0, int K1>
+    __device__ __forceinline__ void b1_read(const B1Addr& ad, Norm& nm) const {
+        typedef __attribute__((address_space(3))) const float lds_f;
+        typedef __attribute__((address_space(3))) const uint16_t lds_h;
+#pragma unroll
+        for (int k = K0; k < K1; k++) {
+            nm.sh[k] = ((lds_f*)(size_t)hh[RT][k])[k * 64];
+            nm.st[k] = ((lds_f*)(size_t)ht[RT][k])[k * 64];
+            nm.ah[k / 2][k % 2] = ((lds_h*)(size_t)ad.ah[k])[k * 64];
+            nm.at[k / 2][k % 2] = ((lds_h*)(size_t)ad.at[k])[k * 64];
+        }
+    }
+
     // stage C reads: the scan outputs at i2 = j - 2 LAG, read at the norm stage's S1 addresses
     // of position j - LAG (tile RT + dt, index q - dt T) plus the ring distance P slots
     template <int RT>
@@ -747,6 +789,18 @@ struct NsV {
                           "+v"(t.a1[0][2]), "+v"(t.a1[0][3]), "+v"(t.a1[0][4]), "+v"(t.a1[0][5]), "+v"(t.a1[0][6]),
                           "+v"(t.a1[1][0]), "+v"(t.a1[1][1]), "+v"(t.a1[1][2]), "+v"(t.a1[1][3]), "+v"(t.a1[1][4]),
                           "+v"(t.a1[1][5]), "+v"(t.a1[1][6]));
+    }
+    // (NsV2 pipelined: each wave waits for its own part of a tile only)
+    __device__ __forceinline__ static void launder_set1(Tile& t) {   // volume rows + set 1 (stage A)
+        static_assert(T == 7, "launder lists a T = 7 tile");
+        asm volatile("" : "+v"(t.x[0]), "+v"(t.x[1]), "+v"(t.x[2]), "+v"(t.x[3]), "+v"(t.x[4]), "+v"(t.x[5]),
+                          "+v"(t.x[6]), "+v"(t.a0[1]), "+v"(t.a1[1][0]), "+v"(t.a1[1][1]), "+v"(t.a1[1][2]),
+                          "+v"(t.a1[1][3]), "+v"(t.a1[1][4]), "+v"(t.a1[1][5]), "+v"(t.a1[1][6]));
+    }
+    __device__ __forceinline__ static void launder_set0(Tile& t) {   // set 0 (B1, C)
+        static_assert(T == 7, "launder lists a T = 7 tile");
+        asm volatile("" : "+v"(t.a0[0]), "+v"(t.a1[0][0]), "+v"(t.a1[0][1]), "+v"(t.a1[0][2]), "+v"(t.a1[0][3]),
+                          "+v"(t.a1[0][4]), "+v"(t.a1[0][5]), "+v"(t.a1[0][6]));
     }
     // T stores that store nothing (out-of-range offsets)
     __device__ __forceinline__ void dummy_stores() const {
@@ -877,6 +931,37 @@ __device__ __forceinline__ void nsv_setup(NsV<RV, CHECK>& L, const CbcaArgs& a, 
 __device__ __forceinline__ void nsv2_bar_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void nsv2_bar() { asm volatile("s_barrier" ::: "memory"); }
 
+// Diagnostic builds only (-DSM_CB_NSV_TRACE=1, tools/nsv_trace.py): per-wave sums of shader-clock
+// cycles spent in each phase of a tile, read back through sm_debug_nsv_trace.  s_memtime is a
+// scalar-memory read whose result waits for lgkmcnt(0), so the phase boundaries sit where the
+// sweep waits for its LDS operations anyway (one exception noted below).
+#ifndef SM_CB_NSV_TRACE
+#define SM_CB_NSV_TRACE 0
+#endif
+#if SM_CB_NSV_TRACE
+constexpr int NSV_TRACE_BLOCKS = 1 << 16, NSV_TRACE_PH = 8;
+__device__ unsigned long long g_nsv_trace[NSV_TRACE_BLOCKS * 2 * NSV_TRACE_PH];
+struct NsvTrace {
+    unsigned long long acc[NSV_TRACE_PH] = {}, t = 0;
+    __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void mark(int ph) {
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        acc[ph] += t2 - t;
+        t = t2;
+    }
+    __device__ __forceinline__ void flush(int blk, int wid, int tiles) {
+        if ((threadIdx.x & 63) == 0 && blk < NSV_TRACE_BLOCKS) {
+            unsigned long long* o = g_nsv_trace + ((size_t)blk * 2 + wid) * NSV_TRACE_PH;
+            for (int i = 0; i < NSV_TRACE_PH - 1; i++) o[i] = acc[i];
+            o[NSV_TRACE_PH - 1] = (unsigned long long)tiles;
+        }
+    }
+};
+#define NSV_TR(x) x
+#else
+#define NSV_TR(x)
+#endif
+
 template <bool RV, bool CHECK>
 __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, float* smem) {
     using L_t = NsV<RV, CHECK>;
@@ -903,18 +988,25 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
             L.template load<false, 5>(tq[k]);
             __builtin_amdgcn_sched_barrier(0);
         }
-        for (int j0 = J0; j0 < nst; j0 += 6 * T) {
+        NSV_TR(NsvTrace tr; tr.start(); int tiles = 0;)
+        const int nst0 = SM_CB_NSV2_PIPE ? nst + T : nst;   // (the pipelined second wave's extra step)
+        for (int j0 = J0; j0 < nst0; j0 += 6 * T) {
             auto step = [&](auto rc) {
                 constexpr int n = decltype(rc)::value;
                 L.template load<false, 5>(tq[(n + LA) % 6]);
-#if SM_CB_NSV_VMWAIT
+#if SM_CB_NSV_VMWAIT && SM_CB_NSV2_PIPE
+                L_t::launder_set1(tq[n]);
+#elif SM_CB_NSV_VMWAIT
                 L_t::launder(tq[n]);
 #endif
                 typename L_t::AVals v;
                 L.stage_a_values(tq[n], v);
+                NSV_TR(tr.mark(0);)   // loads issued, tile n waited for, A(n) values
                 nsv2_bar();        // B1(n - 1) read
+                NSV_TR(tr.mark(1);)   // waiting for B1(n - 1)
                 L.stage_a_write(v);
                 nsv2_bar_lgkm();   // A(n) written
+                NSV_TR(tr.mark(2); tiles++;)   // ring writes + lgkm + barrier
             };
             step(std::integral_constant<int, 0>{});
             step(std::integral_constant<int, 1>{});
@@ -924,9 +1016,71 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
             step(std::integral_constant<int, 5>{});
         }
         nsv2_bar();   // (pairs with the second wave's last "B1 read")
+        NSV_TR(tr.flush(blk, 0, tiles);)
     } else {
 #if SM_CB_NSV2_PRIO
         __builtin_amdgcn_s_setprio(SM_CB_NSV2_PRIO);   // the second wave carries the critical chain
+#endif
+#if SM_CB_NSV2_PIPE
+        // Software-pipelined over tiles: step n = X1(n) | B1(n) reads, first positions | C(n-1)'s
+        // differences and stores (its reads, issued in step n-1, long returned) | B1(n) reads, the
+        // rest | tile n+1's loads and pass intersections | X2(n) | B2(n) | C(n) reads (not waited
+        // for) | B1(n+1)'s addresses.  So B1's LDS latency hides C(n-1)'s stores, C's LDS latency
+        // hides the barrier and B1(n+1)'s issue, and the window X1(n) -> X2(n), in which the first
+        // wave waits, holds only B1's reads.  C(n) of the last tile needs one more step.
+        {
+            typename L_t::Norm nm;
+            typename L_t::B1Addr ad;
+            int C = L_t::out_slot(0);
+            L.jst -= T;   // step 0 stores "C(-1)": rows before the line, out of range
+            L.xst -= (long)T * (long)L.vsb;
+            float s2h[T], s2t[T];
+            uint32_t pi[T];
+#pragma unroll
+            for (int k = 0; k < T; k++) s2h[k] = s2t[k] = 0.f;
+            // (the steady state's vmcnt sequence: T stores, then a tile's loads)
+            L.template load<false, 2>(tq[0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 1; k <= LA; k++) {
+                L.dummy_stores();
+                __builtin_amdgcn_sched_barrier(0);
+                L.template load<false, 2>(tq[k]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            L_t::launder_set0(tq[0]);
+            L.pass_isect(tq[0], pi);
+            L.template b1_addr<0>(pi, C, ad);
+            nsv2_bar();   // (pairs with the first wave's "B1(-1) read")
+            const int nst1 = nst + T;
+            for (int j0 = J0; j0 < nst1; j0 += 6 * T) {
+                auto step = [&](auto rc) {
+                    constexpr int n = decltype(rc)::value;
+                    nsv2_bar();                                       // X1(n): A(n) written
+                    L.template b1_read<n, 0, SM_CB_NSV2_SPLIT>(ad, nm);
+                    __builtin_amdgcn_sched_barrier(0);
+                    L.stage_c_store(s2h, s2t);                        // C(n-1)
+                    __builtin_amdgcn_sched_barrier(0);
+                    L.template b1_read<n, SM_CB_NSV2_SPLIT, T>(ad, nm);
+                    __builtin_amdgcn_sched_barrier(0);
+                    L.template load<false, 2>(tq[(n + LA + 1) % 6]);
+                    L_t::launder_set0(tq[(n + 1) % 6]);
+                    L.pass_isect(tq[(n + 1) % 6], pi);
+                    nsv2_bar_lgkm();                                  // X2(n): B1(n) read
+                    L.stage_b2(nm, C);                                // B2(n)
+                    L.template stage_c_read<n>(s2h, s2t);             // C(n)
+                    C = C + T >= L_t::R ? C + T - L_t::R : C + T;
+                    L.template b1_addr<(n + 1) % 6>(pi, C, ad);       // (tile n + 1)
+                };
+                step(std::integral_constant<int, 0>{});
+                step(std::integral_constant<int, 1>{});
+                step(std::integral_constant<int, 2>{});
+                step(std::integral_constant<int, 3>{});
+                step(std::integral_constant<int, 4>{});
+                step(std::integral_constant<int, 5>{});
+            }
+            return;
+        }
 #endif
         typename L_t::Norm nm;
         int C = L_t::out_slot(0);
@@ -942,6 +1096,7 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
 #endif
         }
         nsv2_bar();   // (pairs with the first wave's "B1(-1) read")
+        NSV_TR(NsvTrace tr; tr.start(); int tiles = 0;)
         for (int j0 = J0; j0 < nst; j0 += 6 * T) {
             auto step = [&](auto rc) {
                 constexpr int n = decltype(rc)::value;
@@ -951,14 +1106,19 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
 #endif
                 uint32_t pi[T];
                 L.pass_isect(tq[n], pi);
+                NSV_TR(tr.mark(0);)   // loads issued, tile n waited for, pass intersections
                 nsv2_bar();                                   // A(n) written
+                NSV_TR(tr.mark(1);)   // waiting for A(n)
                 L.template stage_b1<n>(pi, C, nm);            // B1(n)
                 nsv2_bar_lgkm();                              // B1(n) read
+                NSV_TR(tr.mark(2);)   // B1 issue + LDS latency + barrier
                 L.stage_b2(nm, C);                            // B2(n)
+                NSV_TR(tr.mark(3);)   // B2 (includes its ring writes' completion: the one perturbation)
                 float s2h[T], s2t[T];
                 L.template stage_c_read<n>(s2h, s2t);         // C(n)
                 C = C + T >= L_t::R ? C + T - L_t::R : C + T;
                 L.stage_c_store(s2h, s2t);
+                NSV_TR(tr.mark(4); tiles++;)   // C reads + their latency + stores issued
             };
             step(std::integral_constant<int, 0>{});
             step(std::integral_constant<int, 1>{});
@@ -967,6 +1127,7 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
             step(std::integral_constant<int, 4>{});
             step(std::integral_constant<int, 5>{});
         }
+        NSV_TR(tr.flush(blk, 1, tiles);)
     }
 }
 
@@ -1227,3 +1388,14 @@ void launch_cbca(const CbcaArgs& a, bool horiz, int mode, int n, hipStream_t st)
 }
 
 }  // namespace sm
+
+#if SM_CB_NSV_TRACE
+// diagnostic builds only: [block][wave][phase] cycle sums of the last NsV2 launch (phase 7 = tiles)
+extern "C" __attribute__((visibility("default"))) int sm_debug_nsv_trace(unsigned long long* dst, int nblocks) {
+    if (nblocks > sm::NSV_TRACE_BLOCKS) nblocks = sm::NSV_TRACE_BLOCKS;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(sm::g_nsv_trace), (size_t)nblocks * 2 * sm::NSV_TRACE_PH * 8, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? nblocks : -1;
+}
+#endif
+

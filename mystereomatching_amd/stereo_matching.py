@@ -369,6 +369,13 @@ class StereoBatch:
         _capi.check(self._lib, self._ctx, st, "set_schedule")
         self.params.num_streams, self.params.sub_batch = int(num_streams), int(sub_batch)
 
+    def placement(self):
+        """The first run's volume placement trials (sm_params.placement_trials): (pipeline ms of
+        each candidate set, index of the set kept), or ([], -1) when none ran."""
+        buf = (C.c_double * 8)()
+        nt = self._lib.sm_placement_trials_ms(self._ctx, buf, 8)
+        return [round(buf[i], 3) for i in range(max(0, min(nt, 8)))], int(self._lib.sm_placement_kept(self._ctx))
+
     def synchronize(self):
         _capi.check(self._lib, self._ctx, self._lib.sm_synchronize(self._ctx), "sync")
         self._async_out.clear()

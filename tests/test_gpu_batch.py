@@ -379,3 +379,26 @@ def test_async_map_download_overlaps_next_run(oracle):
             np.testing.assert_array_equal(bufs[1], _oracle_maps(oracle, b, H, W, md), err_msg=f"round {rnd}, batch b")
     finally:
         sb.close()
+
+
+def test_placement_trials_keep_maps(oracle):
+    """sm_params.placement_trials: the first sm_run times its pipeline on k candidate volume sets
+    (held at once) and keeps the fastest; the maps of that and every later run equal the oracle's,
+    the trial times are reported, and contexts without trials report none."""
+    H, W, md, n = 40, 72, 255, 3
+    batch = S.make_batch(n, H, W, md + 1, first_index=760)
+    want = _oracle_maps(oracle, batch, H, W, md)
+    for k in (3, 2, 0):
+        sb = StereoBatch(md, H, W, n, device=0, placement_trials=k)
+        try:
+            sb.upload(*(batch[key] for key in KEYS))
+            np.testing.assert_array_equal(sb.run(0.3), want, err_msg=f"trials {k}, first run")
+            np.testing.assert_array_equal(sb.run(0.3), want, err_msg=f"trials {k}, second run")
+            ms, kept = sb.placement()
+            if k:
+                assert len(ms) == k and 0 <= kept < k and all(t > 0 for t in ms), (ms, kept)
+                assert ms[kept] == min(ms)
+            else:
+                assert (ms, kept) == ([], -1)
+        finally:
+            sb.close()

@@ -236,11 +236,15 @@ struct CbLine {
 
     // Tile loads: positions past the line end read the next line (or 0 past the allocation);
     // their prefix values are never read.
+    // (MASK: bit 0 the volume rows, bit 1 + s arm set s; HN2's waves load their parts)
+    template <int MASK = 0xff>
     __device__ __forceinline__ void load(Tile& t, int j0) const {
         const __amdgpu_buffer_rsrc_t rx = bounded_rsrc(xline + (long)j0 * (long)vsb, xend);
+        if constexpr (MASK & 1) {
 #pragma unroll
         for (int k = 0; k < T; k++)   // normalising sweeps: non-temporal volume loads (v_norm 0.466 -> 0.434 ms)
             t.x[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, (int)xo[k], 0, MODE == CB_SCAN ? SM_LD_AUX : 2));
+        }
         // lane-vector arm loads: positions outside the line read 0 (an out-of-range offset) --
         // for the other image's arms that is the reference's zeroed intersection when u - d < 0.
         // The offset is a select, never a wrapped negative sum: the range check does not wrap,
@@ -248,6 +252,7 @@ struct CbLine {
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
             if (REUSE2 && s == 2) continue;
+            if (!(MASK & (2 << s))) continue;
             const int base = j0 - set_off(s);
             // (only lanes k < T are read back; the others stay off the memory system, which
             // matters for the strided column loads of vertical sweeps)
@@ -453,6 +458,89 @@ struct CbLine {
         }
         if (RC < 0) ws = (ws + T == ring) ? 0 : ws + T;
         wrs = (wrs + T >= cbca_win_ring(T)) ? wrs + T - cbca_win_ring(T) : wrs + T;
+    }
+
+    // ---- HN2: H NORM at the reference's lag as two waves per line (RING8's 8-tile ring cycle) ----
+    // Each wave stages (and reads) only its own arm set's words: set 0 (pass pairs, stage B) on the
+    // second wave, set 1 (perpendicular pairs, the area) on the first; the S1 / area rings are shared.
+    template <int S>
+    __device__ __forceinline__ void stage_set(const Tile& t) {
+        constexpr int R = cbca_win_ring(T);
+        if (lane < T) wown[S * T + lane] = t.a0[S];
+        uint32_t* sp = wspan + S * 2 * R;
+        const int w = wrs + 63 + lane;
+        const int i = w >= R ? w - R : w;
+        if (lane < T) {
+            sp[i] = t.a1w[S];
+            sp[i + R] = t.a1w[S];
+        }
+    }
+    __device__ __forceinline__ void adv_span() {
+        wrs = (wrs + T >= cbca_win_ring(T)) ? wrs + T - cbca_win_ring(T) : wrs + T;
+    }
+    // stage A's register part (first wave): the S1 and area prefixes of the tile's positions
+    __device__ __forceinline__ void hn_a_vals(const Tile& t, float (&s1v)[T], uint16_t (&acv)[T]) {
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            S1 = S1 + t.x[k];
+            s1v[k] = S1;
+            const uint32_t pp = isect(t, 1, k);
+            Acc = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), us2{1, 1}, Acc, false) + 1u;
+            acv[k] = (uint16_t)Acc;
+        }
+    }
+    template <int RC>
+    __device__ __forceinline__ void hn_a_write(const float (&s1v)[T], const uint16_t (&acv)[T]) {
+        float* w1 = r1 + RC * T * 64 + lane;
+        uint16_t* wa = ra + RC * T * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            w1[k * 64] = s1v[k];
+            wa[k * 64] = acv[k];
+        }
+    }
+    // stage B (second wave): the window slot pairs of the tile's outputs i = j - lag ...
+    template <int RC>
+    __device__ __forceinline__ void hn_b_slots(const Tile& t, uint32_t (&sp)[T]) const {
+        constexpr int RINGC = 8 * T;
+        constexpr int si0 = (RC * T - LAGC + 2 * RINGC) % RINGC;
+#pragma unroll
+        for (int k = 0; k < T; k++) sp[k] = slot_pair_c(isect(t, 0, k), (si0 + k) % RINGC);
+    }
+    // ... their S1 / area window reads ...
+    __device__ __forceinline__ void hn_b_read(const uint32_t (&sp)[T], float (&shv)[T], float (&stv)[T],
+                                              uint32_t (&ahv)[T], uint32_t (&atv)[T]) const {
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            shv[k] = ring_at<1, 0>(sp[k]);
+            stv[k] = ring_at<0, 0>(sp[k]);
+            ahv[k] = ring_at<1, 2>(sp[k]);
+            atv[k] = ring_at<0, 2>(sp[k]);
+        }
+    }
+    // ... and genfinalVm_cbca's division (+ SolveAll's scale) and the stores, as in tile()
+    template <bool GUARD>
+    __device__ __forceinline__ void hn_b_finish(int j0, const float (&shv)[T], const float (&stv)[T],
+                                                const uint32_t (&ahv)[T], const uint32_t (&atv)[T]) const {
+        const int i0 = j0 - lag;
+        const __amdgpu_buffer_rsrc_t ob = tile_rsrc(i0);
+        float dv[T], qv[T];
+        uint32_t av[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            dv[k] = shv[k] - stv[k];
+            av[k] = (ahv[k] - atv[k]) & 0xffffu;
+            qv[k] = div_area(dv[k], av[k]);
+        }
+        uint32_t tmin = 0xffffffffu;
+#pragma unroll
+        for (int k = 0; k < T; k++) tmin = min(tmin, __builtin_bit_cast(uint32_t, dv[k]) - 1u);
+        if (__ballot(tmin < 0x087fffffu)) {
+#pragma unroll
+            for (int k = 0; k < T; k++) qv[k] = dv[k] / (float)av[k];
+        }
+#pragma unroll
+        for (int k = 0; k < T; k++) store_tile(ob, k, finish_norm(qv[k]), !GUARD || (unsigned)(i0 + k) < (unsigned)len);
     }
 
     template <int R = 0, int RC = -1>   // R: the tile's slot in the four-tile loop (REUSE2 history)
@@ -1136,12 +1224,14 @@ __global__ __launch_bounds__(128) void k_cbca_nsv2(const CbcaArgs a) {
     extern __shared__ float smem[];
     cbca_run_nsv2<RV, CHECK>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
 }
+// the line's state, zeroed rings and the H sweeps' span-ring prologue; returns the sweep length
+// (both waves of HN2 run it: they write the same values)
 template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int LAGC>
-__device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
-    CbLine<HORIZ, MODE, FULL, SCALE, RV, LAGC> L;
+__device__ __forceinline__ int cbca_line_setup(CbLine<HORIZ, MODE, FULL, SCALE, RV, LAGC>& L, const CbcaArgs& a,
+                                               const int blk, float* smem, const int prologue_sets = 0xff) {
     constexpr int T = CbCfg<HORIZ, MODE>::T;
     constexpr int NSETS = CbCfg<HORIZ, MODE>::NSETS;
-    L.lane = (int)threadIdx.x;
+    L.lane = (int)threadIdx.x & 63;
     const int nchunks = (a.D + 63) / 64;
     const int nlines = HORIZ ? a.H : a.W;
     const int per_pair = nlines * nchunks;
@@ -1194,7 +1284,7 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     L.len = HORIZ ? a.W : a.H;
     L.lag = a.lag;
     L.ring = cbca_ring(a.lag, HORIZ, MODE);
-    if constexpr (decltype(L)::REUSE2) {
+    if constexpr (std::remove_reference_t<decltype(L)>::REUSE2) {
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -1228,6 +1318,7 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
         constexpr int R = cbca_win_ring(T);
 #pragma unroll
         for (int s = 0; s < NSETS; s++) {
+            if (!(prologue_sets & (1 << s))) continue;   // (HN2: each wave its own set's words)
             const int base = -L.set_off(s);
             const int q = (RV ? base + L.c64 : base - L.c64 - 63) + L.lane;
             const uint32_t w = buf_ld_u32(L.A1r[s], (L.lane < 63 && (unsigned)q < (unsigned)L.len) ? (uint32_t)q * 4u : 0x80000000u, 0);
@@ -1237,7 +1328,14 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
             }
         }
     }
-    const int nst = L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
+    return L.len + a.lag * (MODE == CB_NORM_SCAN ? 2 : 1);
+}
+
+template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int LAGC>
+__device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, float* smem) {
+    CbLine<HORIZ, MODE, FULL, SCALE, RV, LAGC> L;
+    constexpr int T = CbCfg<HORIZ, MODE>::T;
+    const int nst = cbca_line_setup(L, a, blk, smem);
     typename CbLine<HORIZ, MODE, FULL, SCALE, RV, LAGC>::Tile ta, tb, tc, td;
     // The loops have no exit but their condition and the prologue's tiles are loaded in order:
     // otherwise the compiler's vmcnt waits at the loop head are conservative and the first tile
@@ -1311,6 +1409,120 @@ __device__ __forceinline__ void cbca_run_line(const CbcaArgs& a, const int blk, 
     }
 }
 
+// HN2: the H normalising sweep at the reference's lag (RING8) as two waves per line sharing the
+// S1 / area rings (a workgroup of 128), the split NsV2 made for the V sweep: the first wave runs
+// stage A (volume rows, perpendicular arm set, S1 and area prefixes, ring writes), the second the
+// pass arm set, the window slot pairs, the ring reads, the division, SolveAll's scale and the
+// stores.  Per tile n two workgroup barriers: X1(n) after A(n)'s ring writes, X2(n) after B(n)'s
+// ring reads (the only reads A(n + 1) can overwrite: 2 lag + T + 1 <= 8 T slots).  The second wave
+// issues tile n + 1's set-0 staging and pass intersections while B(n)'s reads are in flight, and
+// runs B(n)'s division and stores while the first wave writes A(n + 1).
+#ifndef SM_CB_HN2
+#define SM_CB_HN2 1   // H NORM at lag 34 as HN2 (two waves per line; same-process A/B with placement trials,
+                      // profiles/r6/ab_hn2_fullres.txt: 5.00-5.02 -> 4.53-4.55 ms; 0: the one-wave RING8 sweep)
+#endif
+#ifndef SM_CB_HN2_LA
+#define SM_CB_HN2_LA 4   // HN2 tiles in flight (8 buffers; LA 6: 4.54-4.55 ms, 4: 4.53-4.55)
+#endif
+#ifndef SM_CB_HN2_PRIO
+#define SM_CB_HN2_PRIO 2   // s_setprio of the second wave
+#endif
+template <bool FULL, bool SCALE, bool RV>
+__device__ __forceinline__ void cbca_run_hn2(const CbcaArgs& a, const int blk, float* smem) {
+    using L_t = CbLine<true, CB_NORM, FULL, SCALE, RV, 34>;
+    static_assert(L_t::RING8, "HN2 runs the 8-tile ring cycle");
+    constexpr int T = L_t::T;
+    constexpr int LA = SM_CB_HN2_LA;
+    static_assert(LA >= 1 && LA <= 7, "HN2 look-ahead");
+    L_t L;
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int nst = cbca_line_setup(L, a, blk, smem, wid == 0 ? 2 : 1);
+    __syncthreads();   // (both waves' setup writes done)
+    typename L_t::Tile tq[8];
+    const int lag = L.lag;
+    if (wid == 0) {
+#pragma unroll
+        for (int k = 0; k < LA; k++) {
+            L.template load<1 | 4>(tq[k], k * T);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        for (int j0 = 0; j0 < nst; j0 += 8 * T) {
+            auto step = [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                L.template load<1 | 4>(tq[(k + LA) % 8], j0 + (k + LA) * T);
+                L.template stage_set<1>(tq[k]);
+                float s1v[T];
+                uint16_t acv[T];
+                L.hn_a_vals(tq[k], s1v, acv);
+                L.adv_span();
+                nsv2_bar();        // X2(n - 1): B(n - 1) read
+                L.template hn_a_write<k>(s1v, acv);
+                nsv2_bar_lgkm();   // X1(n): A(n) written
+            };
+            step(std::integral_constant<int, 0>{});
+            step(std::integral_constant<int, 1>{});
+            step(std::integral_constant<int, 2>{});
+            step(std::integral_constant<int, 3>{});
+            step(std::integral_constant<int, 4>{});
+            step(std::integral_constant<int, 5>{});
+            step(std::integral_constant<int, 6>{});
+            step(std::integral_constant<int, 7>{});
+        }
+        nsv2_bar();   // (pairs with the second wave's last X2)
+    } else {
+#if SM_CB_HN2_PRIO
+        __builtin_amdgcn_s_setprio(SM_CB_HN2_PRIO);
+#endif
+#pragma unroll
+        for (int k = 0; k < LA; k++) {
+            L.template load<2>(tq[k], k * T);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t sp[T];
+        L.template stage_set<0>(tq[0]);
+        L.template hn_b_slots<0>(tq[0], sp);
+        L.adv_span();
+        nsv2_bar();   // X2(-1)
+        for (int j0 = 0; j0 < nst; j0 += 8 * T) {
+            auto step = [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                nsv2_bar();                                   // X1(n): A(n) written
+                float shv[T], stv[T];
+                uint32_t ahv[T], atv[T];
+                L.hn_b_read(sp, shv, stv, ahv, atv);          // B(n)
+                // tile n + 1: loads LA ahead, its set-0 words and slot pairs (reads in flight with B(n)'s)
+                L.template load<2>(tq[(k + LA) % 8], j0 + (k + LA) * T);
+                L.template stage_set<0>(tq[(k + 1) % 8]);
+                uint32_t sp2[T];
+                L.template hn_b_slots<(k + 1) % 8>(tq[(k + 1) % 8], sp2);
+                L.adv_span();
+                nsv2_bar_lgkm();                              // X2(n): B(n) read
+                const int jt = j0 + k * T;
+                if (jt - lag >= 0 && jt + T - 1 - lag < L.len)
+                    L.template hn_b_finish<false>(jt, shv, stv, ahv, atv);
+                else
+                    L.template hn_b_finish<true>(jt, shv, stv, ahv, atv);
+#pragma unroll
+                for (int q = 0; q < T; q++) sp[q] = sp2[q];
+            };
+            step(std::integral_constant<int, 0>{});
+            step(std::integral_constant<int, 1>{});
+            step(std::integral_constant<int, 2>{});
+            step(std::integral_constant<int, 3>{});
+            step(std::integral_constant<int, 4>{});
+            step(std::integral_constant<int, 5>{});
+            step(std::integral_constant<int, 6>{});
+            step(std::integral_constant<int, 7>{});
+        }
+    }
+}
+
+template <bool FULL, bool SCALE, bool RV>
+__global__ __launch_bounds__(128) void k_cbca_hn2(const CbcaArgs a) {
+    extern __shared__ float smem[];
+    cbca_run_hn2<FULL, SCALE, RV>(a, xcd_swizzle(blockIdx.x, gridDim.x), smem);
+}
+
 template <bool HORIZ, int MODE, bool FULL, bool SCALE, bool RV, int LAGC = 0>
 __global__ __launch_bounds__(64) void k_cbca(const CbcaArgs a) {
     extern __shared__ float smem[];
@@ -1361,6 +1573,19 @@ static void launch_scaled(const CbcaArgs& a, int n, hipStream_t st) {
 #if SM_CB_RING8
     // H NORM at the reference's lag: the compile-time 8-tile ring cycle (CbLine::RING8)
     if constexpr (HORIZ && MODE == CB_NORM) {
+        if (a.lag == 34 && SM_CB_HN2) {   // two waves per line (HN2)
+            dim3 grid(a.H * ((a.D + 63) / 64) * n), block(128);
+            const size_t shm = 4 * (size_t)cbca_smem_words(a.lag, true, CB_NORM);
+            const bool full = a.D % 64 == 0;
+            if (a.view == 0) {
+                if (full) hipLaunchKernelGGL((k_cbca_hn2<true, SCALE, false>), grid, block, shm, st, a);
+                else hipLaunchKernelGGL((k_cbca_hn2<false, SCALE, false>), grid, block, shm, st, a);
+            } else {
+                if (full) hipLaunchKernelGGL((k_cbca_hn2<true, SCALE, true>), grid, block, shm, st, a);
+                else hipLaunchKernelGGL((k_cbca_hn2<false, SCALE, true>), grid, block, shm, st, a);
+            }
+            return;
+        }
         if (a.lag == 34) return launch_lag<HORIZ, MODE, SCALE, 34>(a, n, st);
     }
 #endif

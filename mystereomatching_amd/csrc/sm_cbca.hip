@@ -1141,10 +1141,12 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
             L.template b1_addr<0>(pi, C, ad);
             nsv2_bar();   // (pairs with the first wave's "B1(-1) read")
             const int nst1 = nst + T;
+            NSV_TR(NsvTrace tr; tr.start(); int tiles = 0;)
             for (int j0 = J0; j0 < nst1; j0 += 6 * T) {
                 auto step = [&](auto rc) {
                     constexpr int n = decltype(rc)::value;
                     nsv2_bar();                                       // X1(n): A(n) written
+                    NSV_TR(tr.mark(0);)   // X2(n-1) -> X1(n): B2, C issue, B1 addresses, X1 wait (+ C(n-1) read wait)
                     L.template b1_read<n, 0, SM_CB_NSV2_SPLIT>(ad, nm);
                     __builtin_amdgcn_sched_barrier(0);
                     L.stage_c_store(s2h, s2t);                        // C(n-1)
@@ -1155,6 +1157,7 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
                     L_t::launder_set0(tq[(n + 1) % 6]);
                     L.pass_isect(tq[(n + 1) % 6], pi);
                     nsv2_bar_lgkm();                                  // X2(n): B1(n) read
+                    NSV_TR(tr.mark(1); tiles++;)   // X1(n) -> X2(n): B1 reads, C(n-1) stores, loads, isect, X2
                     L.stage_b2(nm, C);                                // B2(n)
                     L.template stage_c_read<n>(s2h, s2t);             // C(n)
                     C = C + T >= L_t::R ? C + T - L_t::R : C + T;
@@ -1167,6 +1170,7 @@ __device__ __forceinline__ void cbca_run_nsv2(const CbcaArgs& a, const int blk, 
                 step(std::integral_constant<int, 4>{});
                 step(std::integral_constant<int, 5>{});
             }
+            NSV_TR(tr.flush(blk, 1, tiles);)
             return;
         }
 #endif

@@ -18,12 +18,14 @@ sys.path.insert(0, ROOT)
 WAVE0 = ["loads+wait+A values", "wait B1(n-1) read", "A writes+lgkm+barrier"]
 WAVE1 = ["loads+wait+pass isect", "wait A(n) written", "B1 issue+lgkm+barrier", "B2 (+write wait)",
          "C reads+wait+stores"]
+WAVE1_PIPE = ["X2->X1: B2, C issue, addr, X1 wait", "X1->X2: B1 reads, C stores, loads, isect"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "abvar", "libsm_hip_tr.so"))
     ap.add_argument("--workload", default="fullres")
+    ap.add_argument("--pipe", action="store_true", help="the library runs SM_CB_NSV2_PIPE (two marks per tile)")
     a = ap.parse_args()
     os.environ["SM_HIP_LIB"] = a.lib
     import bench
@@ -47,7 +49,7 @@ def main():
     assert got > 0, "sm_debug_nsv_trace failed"
     tiles = buf[:, 1, 7].astype(np.float64)
     print(f"{a.workload}: {nblk} lines, NsV2 {ms:.3f} ms per launch (HIP events), tiles per line {tiles.mean():.1f}")
-    for w, names in ((0, WAVE0), (1, WAVE1)):
+    for w, names in ((0, WAVE0), (1, WAVE1_PIPE if a.pipe else WAVE1)):
         per = buf[:, w, :len(names)].astype(np.float64) / tiles[:, None]
         tot = per.sum(axis=1)
         print(f"wave {w}: {tot.mean():.0f} cycles per tile (p10 {np.percentile(tot, 10):.0f}, p90 {np.percentile(tot, 90):.0f})")
@@ -55,7 +57,7 @@ def main():
             print(f"   {nm:28s} {per[:, i].mean():8.1f}  ({100 * per[:, i].mean() / tot.mean():4.1f} %)")
     # clock calibration: a line's cycles vs the launch time (lines run 3 per CU, 256 CUs)
     rounds = nblk / (3 * 256)
-    line_cycles = (buf[:, 1, :5].astype(np.float64).sum(axis=1)).mean()
+    line_cycles = (buf[:, 1, :(2 if a.pipe else 5)].astype(np.float64).sum(axis=1)).mean()
     print(f"implied clock: {line_cycles * rounds / (ms * 1e-3) / 1e9:.2f} GHz if {rounds:.2f} rounds of 3 lines per CU")
     sb.close()
 

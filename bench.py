@@ -156,6 +156,9 @@ def parse():
     ap.add_argument("--e2e-sub-batch", default="0",
                     help="--e2e: the sub-blocks of a rank's pairs (DistributedBatchRunner sub_batch): s pairs each, "
                          "a comma list of sizes, or 0 = auto (batch.sub_sizes)")
+    ap.add_argument("--e2e-stream", action="store_true",
+                    help="--e2e: time DistributedBatchRunner.run_many over the K batches as one stream (batch k + 1's "
+                         "first scatter overlaps batch k's last sub-block; every batch's maps still end in host memory)")
     ap.add_argument("--e2e-input", choices=["pinned", "numpy"], default="pinned",
                     help="--e2e: rank 0's host batch as page-locked torch tensors (batch.pinned_batch) or numpy "
                          "arrays (staged into page-locked buffers by the runner's copy threads)")
@@ -555,8 +558,12 @@ def run_e2e(args, world, rank, local, dist, backend):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     maps = None
-    for _ in range(args.steps):
-        maps = runner.run(batch, md, 0.3)
+    if args.e2e_stream:   # one stream of K batches (run_many); the last batch's maps are checked
+        maps = runner.run_many([batch] * args.steps if rank == 0 else None, md, 0.3)
+        maps = maps[-1] if maps is not None else None
+    else:
+        for _ in range(args.steps):
+            maps = runner.run(batch, md, 0.3)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
@@ -579,7 +586,10 @@ def run_e2e(args, world, rank, local, dist, backend):
                        "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": n, "sgm_paths": paths,
                        "parallelism": f"dp{world} via DistributedBatchRunner ({backend})", "e2e": True,
                        "e2e_input": args.e2e_input, "sub_blocks": sub_sizes(B, sub),
-                       "timed_region": "rank 0 host batch -> maps in rank 0 host memory"},
+                       "e2e_stream": bool(args.e2e_stream),
+                       "timed_region": ("K batches as one stream (run_many): rank 0 host batches -> maps in rank 0 "
+                                        "host memory" if args.e2e_stream else
+                                        "rank 0 host batch -> maps in rank 0 host memory, one run() per step")},
             "parity": parity,
         }))
     runner.close()

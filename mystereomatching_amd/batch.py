@@ -148,7 +148,7 @@ class DistributedBatchRunner:
         self._staging.clear()
 
     def _bcast_header(self, header: Optional[list]) -> list:
-        t = torch.zeros(6 + _MAX_SUB, dtype=torch.float64, device=self.device)
+        t = torch.zeros(7 + _MAX_SUB, dtype=torch.float64, device=self.device)
         if self.rank == 0:
             t[:] = torch.tensor(header, dtype=torch.float64)
         if self.collective:
@@ -184,9 +184,23 @@ class DistributedBatchRunner:
         """batch (rank 0 only): dict of stacked arrays lbgr/rbgr [n,H,W,3], lgray/rgray [n,H,W]
         (numpy, or torch tensors: page-locked host or on rank 0's GPU).  Returns the [n,H,W]
         int16 maps on rank 0 (numpy; page-locked when the runner is on a GPU), None elsewhere."""
+        out = self.run_many([batch] if self.rank == 0 else None, max_disp, reg_lambda)
+        return out[0] if out is not None else None
+
+    def run_many(self, batches: Optional[list], max_disp: int = 0, reg_lambda: float = 0.3) -> Optional[list]:
+        """A stream of batches of one shape (rank 0 only; every rank calls it once) through one
+        pipeline: the sub-blocks of all batches run back to back, so batch b + 1's first scatter
+        travels while batch b's last sub-block computes and batch b's last gather while batch
+        b + 1 computes -- only the stream's first inputs and last maps stay exposed, not every
+        batch's.  Returns the list of [n,H,W] maps on rank 0, None elsewhere."""
         header = None
         if self.rank == 0:
-            n, H, W = batch["lgray"].shape
+            if not batches:
+                raise ValueError("run_many needs at least one batch")
+            n, H, W = batches[0]["lgray"].shape
+            for bt in batches:
+                if tuple(bt["lgray"].shape) != (n, H, W):
+                    raise ValueError("run_many: every batch of a stream has the same shape")
             _, _, per0 = shard_bounds(n, self.world, 0)
             sizes0 = sub_sizes(per0, self.sub_batch)
             cap = getattr(self.compute_fn, "capacity", None)
@@ -198,19 +212,24 @@ class DistributedBatchRunner:
             if cap and max(sizes0, default=0) > cap:
                 raise ValueError(f"{per0} pairs per rank need sub-blocks of at most {cap} pairs (the compute "
                                  f"function's capacity) in at most {_MAX_SUB} blocks: raise the capacity or the world size")
-            header = [n, H, W, max_disp, reg_lambda, len(sizes0)] + sizes0 + [0] * (_MAX_SUB - len(sizes0))
+            header = [n, H, W, max_disp, reg_lambda, len(sizes0), len(batches)] + sizes0 + [0] * (_MAX_SUB - len(sizes0))
         hd = self._bcast_header(header)
-        n, H, W, max_disp, reg_lambda, nsub = int(hd[0]), int(hd[1]), int(hd[2]), int(hd[3]), hd[4], int(hd[5])
-        sizes = [int(x) for x in hd[6:6 + nsub]]
+        n, H, W, max_disp, reg_lambda, nsub, nb = (int(hd[0]), int(hd[1]), int(hd[2]), int(hd[3]), hd[4], int(hd[5]),
+                                                   int(hd[6]))
+        sizes = [int(x) for x in hd[7:7 + nsub]]
         offs = [sum(sizes[:k]) for k in range(nsub)]
         lo_me, hi_me, per = shard_bounds(n, self.world, self.rank)
         mine = hi_me - lo_me
         smax = max(sizes, default=1)
         dev, gpu, world = self.device, self.gpu, self.world
         pair_b = H * W * 8            # both views' BGR + gray bytes of one pair
-        host_in = self.rank == 0 and not isinstance(batch["lgray"], torch.Tensor)
-        if host_in and self._pool is None:
+        host_in = [self.rank == 0 and not isinstance(bt["lgray"], torch.Tensor) for bt in batches] \
+            if self.rank == 0 else [False] * nb
+        if any(host_in) and self._pool is None:
             self._pool = ThreadPoolExecutor(self.host_threads)
+        # the stream's blocks: (batch, sub-block) in order; block i's buffers alternate by i % 2
+        blocks = [(bi, k) for bi in range(nb) for k in range(nsub)]
+        nblk = len(blocks)
 
         # double-buffered device chunks: recv (every rank), send (rank 0), maps, gathered maps
         recv = [torch.empty(smax * pair_b, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -219,7 +238,7 @@ class DistributedBatchRunner:
         maps = [torch.zeros((smax, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
         gath = [torch.empty((world * smax, H, W), dtype=torch.int16, device=dev) for _ in range(2)] \
             if self.rank == 0 and self.collective else None
-        out = torch.empty((n, H, W), dtype=torch.int16, pin_memory=gpu) if self.rank == 0 else None
+        outs = [torch.empty((n, H, W), dtype=torch.int16, pin_memory=gpu) for _ in range(nb)] if self.rank == 0 else None
         ev_send = [torch.cuda.Event() if gpu else None for _ in range(2)]    # send slot's copy done
         ev_out = [torch.cuda.Event() if gpu else None for _ in range(2)]     # gathered slot copied out
         ev_stage = [torch.cuda.Event() if gpu else None for _ in range(3)]   # staging slot's copy done
@@ -227,13 +246,15 @@ class DistributedBatchRunner:
         gath_work = [None, None]
         staged = {}
 
-        def stage_future(k):
-            """numpy inputs: sub-block k into page-locked staging slot k % 3 (a pool thread)."""
-            if not host_in or k >= nsub:
+        def stage_future(i):
+            """numpy inputs: block i into page-locked staging slot i % 3 (a pool thread)."""
+            if i >= nblk or not host_in[blocks[i][0]]:
                 return None
-            spans, slot = self._spans(n, per, offs[k], sizes[k]), k % 3
-            ev = ev_stage[slot] if k >= 3 else None   # recorded when sub-block k - 3's copy was posted
+            bi, k = blocks[i]
+            spans, slot = self._spans(n, per, offs[k], sizes[k]), i % 3
+            ev = ev_stage[slot] if i >= 3 else None   # recorded when block i - 3's copy was posted
             nbytes = world * smax * pair_b
+            src = batches[bi]
 
             def fill():
                 if ev is not None:
@@ -242,37 +263,40 @@ class DistributedBatchRunner:
                 if buf is None or buf.numel() != nbytes:
                     buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=gpu)
                     self._staging[slot] = buf
-                self._fill(batch, buf, spans, sizes[k], H, W)
+                self._fill(src, buf, spans, sizes[k], H, W)
                 return buf
             return self._pool.submit(fill)
 
-        def post_scatter(k):
-            """Rank 0 fills the send slot of sub-block k on the copy stream; every rank posts the
-            scatter of it into recv[k % 2] (RCCL waits for the copy stream)."""
-            b, size = k % 2, sizes[k]
+        def post_scatter(i):
+            """Rank 0 fills the send slot of block i on the copy stream; every rank posts the
+            scatter of it into recv[i % 2] (RCCL waits for the copy stream)."""
+            bi, k = blocks[i]
+            b, size = i % 2, sizes[k]
             cb = size * pair_b
             with torch.cuda.stream(self._copy) if gpu else _nullctx():
                 if self.rank == 0:
                     if self.collective and scat_work[b] is not None:
-                        scat_work[b].wait()   # the copy stream waits for scatter k - 2 (same slot)
+                        scat_work[b].wait()   # the copy stream waits for scatter i - 2 (same slot)
                     dst = send[b] if self.collective else recv[b]
-                    if host_in:
-                        dst[:world * cb].copy_(staged[k][:world * cb], non_blocking=True)
+                    if host_in[bi]:
+                        dst[:world * cb].copy_(staged[i][:world * cb], non_blocking=True)
                     else:
-                        self._fill(batch, dst, self._spans(n, per, offs[k], size), size, H, W)
+                        self._fill(batches[bi], dst, self._spans(n, per, offs[k], size), size, H, W)
                     if gpu:
                         ev_send[b].record()
-                        if host_in:
-                            ev_stage[k % 3].record()
+                        if host_in[bi]:
+                            ev_stage[i % 3].record()
                 if self.collective:
                     ch = list(send[b][:world * cb].split(cb)) if self.rank == 0 else None
                     scat_work[b] = dist.scatter(recv[b][:cb], ch, src=0, group=self.group, async_op=True)
 
-        def post_gather(k):
-            """Every rank posts the gather of maps[k % 2]; rank 0 copies the valid rows into the
-            page-locked output on the copy stream."""
-            b, size = k % 2, sizes[k]
+        def post_gather(i):
+            """Every rank posts the gather of maps[i % 2]; rank 0 copies the valid rows into the
+            page-locked output of the block's batch on the copy stream."""
+            bi, k = blocks[i]
+            b, size = i % 2, sizes[k]
             spans = self._spans(n, per, offs[k], size)
+            out = outs[bi] if self.rank == 0 else None
             if not self.collective:
                 if self.rank == 0:
                     _, lo, cnt = spans[0]
@@ -284,8 +308,8 @@ class DistributedBatchRunner:
                         if gpu:
                             ev_out[b].record()
                 return
-            if gpu and k >= 2:
-                torch.cuda.current_stream(dev).wait_event(ev_out[b])   # gath[b] of k - 2 copied out
+            if gpu and i >= 2:
+                torch.cuda.current_stream(dev).wait_event(ev_out[b])   # gath[b] of block i - 2 copied out
             raw = maps[b][:size].view(torch.uint8).reshape(-1)   # bytes: gloo has no int16 collectives
             gl = list(gath[b][:world * size].view(torch.uint8).reshape(-1).split(raw.numel())) \
                 if self.rank == 0 else None
@@ -301,23 +325,25 @@ class DistributedBatchRunner:
 
         # inputs on rank 0's GPU may have been produced on the caller's stream (decode, augment):
         # the copy stream that reads them starts after it
-        if gpu and self.rank == 0 and not host_in:
+        if gpu and self.rank == 0 and not all(host_in):
             self._copy.wait_stream(torch.cuda.current_stream(dev))
-        # prologue: stage sub-blocks 0 and 1, post the first scatter
+        # prologue: stage blocks 0 and 1, post the first scatter
         fut = {0: stage_future(0), 1: stage_future(1)}
-        if nsub:
+        if nblk:
             if fut[0] is not None:
                 staged[0] = fut.pop(0).result()
             post_scatter(0)
-        for k in range(nsub):
-            b = k % 2
-            # inputs of sub-block k + 1 on their way while sub-block k computes
-            if k + 1 < nsub:
-                if fut.get(k + 1) is not None:
-                    staged[k + 1] = fut.pop(k + 1).result()
-                post_scatter(k + 1)
-                fut[k + 2] = stage_future(k + 2)
-            staged.pop(k, None)
+        for i in range(nblk):
+            bi, k = blocks[i]
+            b = i % 2
+            # inputs of block i + 1 (the next batch's first sub-block after a batch's last) on
+            # their way while block i computes
+            if i + 1 < nblk:
+                if fut.get(i + 1) is not None:
+                    staged[i + 1] = fut.pop(i + 1).result()
+                post_scatter(i + 1)
+                fut[i + 2] = stage_future(i + 2)
+            staged.pop(i, None)
             if self.collective:
                 scat_work[b].wait()
             elif gpu:
@@ -328,13 +354,13 @@ class DistributedBatchRunner:
                 if not gpu or getattr(self.compute_fn, "device", None) is None:
                     blk = {key: v.cpu().numpy() for key, v in blk.items()}
                 res = self.compute_fn(blk, reg_lambda)
-                if k >= 2:   # maps[b] still read by sub-block k - 2's gather / copy-out
+                if i >= 2:   # maps[b] still read by block i - 2's gather / copy-out
                     if self.collective:
                         gath_work[b].wait()
                     elif gpu:
                         torch.cuda.current_stream(dev).wait_event(ev_out[b])
                 maps[b][:m] = res if isinstance(res, torch.Tensor) else torch.from_numpy(res).to(dev)
-            post_gather(k)
+            post_gather(i)
         if self.collective:
             for w in gath_work:
                 if w is not None:
@@ -344,7 +370,7 @@ class DistributedBatchRunner:
             self._copy.synchronize()
         if self.rank != 0:
             return None
-        return out.numpy()
+        return [o.numpy() for o in outs]
 
 
 class _nullctx:

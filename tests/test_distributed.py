@@ -83,6 +83,41 @@ def test_two_rank_sub_blocks(tmp_path, n, sub_batch, tensor_in):
     np.testing.assert_array_equal(got, ref)
 
 
+def _stream_worker(rank, world, port, n, out_path, sub_batch):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mystereomatching_amd import synthetic as S
+        runner = DistributedBatchRunner(_oracle_fn(), sub_batch=sub_batch)
+        bs = [S.make_batch(n, H, W, MD + 1, first_index=200 + 10 * i) for i in range(3)] if rank == 0 else None
+        got = runner.run_many(bs, max_disp=MD, reg_lambda=0.3)
+        runner.close()
+        if rank == 0:
+            np.save(out_path, np.stack(got))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,sub_batch", [(5, 2), (4, 0), (3, 1)])
+def test_two_rank_stream_of_batches(tmp_path, n, sub_batch):
+    """run_many: three different batches as one stream of sub-blocks (batch b + 1's first scatter
+    while batch b's last block computes); every batch's maps in order, equal to the oracle's."""
+    out = str(tmp_path / "disp.npy")
+    mp.spawn(_stream_worker, args=(2, _free_port(), n, out, sub_batch), nprocs=2, join=True)
+    got = np.load(out)
+    from mystereomatching_amd import synthetic as S
+    for i in range(3):
+        b = S.make_batch(n, H, W, MD + 1, first_index=200 + 10 * i)
+        ref = _oracle_fn()({k: b[k] for k in ("lbgr", "rbgr", "lgray", "rgray")}, 0.3)
+        np.testing.assert_array_equal(got[i], ref, err_msg=f"batch {i}")
+
+
 def test_single_process_sub_blocks():
     """No process group: the runner pipelines rank 0's own sub-blocks (host compute function)."""
     from mystereomatching_amd import synthetic as S
@@ -92,7 +127,16 @@ def test_single_process_sub_blocks():
     for sb in (0, 1, 2, 5):
         r = DistributedBatchRunner(_oracle_fn(), sub_batch=sb)
         np.testing.assert_array_equal(r.run(batch, max_disp=MD, reg_lambda=0.3), ref)
+        # a stream: the same batch twice and a shuffled copy, one pipeline
+        perm = [3, 0, 4, 1, 2]
+        shuf = {k: v[perm] for k, v in batch.items()}
+        got = r.run_many([batch, shuf, batch], max_disp=MD, reg_lambda=0.3)
+        np.testing.assert_array_equal(got[0], ref)
+        np.testing.assert_array_equal(got[1], ref[perm])
+        np.testing.assert_array_equal(got[2], ref)
         r.close()
+    with pytest.raises(ValueError):
+        DistributedBatchRunner(_oracle_fn()).run_many([batch, {k: v[:3] for k, v in batch.items()}], max_disp=MD)
 
 
 def test_capacity_exceeded_is_refused_at_the_header():

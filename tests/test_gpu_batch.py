@@ -53,6 +53,13 @@ def test_runner_single_rank_hip(oracle):
         assert default.device.type == "cuda"
         for _ in range(2):
             np.testing.assert_array_equal(default.run(batch, max_disp=md, reg_lambda=0.3), want)
+        # a stream of batches through one pipeline (run_many), device and host inputs mixed
+        other = S.make_batch(n, H, W, md + 1, first_index=420)
+        want2 = _oracle_maps(oracle, other, H, W, md)
+        dev = {k: torch.from_numpy(np.ascontiguousarray(other[k])).cuda() for k in KEYS}
+        got = DistributedBatchRunner(fn, sub_batch=1).run_many([batch, dev, other, batch], max_disp=md, reg_lambda=0.3)
+        for g, w in zip(got, (want, want2, want2, want)):
+            np.testing.assert_array_equal(g, w)
     finally:
         fn.close()
 

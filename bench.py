@@ -496,8 +496,10 @@ def _e2e_batch(args, world, rank, local, dist, backend, batch, H, W, md, paths, 
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            maps = runner.run(glob, md, 0.3)
+        # the steps as one stream of batches (run_many: each rank's pipeline stays full across
+        # batches; every batch's maps still end in rank 0's host memory)
+        maps = runner.run_many([glob] * steps if rank == 0 else None, md, 0.3)
+        maps = maps[-1] if maps is not None else None
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         dist.barrier()
@@ -514,9 +516,10 @@ def _e2e_batch(args, world, rank, local, dist, backend, batch, H, W, md, paths, 
         runner.close()
         return {"value": round(world * B * H * W * D * steps / el / 1e6, 2), "unit": "Mdisp/s",
                 "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "global_batch": world * B,
-                "path": f"DistributedBatchRunner ({backend}): header broadcast, sub-blocks of pairs staged from "
-                        "page-locked host memory on rank 0 and scattered while the previous sub-block computes, "
-                        "int16 maps gathered to rank 0 host memory while the next one computes",
+                "path": f"DistributedBatchRunner.run_many ({backend}), {steps} batches as one stream: header "
+                        "broadcast, each rank's pairs scattered from page-locked host memory on rank 0 while the "
+                        "previous batch computes, int16 maps gathered to rank 0 host memory while the next one "
+                        "computes",
                 "maps_ok": ok}
     except Exception as e:   # noqa: BLE001 -- reported, not raised
         return {"error": f"{type(e).__name__}: {e}"[:300]}
@@ -585,7 +588,8 @@ def run_e2e(args, world, rank, local, dist, backend):
             "config": {"workload": desc + " -- end to end: broadcast header, scatter pairs, compute, gather maps",
                        "H": H, "W": W, "D": D, "pairs_per_gpu": B, "global_batch": n, "sgm_paths": paths,
                        "parallelism": f"dp{world} via DistributedBatchRunner ({backend})", "e2e": True,
-                       "e2e_input": args.e2e_input, "sub_blocks": sub_sizes(B, sub),
+                       "e2e_input": args.e2e_input,
+                       "sub_blocks": [B] if args.e2e_stream and sub == 0 else sub_sizes(B, sub),
                        "e2e_stream": bool(args.e2e_stream),
                        "timed_region": ("K batches as one stream (run_many): rank 0 host batches -> maps in rank 0 "
                                         "host memory" if args.e2e_stream else

@@ -204,6 +204,16 @@ SM_API sm_status sm_download_disp(sm_ctx* ctx, int32_t n, int16_t* disp_out);
  * run's cost / aggregation work.  disp_out must be page-locked host memory (or device memory) and
  * stays in flight until sm_synchronize. */
 SM_API sm_status sm_download_disp_async(sm_ctx* ctx, int32_t n, int16_t* disp_out);
+/* A pipelined stream of calls without host waits in between (the batch runner's product path):
+ * sm_upload_batch_async queues the copies of the next call's inputs behind the groups of the
+ * previous call that read the same pairs (no join, no host wait; the sources must stay unchanged
+ * until sm_upload_wait returns); sm_download_wait(ctx, back) waits on the host for the copies of
+ * the last (back = 0) or the previous (back = 1) sm_download_disp_async -- neither joins the
+ * pipeline. */
+SM_API sm_status sm_upload_batch_async(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
+                                       const uint8_t* lgray, const uint8_t* rgray);
+SM_API sm_status sm_upload_wait(sm_ctx* ctx);
+SM_API sm_status sm_download_wait(sm_ctx* ctx, int32_t back);
 SM_API sm_status sm_run_batch(sm_ctx* ctx, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr,
                               const uint8_t* lgray, const uint8_t* rgray, float reg_lambda,
                               int16_t* disp_out);

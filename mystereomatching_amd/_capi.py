@@ -71,6 +71,9 @@ SIGNATURES = [
     ("sm_run", C.c_int, [_P, C.c_int32, C.c_float, _P]),
     ("sm_download_disp", C.c_int, [_P, C.c_int32, _P]),
     ("sm_download_disp_async", C.c_int, [_P, C.c_int32, _P]),
+    ("sm_upload_batch_async", C.c_int, [_P, C.c_int32, _P, _P, _P, _P]),
+    ("sm_upload_wait", C.c_int, [_P]),
+    ("sm_download_wait", C.c_int, [_P, C.c_int32]),
     ("sm_run_batch", C.c_int, [_P, C.c_int32, _P, _P, _P, _P, C.c_float, _P]),
     ("sm_run_batch_multi", C.c_int, [C.POINTER(_P), C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_float, _P]),
     ("sm_set_schedule", C.c_int, [_P, C.c_int32, C.c_int32]),

@@ -92,6 +92,19 @@ def hip_compute_fn(max_disp: int, rows: int, cols: int, capacity: int, device: i
             return sb.download(out)
         return sb.download()
 
+    # The asynchronous form (DistributedBatchRunner's GPU path): submit queues the block's upload,
+    # the pipelined run and the maps' copy into `out` without a host wait or a join, so that
+    # consecutive blocks keep the two pair groups running across calls; inputs_done / maps_done
+    # are the host waits that make the runner's buffers reusable (its torch streams and this
+    # library's HIP runtime share device memory, not streams).
+    def submit(block: dict, reg_lambda: float, out):
+        sb.upload_async(block["lbgr"], block["rbgr"], block["lgray"], block["rgray"])
+        sb.run(reg_lambda, download=False)
+        sb.download_async(out)
+
+    run.submit = submit  # type: ignore[attr-defined]
+    run.inputs_done = sb.upload_wait  # type: ignore[attr-defined]
+    run.maps_done = sb.download_wait  # type: ignore[attr-defined]
     run.close = sb.close  # type: ignore[attr-defined]
     # the runner may hand this function device tensors on its own GPU (no host round trip)
     run.device = torch.device("cuda", device)  # type: ignore[attr-defined]
@@ -203,6 +216,11 @@ class DistributedBatchRunner:
                     raise ValueError("run_many: every batch of a stream has the same shape")
             _, _, per0 = shard_bounds(n, self.world, 0)
             sizes0 = sub_sizes(per0, self.sub_batch)
+            if self.sub_batch == 0 and len(batches) > 1 and hasattr(self.compute_fn, "submit"):
+                # a stream through the asynchronous compute form: one block per batch, so that
+                # every call has the same pairs and the library's two pair groups stay pipelined
+                # across calls (the next batch's inputs travel during this batch's compute)
+                sizes0 = [per0] if per0 else []
             cap = getattr(self.compute_fn, "capacity", None)
             if cap and max(sizes0, default=0) > cap:
                 sizes0 = sub_sizes(per0, cap)
@@ -333,6 +351,24 @@ class DistributedBatchRunner:
             if fut[0] is not None:
                 staged[0] = fut.pop(0).result()
             post_scatter(0)
+        # The asynchronous compute form (hip_compute_fn.submit): block i is queued -- upload,
+        # pipelined run, maps copy -- without a host wait, so the library keeps its two pair groups
+        # running across blocks (and batches); block i - 1's maps are gathered once its copy is
+        # done.  The library runs in its own HIP runtime (it shares device memory with torch, not
+        # streams or events), so buffer reuse is ordered by host waits: recv[b] after the upload
+        # that read it (inputs_done), maps[b] after the gather that read it.
+        afn = getattr(self.compute_fn, "submit", None) if gpu else None
+        if afn is not None and torch.device(getattr(self.compute_fn, "device", dev)) != torch.device(dev):
+            afn = None
+        subm = {}   # block -> submission index (async form)
+
+        def finish(j):
+            """async form: block j's maps copied into maps[j % 2] -> post its gather"""
+            if j in subm:
+                back = len(subm) - 1 - subm[j]
+                self.compute_fn.maps_done(back)
+            post_gather(j)
+
         for i in range(nblk):
             bi, k = blocks[i]
             b = i % 2
@@ -341,6 +377,8 @@ class DistributedBatchRunner:
             if i + 1 < nblk:
                 if fut.get(i + 1) is not None:
                     staged[i + 1] = fut.pop(i + 1).result()
+                if afn is not None and (i - 1) in subm:
+                    self.compute_fn.inputs_done()   # recv[(i + 1) % 2] was read by block i - 1's upload
                 post_scatter(i + 1)
                 fut[i + 2] = stage_future(i + 2)
             staged.pop(i, None)
@@ -349,6 +387,24 @@ class DistributedBatchRunner:
             elif gpu:
                 torch.cuda.current_stream(dev).wait_event(ev_send[b])
             m = max(0, min(sizes[k], mine - offs[k]))
+            if afn is not None:
+                if m:
+                    if self.collective:
+                        torch.cuda.current_stream(dev).synchronize()   # recv[b] scattered
+                    else:
+                        ev_send[b].synchronize()
+                    if i >= 2:   # maps[b] read by block i - 2's gather / copy-out
+                        if self.collective:
+                            gath_work[b].wait()
+                            torch.cuda.current_stream(dev).synchronize()
+                        else:
+                            ev_out[b].synchronize()
+                    blk = {key: v[:m] for key, v in _sections(recv[b], sizes[k], H, W).items()}
+                    afn(blk, reg_lambda, maps[b][:m])
+                    subm[i] = len(subm)
+                if i >= 1:
+                    finish(i - 1)
+                continue
             if m:
                 blk = {key: v[:m] for key, v in _sections(recv[b], sizes[k], H, W).items()}
                 if not gpu or getattr(self.compute_fn, "device", None) is None:
@@ -361,6 +417,8 @@ class DistributedBatchRunner:
                         torch.cuda.current_stream(dev).wait_event(ev_out[b])
                 maps[b][:m] = res if isinstance(res, torch.Tensor) else torch.from_numpy(res).to(dev)
             post_gather(i)
+        if afn is not None and nblk:
+            finish(nblk - 1)
         if self.collective:
             for w in gath_work:
                 if w is not None:

@@ -120,6 +120,11 @@ struct sm_ctx {
     hipEvent_t ev_copy2 = nullptr;   // async copy of a pipelined run's second group done (cst)
     bool copy_split = false;    // the pending async copy is two copies (ev_copy: group 0, ev_copy2: group 1)
     int copy_g = 0;             // with copy_split: pairs [0, copy_g) are ev_copy's, ev_copy2 covers all n
+    hipEvent_t ev_dl[2] = {};   // the last two async downloads' copies done (cst), for sm_download_wait
+    int dl_slot = 0;            // ev_dl slot of the next async download
+    int dl_count = 0;
+    hipEvent_t ev_up[2] = {};   // an async upload's copies done: main stream, side stream
+    bool up_split = false;      // the async upload's second group went on the side stream
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
     hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
     hipEvent_t ev_run = nullptr, ev_copy = nullptr;     // run done (c->st) / async copy done (cst)
@@ -396,6 +401,11 @@ void free_all(sm_ctx* c) {
         hipStreamDestroy(c->cst);
         c->cst = nullptr;
     }
+    for (hipEvent_t* ev : {&c->ev_dl[0], &c->ev_dl[1], &c->ev_up[0], &c->ev_up[1]})
+        if (*ev) {
+            hipEventDestroy(*ev);
+            *ev = nullptr;
+        }
     if (c->ev_run) hipEventDestroy(c->ev_run);
     if (c->ev_copy) hipEventDestroy(c->ev_copy);
     if (c->ev_copy2) hipEventDestroy(c->ev_copy2);
@@ -1664,6 +1674,68 @@ sm_status sm_download_disp_async(sm_ctx* c, int32_t n, int16_t* disp_out) {
         HIP_TRY(c, hipEventRecord(c->ev_copy, c->cst));
     }
     c->copy_pending = true;
+    // (one event after both copies on the copy stream: sm_download_wait's per-call marker)
+    if (!c->ev_dl[c->dl_slot]) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_dl[c->dl_slot], hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(c->ev_dl[c->dl_slot], c->cst));
+    c->dl_slot ^= 1;
+    c->dl_count++;
+    return SM_OK;
+}
+
+sm_status sm_download_wait(sm_ctx* c, int32_t back) {
+    sm_status s = check_nojoin(c);   // (the pipeline stays live)
+    if (s) return s;
+    if (back < 0 || back > 1) return fail(c, SM_EINVAL, "back must be 0 (the last async download) or 1 (the one before)");
+    if (c->dl_count <= back) return SM_OK;   // (no such download: nothing to wait for)
+    hipEvent_t e = c->ev_dl[(c->dl_slot + 1 + back) & 1];
+    if (e) HIP_TRY(c, hipEventSynchronize(e));
+    return SM_OK;
+}
+
+// Asynchronous upload for a pipelined stream of calls (DistributedBatchRunner over hip_compute_fn):
+// the copies are queued without joining a live pipeline or waiting on the host -- the next call's
+// first group's pairs on the main stream (after that group's previous call), the second group's on
+// the side stream (after the previous call's second group) -- so a call's inputs arrive while the
+// previous call still runs.  The sources must stay unchanged until sm_upload_wait returns.
+sm_status sm_upload_batch_async(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8_t* rbgr, const uint8_t* lgray,
+                                const uint8_t* rgray) {
+    sm_status s = check_nojoin(c);
+    if (s) return s;
+    if (n < 1 || n > c->cap) return fail(c, SM_EINVAL, "n must be in [1, batch_capacity]");
+    if (!lbgr || !rbgr || !lgray || !rgray) return fail(c, SM_EINVAL, "null image pointer");
+    // the split the next run will keep (sm_run: g = (n + 1) / 2 under the auto schedule); any
+    // other shape joins first, as a synchronous upload does
+    const int g = c->sub_batch > 0 ? c->sub_batch : (c->auto_groups ? (n + 1) / 2 : n);
+    const bool split = c->pipe_live && c->pipelined && g == c->pipe_g && (n + g - 1) / g == 2;
+    if (!split && (s = join_all(c))) return s;
+    for (int i = 0; i < 2; i++)
+        if (!c->ev_up[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_up[i], hipEventDisableTiming));
+    const sm_params& p = c->p;
+    const size_t H = p.rows, W = p.cols, crow = W * 3;
+    for (int view = 0; view < 2; view++) {
+        const uint8_t* src = view == 0 ? lbgr : rbgr;
+        const uint8_t* gsrc = view == 0 ? lgray : rgray;
+        for (int b = 0; b < n; b++) {
+            hipStream_t st = (split && b >= g) ? c->xst[0] : c->st;
+            uint8_t* dst = c->bgr + ((size_t)b * 2 + view) * c->npix * 3;
+            HIP_TRY(c, hipMemcpy2DAsync(dst, crow, src + (size_t)b * H * crow, crow, crow, H, hipMemcpyDefault, st));
+            uint8_t* gdst = c->gray + ((size_t)b * 2 + view) * c->npix;
+            HIP_TRY(c, hipMemcpy2DAsync(gdst, W, gsrc + (size_t)b * H * W, W, W, H, hipMemcpyDefault, st));
+        }
+    }
+    HIP_TRY(c, hipEventRecord(c->ev_up[0], c->st));
+    if (split) HIP_TRY(c, hipEventRecord(c->ev_up[1], c->xst[0]));
+    c->up_split = split;
+    c->n_loaded = n;
+    c->stage = 1;
+    return SM_OK;
+}
+
+sm_status sm_upload_wait(sm_ctx* c) {
+    sm_status s = check_nojoin(c);
+    if (s) return s;
+    if (c->ev_up[0]) HIP_TRY(c, hipEventSynchronize(c->ev_up[0]));
+    if (c->up_split && c->ev_up[1]) HIP_TRY(c, hipEventSynchronize(c->ev_up[1]));
     return SM_OK;
 }
 

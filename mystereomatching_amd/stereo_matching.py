@@ -309,6 +309,32 @@ class StereoBatch:
         _capi.check(self._lib, self._ctx, st, "sm_upload_batch")
         self.n = n
 
+    def upload_async(self, lbgr, rbgr, lgray, rgray):
+        """sm_upload_batch_async: contiguous uint8 device tensors (or page-locked host tensors)
+        copied in behind the previous pipelined call's groups, without a join or a host wait.
+        The sources must stay unchanged until upload_wait() returns."""
+        ts = [a.contiguous() for a in (lbgr, rbgr, lgray, rgray)]
+        import torch
+        if any(t.dtype != torch.uint8 for t in ts):
+            raise TypeError("images must be uint8 tensors")
+        if any(t.data_ptr() != a.data_ptr() for t, a in zip(ts, (lbgr, rbgr, lgray, rgray))):
+            raise ValueError("upload_async needs contiguous tensors (a copy would be freed before the upload)")
+        n = ts[2].shape[0]
+        if tuple(ts[2].shape[1:]) != self.shape[:2] or tuple(ts[0].shape[1:]) != self.shape[:2] + (3,):
+            raise ValueError("upload_async: image shape differs from the context's")
+        st = self._lib.sm_upload_batch_async(self._ctx, n, *[C.c_void_p(t.data_ptr()) for t in ts])
+        _capi.check(self._lib, self._ctx, st, "sm_upload_batch_async")
+        self.n = n
+
+    def upload_wait(self):
+        _capi.check(self._lib, self._ctx, self._lib.sm_upload_wait(self._ctx), "upload_wait")
+
+    def download_wait(self, back: int = 0):
+        """Host wait for the copies of the last (back 0) or previous (back 1) download_async."""
+        _capi.check(self._lib, self._ctx, self._lib.sm_download_wait(self._ctx, int(back)), "download_wait")
+        # (buffers of copies known done are released; the later one may still be in flight)
+        del self._async_out[:max(0, len(self._async_out) - int(back))]
+
     def run(self, reg_lambda: float = 0.3, download: bool = True) -> Optional[np.ndarray]:
         out = np.empty((self.n, self.shape[0], self.shape[1]), np.int16) if download else None
         st = self._lib.sm_run(self._ctx, self.n, float(reg_lambda), _capi.ptr(out) if download else None)

@@ -409,3 +409,38 @@ def test_placement_trials_keep_maps(oracle):
                 assert (ms, kept) == ([], -1)
         finally:
             sb.close()
+
+
+def test_async_upload_stream(oracle):
+    """sm_upload_batch_async + sm_run + sm_download_disp_async back to back, no host wait and no
+    join in between (the batch runner's asynchronous form): the next call's inputs are copied in
+    behind the previous call's pair groups on their own streams.  Two image sets alternate (a copy
+    racing a group that still reads its pairs would mix them), download_wait(1) releases the
+    previous call's maps mid-stream, then a call with fewer pairs (another group split: joined)
+    and a synchronous upload.  Every map equals the oracle's."""
+    import torch
+    H, W, md, n = 72, 96, 255, 8
+    sets = [S.make_batch(n, H, W, md + 1, first_index=840 + 20 * s) for s in range(2)]
+    want = [_oracle_maps(oracle, b, H, W, md) for b in sets]
+    dev = [{k: torch.from_numpy(np.ascontiguousarray(b[k])).cuda() for k in KEYS} for b in sets]
+    torch.cuda.synchronize()
+    sb = StereoBatch(md, H, W, n, device=0)
+    try:
+        outs = [torch.full((n, H, W), -5, dtype=torch.int16, pin_memory=True).numpy() for _ in range(6)]
+        for i in range(6):
+            sb.upload_async(*(dev[i % 2][k] for k in KEYS))
+            sb.run(0.3, download=False)
+            sb.download_async(outs[i])
+            if i >= 1:
+                sb.download_wait(1)
+                np.testing.assert_array_equal(outs[i - 1], want[(i - 1) % 2], err_msg=f"call {i - 1}")
+            sb.upload_wait()
+        sb.download_wait(0)
+        np.testing.assert_array_equal(outs[5], want[1])
+        sub = {k: dev[0][k][:5] for k in KEYS}
+        sb.upload_async(*(sub[k] for k in KEYS))
+        np.testing.assert_array_equal(sb.run(0.3), want[0][:5])
+        sb.upload(*(sets[1][k] for k in KEYS))
+        np.testing.assert_array_equal(sb.run(0.3), want[1])
+    finally:
+        sb.close()

@@ -11,8 +11,9 @@ the resident measurement.
 
 Default workload = BASELINE.json configs[3], the largest single-GPU config and the one north_star's
 targets are quoted on: Middlebury-2014 full resolution 3000x2000, D = 256, censusGrad + CBCA(2) +
-SolveAll + SGM 4-path + WTA, 2 pairs per GPU.  Rank 0's pair 0 map is checked bit-exact against
-the committed oracle fixture of that pair (tests/golden/large_fullres_d256.npz).  Other configs:
+SolveAll + SGM 4-path + WTA, 2 pairs per GPU.  Every map rank 0's timed loop produced is checked
+bit-exact against the committed oracle map of that pair (tests/golden/bench_maps_<workload>.npz),
+and the one-stream per-kernel pass must reproduce them.  Other configs:
 --workload teddy (configs[1], 16 pairs, CPU baseline on whole pairs with map comparison),
 kitti (configs[2]), hd (configs[4] per-GPU shard).  Prints ONE JSON line on rank 0.
 """
@@ -136,7 +137,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP-event timing")
-    ap.add_argument("--no-parity", action="store_true", help="skip the pair-0 fixture comparison (timing probes)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle-map comparison (timing probes)")
     ap.add_argument("--no-d2h", action="store_true",
                     help="leave the maps in HBM at the end of a step (default: every timed step ends with the "
                          "int16 maps in pinned host memory, SURVEY §8d's `disp_out` ready)")

@@ -15,7 +15,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-WAVE0 = ["loads+wait+A values", "wait B1(n-1) read", "A writes+lgkm+barrier"]
+WAVE0 = ["loads+wait+A values (+NsW mailbox)", "wait B1(n-1) read", "A writes+lgkm+barrier"]
 WAVE1 = ["loads+wait+pass isect", "wait A(n) written", "B1 issue+lgkm+barrier", "B2 (+write wait)",
          "C reads+wait+stores"]
 WAVE1_PIPE = ["X2->X1: B2, C issue, addr, X1 wait", "X1->X2: B1 reads, C stores, loads, isect"]

@@ -168,7 +168,7 @@ SM_API sm_status sm_set_images(sm_ctx* ctx, const uint8_t* lbgr, const uint8_t* 
 SM_API sm_status sm_cost_calculate(sm_ctx* ctx);
 SM_API sm_status sm_solve_all(sm_ctx* ctx, int32_t py_lev, float reg_lambda);
 SM_API sm_status sm_disp_optimize(sm_ctx* ctx, int16_t* disp_out);
-/* SolveAll(smPyr, PY_LVL, REG_LAMBDA) over PY_LVL in [1, 3] contexts, one per pyramid level
+/* SolveAll(smPyr, PY_LVL, REG_LAMBDA) over PY_LVL in [1, 8] contexts, one per pyramid level
  * (main_.cpp:131-158): level s has rows (rows_{s-1} + 1) / 2, cols likewise, num_disparities
  * >= num_disparities_{s-1} / 2 + 1, the same pair count and device, and sm_cost_calculate done.
  * levels[0]'s volume(s) receive the cross-scale sum; the coarser levels are only read. */

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <array>
 #include <chrono>
 #include <cmath>
@@ -1219,9 +1220,42 @@ sm_status sm_solve_all(sm_ctx* c, int32_t py_lev, float reg_lambda) {
 }
 
 // invWgt = row 0 of regMat.inv() (cpp:2147-2168): OpenCV's invert for a CV_32F matrix of order
-// n <= 3 evaluates the adjugate over the determinant in double and rounds each entry to float.
+// n <= 3 evaluates the adjugate over the determinant in double and rounds each entry to float;
+// for n > 3 Mat::inv (DECOMP_LU) runs LUImpl<float> on a copy with the identity as right-hand
+// side (lu_inv_row0; OpenCV's scalar loops, each product and sum rounded, pivot failure below
+// 10 * FLT_EPSILON).
+static bool lu_inv_row0(int L, float (*M)[sm::kMaxPyr], float* w) {
+    float B[sm::kMaxPyr][sm::kMaxPyr];
+    for (int i = 0; i < L; i++)
+        for (int j = 0; j < L; j++) B[i][j] = i == j ? 1.f : 0.f;
+    for (int i = 0; i < L; i++) {
+        int k = i;
+        for (int j = i + 1; j < L; j++)
+            if (std::fabs(M[j][i]) > std::fabs(M[k][i])) k = j;
+        if (std::fabs(M[k][i]) < FLT_EPSILON * 10) return false;
+        if (k != i) {
+            for (int j = i; j < L; j++) std::swap(M[i][j], M[k][j]);
+            for (int j = 0; j < L; j++) std::swap(B[i][j], B[k][j]);
+        }
+        const float d = -1 / M[i][i];
+        for (int j = i + 1; j < L; j++) {
+            const float alpha = M[j][i] * d;
+            for (int q = i + 1; q < L; q++) M[j][q] += alpha * M[i][q];
+            for (int q = 0; q < L; q++) B[j][q] += alpha * B[i][q];
+        }
+    }
+    for (int i = L - 1; i >= 0; i--)
+        for (int j = 0; j < L; j++) {
+            float s = B[i][j];
+            for (int q = i + 1; q < L; q++) s -= M[i][q] * B[q][j];
+            B[i][j] = s / M[i][i];
+        }
+    for (int j = 0; j < L; j++) w[j] = B[0][j];
+    return true;
+}
+
 static bool pyr_weights(int L, float lam, float* w) {
-    float M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    float M[sm::kMaxPyr][sm::kMaxPyr] = {};
     for (int s = 0; s < L; s++) {
         if (s == 0) {
             M[s][s] = 1 + lam;
@@ -1235,6 +1269,7 @@ static bool pyr_weights(int L, float lam, float* w) {
             M[s][s + 1] = -lam;
         }
     }
+    if (L > 3) return lu_inv_row0(L, M, w);
     if (L == 1) {
         w[0] = (float)(1. / (double)M[0][0]);
         return true;
@@ -1263,8 +1298,7 @@ sm_status sm_solve_all_pyr(sm_ctx* const* levels, int32_t py_lvl, float reg_lamb
     sm_ctx* c = levels[0];
     sm_status s = check(c);
     if (s) return s;
-    if (py_lvl < 1 || py_lvl > 3)
-        return fail(c, SM_EINVAL, "PY_LVL must be in [1, 3] (OpenCV's closed-form small-matrix invert)");
+    if (py_lvl < 1 || py_lvl > sm::kMaxPyr) return fail(c, SM_EINVAL, "PY_LVL must be in [1, 8]");
     if (py_lvl == 1) return sm_solve_all(c, 1, reg_lambda);
     sm::PyrArgs a{};
     a.levels = py_lvl;

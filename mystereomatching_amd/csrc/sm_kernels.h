@@ -171,10 +171,11 @@ struct SoArgs {                 // scan-line optimisation "so" (sm_so.hip)
     int H, W, D, n, keep_final;
 };
 
+constexpr int kMaxPyr = 8;      // PY_LVL limit (sm_solve_all_pyr)
 struct PyrArgs {                // SolveAll over PY_LVL pyramid levels (sm_pyramid.hip)
-    float* vm[3];               // level s volume [n][H_s][W_s][D_s]; vm[0] is updated in place
-    int H[3], W[3], D[3];
-    float w[3];                 // invWgt[s] = regInv(0, s)
+    float* vm[kMaxPyr];         // level s volume [n][H_s][W_s][D_s]; vm[0] is updated in place
+    int H[kMaxPyr], W[kMaxPyr], D[kMaxPyr];
+    float w[kMaxPyr];           // invWgt[s] = regInv(0, s)
     int levels, n;
 };
 

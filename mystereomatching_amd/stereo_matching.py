@@ -224,7 +224,7 @@ class StereoMatching:
 
 
 def SolveAll(smPyr: Sequence[StereoMatching], PY_LVL: int, REG_LAMBDA: float):
-    """SolveAll (cpp:2142-2208).  PY_LVL = 1 (main_.cpp:131) scales vm; PY_LVL in [2, 3] combines
+    """SolveAll (cpp:2142-2208).  PY_LVL = 1 (main_.cpp:131) scales vm; PY_LVL in [2, 8] combines
     the pyramid levels smPyr[0..PY_LVL-1] (built with pyrDown, main_.cpp:134-156) into smPyr[0]."""
     sm = smPyr[0]
     if int(PY_LVL) == 1:

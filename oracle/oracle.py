@@ -203,9 +203,9 @@ def pyr_down(img: np.ndarray) -> np.ndarray:
 
 
 def pyr_weights(py_lvl: int, reg_lambda: float = 0.3) -> np.ndarray:
-    w = np.zeros(3, np.float32)
+    w = np.zeros(8, np.float32)
     if load().smo_pyr_weights(py_lvl, reg_lambda, _p(w)) != 0:
-        raise ValueError("PY_LVL must be in [1, 3]")
+        raise ValueError("PY_LVL must be in [1, 8]")
     return w[:py_lvl]
 
 

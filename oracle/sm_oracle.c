@@ -892,10 +892,47 @@ void smo_pyr_down_u8(const uint8_t* src, int rows, int cols, int ch, uint8_t* ds
 /* SolveAll's regMat (cpp:2147-2163) and regInv = regMat.inv() (cpp:2164): OpenCV's invert for
  * CV_32F with n <= 3 evaluates the adjugate / determinant in double and rounds each entry to
  * float (n = 1: (float)(1. / a); n = 2: d = 1 / det2, Df(0,j) = (float)(+-S * d); n = 3: the
- * t[0..2] cofactor row times 1 / det3).  invWgt[s] = regInv(0, s) (cpp:2165-2168). */
+ * t[0..2] cofactor row times 1 / det3).  For n > 3 Mat::inv (DECOMP_LU) copies regMat, sets the
+ * destination to the identity and runs hal::LU32f on it: OpenCV's LUImpl<float> (core
+ * matrix_decomp.cpp; OpenCV is not vendored in the reference) — per column the partial pivot
+ * (first row of largest |a|, failure below 10 * FLT_EPSILON), d = -1 / a_ii, every later row
+ * a_jk += (a_ji * d) * a_ik and b_jk += (a_ji * d) * b_ik, then back substitution
+ * b_ij = (b_ij - sum_k a_ik * b_kj) / a_ii; all in float, each product and sum rounded (the
+ * scalar loops; an OpenCV build whose SIMD rows fuse the multiply-add could differ in the last
+ * bit: parity unpinned beyond n = 3).  invWgt[s] = regInv(0, s) (cpp:2165-2168). */
+static int lu_inv_row0(int L, float M[SMO_MAX_PYR][SMO_MAX_PYR], float* w) {
+    float B[SMO_MAX_PYR][SMO_MAX_PYR];
+    for (int i = 0; i < L; i++)
+        for (int j = 0; j < L; j++) B[i][j] = i == j ? 1.f : 0.f;
+    for (int i = 0; i < L; i++) {
+        int k = i;
+        for (int j = i + 1; j < L; j++)
+            if (fabsf(M[j][i]) > fabsf(M[k][i])) k = j;
+        if (fabsf(M[k][i]) < FLT_EPSILON * 10) return -1;
+        if (k != i) {
+            for (int j = i; j < L; j++) { float t = M[i][j]; M[i][j] = M[k][j]; M[k][j] = t; }
+            for (int j = 0; j < L; j++) { float t = B[i][j]; B[i][j] = B[k][j]; B[k][j] = t; }
+        }
+        const float d = -1 / M[i][i];
+        for (int j = i + 1; j < L; j++) {
+            const float alpha = M[j][i] * d;
+            for (int q = i + 1; q < L; q++) M[j][q] += alpha * M[i][q];
+            for (int q = 0; q < L; q++) B[j][q] += alpha * B[i][q];
+        }
+    }
+    for (int i = L - 1; i >= 0; i--)
+        for (int j = 0; j < L; j++) {
+            float s = B[i][j];
+            for (int q = i + 1; q < L; q++) s -= M[i][q] * B[q][j];
+            B[i][j] = s / M[i][i];
+        }
+    for (int j = 0; j < L; j++) w[j] = B[0][j];
+    return 0;
+}
+
 int smo_pyr_weights(int L, float lam, float* w) {
-    if (L < 1 || L > 3) return -1;
-    float M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    if (L < 1 || L > SMO_MAX_PYR) return -1;
+    float M[SMO_MAX_PYR][SMO_MAX_PYR] = {{0}};
     for (int s = 0; s < L; s++) {
         if (s == 0) {
             M[s][s] = 1 + lam;
@@ -909,6 +946,7 @@ int smo_pyr_weights(int L, float lam, float* w) {
             M[s][s + 1] = -lam;
         }
     }
+    if (L > 3) return lu_inv_row0(L, M, w);
     if (L == 1) {
         w[0] = (float)(1. / (double)M[0][0]);
     } else if (L == 2) {
@@ -933,7 +971,7 @@ int smo_pyr_weights(int L, float lam, float* w) {
 /* SolveAll (cpp:2169-2205) for PY_LVL levels, one view: sum += invWgt[s] * vm_s[curY][curX][curD]
  * in level order, then curY /= 2, curX /= 2, curD = (curD + 1) / 2. */
 int smo_solve_all_pyr(const smo_config* cfgs, float* const* vms, int L, float lam) {
-    float w[3];
+    float w[SMO_MAX_PYR];
     if (smo_pyr_weights(L, lam, w)) return -1;
     const smo_config* c0 = &cfgs[0];
     for (int y = 0; y < c0->H; y++)
@@ -957,11 +995,11 @@ int smo_solve_all_pyr(const smo_config* cfgs, float* const* vms, int L, float la
 
 int smo_run_pyr(const smo_config* c0, int L, const uint8_t* bgrL, const uint8_t* bgrR, const uint8_t* grayL,
                 const uint8_t* grayR, int16_t* disp) {
-    if (L < 1 || L > 3 || c0->H < 2 || c0->W < 2) return -1;
-    smo_config cfg[3];
-    uint8_t* img[3][4] = {{NULL}};            /* per level: bgrL, bgrR, grayL, grayR */
-    float* vm[3][2] = {{NULL}};
-    uint16_t* arms[3][2] = {{NULL}};
+    if (L < 1 || L > SMO_MAX_PYR || c0->H < 2 || c0->W < 2) return -1;
+    smo_config cfg[SMO_MAX_PYR];
+    uint8_t* img[SMO_MAX_PYR][4] = {{NULL}};  /* per level: bgrL, bgrR, grayL, grayR */
+    float* vm[SMO_MAX_PYR][2] = {{NULL}};
+    uint16_t* arms[SMO_MAX_PYR][2] = {{NULL}};
     const int views = c0->do_refine ? 2 : 1;
     int rc = -1, maxdisp = c0->D - 1, disSc = 1;
     for (int p = 0; p < L; p++) {
@@ -1004,7 +1042,8 @@ int smo_run_pyr(const smo_config* c0, int L, const uint8_t* bgrL, const uint8_t*
         disSc *= 2;
     }
     for (int v = 0; v < views; v++) {          /* SolveAll(smPsy, PY_LEV, REG_LAMBDA) (main:158) */
-        float* vv[3] = {vm[0][v], vm[1][v], vm[2][v]};
+        float* vv[SMO_MAX_PYR];
+        for (int p = 0; p < L; p++) vv[p] = vm[p][v];
         if (c0->solve_all && smo_solve_all_pyr(cfg, vv, L, c0->reg_lambda)) goto done;
     }
     {
@@ -1028,7 +1067,7 @@ int smo_run_pyr(const smo_config* c0, int L, const uint8_t* bgrL, const uint8_t*
     }
     rc = 0;
 done:
-    for (int p = 0; p < 3; p++) {
+    for (int p = 0; p < SMO_MAX_PYR; p++) {
         for (int k = 0; k < 4; k++) free(img[p][k]);
         for (int v = 0; v < 2; v++) free(vm[p][v]);
         for (int k = 0; k < 2; k++) free(arms[p][k]);

@@ -135,8 +135,10 @@ int smo_run_ex(const smo_config* c, const uint8_t* bgrL, const uint8_t* bgrR,
  * cv::pyrDown for u8 images (BORDER_REFLECT_101): dst is ((rows+1)/2) x ((cols+1)/2),
  * dst = (sum_ij k_i k_j src(2y+i-2, 2x+j-2) + 128) >> 8 with k = {1, 4, 6, 4, 1}. */
 void smo_pyr_down_u8(const uint8_t* src, int rows, int cols, int channels, uint8_t* dst);
+#define SMO_MAX_PYR 8
 /* invWgt[s] = regInv(0, s) of SolveAll's regularisation matrix (cpp:2147-2167), OpenCV's float
- * Mat::inv small-matrix path (n <= 3).  Returns 0, or -1 for PY_LVL outside [1, 3]. */
+ * Mat::inv: the small-matrix path (n <= 3), LUImpl<float> above.  Returns 0, or -1 for PY_LVL
+ * outside [1, SMO_MAX_PYR] or a singular matrix. */
 int smo_pyr_weights(int py_lvl, float reg_lambda, float* w);
 /* SolveAll's cross-scale sum for one view: vms[s] is level s's volume (cfgs[s] its shape);
  * vms[0] receives sum_s invWgt[s] * vm_s(y >> s, x >> s, d_s) with d_s = (d_{s-1} + 1) / 2. */

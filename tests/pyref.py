@@ -449,6 +449,8 @@ def pyr_weights(L, lam=f32(0.3)):
             M[s, s] = f32(1) + f32(f32(2) * lam)
             M[s, s - 1] = -lam
             M[s, s + 1] = -lam
+    if L > 3:
+        return _lu_inv_row0(M)
     m = M.astype(np.float64)
     if L == 1:
         return np.array([f32(1.0 / m[0, 0])], np.float32)
@@ -460,6 +462,39 @@ def pyr_weights(L, lam=f32(0.3)):
     d = 1.0 / det
     return np.array([(m[1, 1] * m[2, 2] - m[1, 2] * m[2, 1]) * d, (m[0, 2] * m[2, 1] - m[0, 1] * m[2, 2]) * d,
                      (m[0, 1] * m[1, 2] - m[0, 2] * m[1, 1]) * d]).astype(np.float32)
+
+
+def _lu_inv_row0(M):
+    """Row 0 of Mat::inv for n > 3 (DECOMP_LU): OpenCV's LUImpl<float> on a copy of M with the
+    identity as right-hand side — partial pivoting, d = -1 / a_ii, row updates, back substitution,
+    every float product and sum rounded on its own."""
+    A = M.copy()
+    n = A.shape[0]
+    B = np.eye(n, dtype=np.float32)
+    for i in range(n):
+        k = i
+        for j in range(i + 1, n):
+            if abs(A[j, i]) > abs(A[k, i]):
+                k = j
+        if abs(A[k, i]) < f32(np.finfo(np.float32).eps * 10):
+            raise ValueError("singular regularisation matrix")
+        if k != i:
+            A[[i, k], i:] = A[[k, i], i:]
+            B[[i, k]] = B[[k, i]]
+        d = f32(f32(-1) / A[i, i])
+        for j in range(i + 1, n):
+            alpha = f32(A[j, i] * d)
+            for q in range(i + 1, n):
+                A[j, q] = f32(A[j, q] + f32(alpha * A[i, q]))
+            for q in range(n):
+                B[j, q] = f32(B[j, q] + f32(alpha * B[i, q]))
+    for i in range(n - 1, -1, -1):
+        for j in range(n):
+            s = B[i, j]
+            for q in range(i + 1, n):
+                s = f32(s - f32(A[i, q] * B[q, j]))
+            B[i, j] = f32(s / A[i, i])
+    return B[0].copy()
 
 
 def solve_all_pyr(vms, lam=f32(0.3)):

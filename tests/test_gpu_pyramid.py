@@ -76,7 +76,8 @@ def run_pyramid(pair, max_disp, L, refine=False):
 
 
 @pytest.mark.parametrize("L,H,W,md,refine", [(2, 60, 83, 23, False), (3, 75, 90, 31, False), (2, 48, 70, 63, True),
-                                             (3, 61, 77, 15, True)])
+                                             (3, 61, 77, 15, True), (4, 75, 90, 31, False), (5, 100, 121, 31, True),
+                                             (8, 300, 260, 63, False)])
 def test_pyramid_pipeline(oracle, L, H, W, md, refine):
     pair = S.make_pair(H, W, md + 1, 300 + L + H)
     cfg = oracle.config(H, W, md, do_refine=int(refine))
@@ -104,4 +105,4 @@ def test_pyramid_validation():
     with pytest.raises(Exception, match="pyrDown"):
         SolveAll([a, b], 2, 0.3)
     with pytest.raises(Exception, match="PY_LVL"):
-        SolveAll([a, b, b, b], 4, 0.3)
+        SolveAll([a] + [b] * 8, 9, 0.3)     # PY_LVL in [1, 8] (sm_capi.h)

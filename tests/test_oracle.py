@@ -172,15 +172,32 @@ def test_pyr_down_constant_and_ramp(oracle):
     np.testing.assert_array_equal(oracle.pyr_down(ramp), pyref.pyr_down(ramp))
 
 
-@pytest.mark.parametrize("L", [1, 2, 3])
+@pytest.mark.parametrize("L", [1, 2, 3, 4, 5, 8])
 @pytest.mark.parametrize("lam", [0.3, 0.1, 1.0])
 def test_pyr_weights(oracle, L, lam):
+    """L <= 3: OpenCV's closed-form invert in double; L > 3: LUImpl<float> (pyref._lu_inv_row0)."""
     np.testing.assert_array_equal(oracle.pyr_weights(L, lam).view(np.uint32), pyref.pyr_weights(L, lam).view(np.uint32))
     if L == 1:
         assert oracle.pyr_weights(1, 0.3).view(np.uint32)[0] == 0x3F44EC4F   # the PY_LVL = 1 weight
 
 
-@pytest.mark.parametrize("L,H,W,md", [(2, 14, 21, 7), (3, 20, 26, 9)])
+def test_pyr_weights_lu_close_to_exact_inverse(oracle):
+    """The float LU row stays within a few float ulps of the float64 inverse (row sums 1)."""
+    for L in range(4, 9):
+        for lam in (0.1, 0.3, 1.0, 4.0):
+            M = np.zeros((L, L))
+            for s in range(L):
+                M[s, s] = 1 + lam if s in (0, L - 1) else 1 + 2 * lam
+                if s:
+                    M[s, s - 1] = -lam
+                if s < L - 1:
+                    M[s, s + 1] = -lam
+            np.testing.assert_allclose(oracle.pyr_weights(L, lam), np.linalg.inv(M)[0], rtol=0, atol=5e-7)
+    with pytest.raises(ValueError):
+        oracle.pyr_weights(9, 0.3)
+
+
+@pytest.mark.parametrize("L,H,W,md", [(2, 14, 21, 7), (3, 20, 26, 9), (4, 34, 40, 15)])
 def test_pyramid_pipeline(oracle, L, H, W, md):
     p = tiny_pair(H, W, md + 1, 31 + L, smooth=True)
     cfg = oracle.config(H, W, md)

@@ -59,8 +59,11 @@ def kernel_symbol(name, D, paths):
     middle SGM paths share one symbol (k_sgm<K, 0, ..>) except the straight vertical ones with
     D % 4 == 0 and D <= 128, which run k_sgm_rows (sm_sgm.hip rows_kv); the right view's SGM
     launches (suffix _r) run the left view's kernels, its CBCA sweeps a separate instantiation.
-    The checkpointed SGM pairs' A passes (sgm_ck_a01, sgm_ck_a23) share one symbol too."""
+    The checkpointed SGM pairs' A passes (sgm_ck_a01, sgm_ck_a23) share one symbol too; the
+    diagonal pair's (sgm_ck_a46, 8 paths) is its own instantiation."""
     base = name[:-2] if name.endswith("_r") else name
+    if base == "sgm_ck_a46":
+        return "k_sgm_ck<A,diag>"
     if base.startswith("sgm_ck_a"):
         return "k_sgm_ck<A>"
     if base.startswith("sgm_path"):

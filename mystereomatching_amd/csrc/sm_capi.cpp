@@ -59,6 +59,7 @@ struct sm_ctx {
     float* acc = nullptr;       // [cap][npix][D]
     float* ck = nullptr;        // [cap][ck_pair]: checkpointed SGM path pairs (k_sgm_ck)
     size_t ck_pair = 0;         // floats per pair: lines x segments x D of the longer direction
+    float* lx = nullptr;        // [cap][npix][D]: L5 between the diagonal pair (8 paths, sgm_ck_diag_ok)
     int16_t* disp = nullptr;    // [cap][npix] DP[0]
     int16_t* disp1 = nullptr;   // [cap][npix] DP[1] (do_refine)
     int16_t* disp_tmp = nullptr;// [cap][npix] refine ping-pong (do_refine)
@@ -367,7 +368,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 }
 
 void free_all(sm_ctx* c) {
-    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->ck, c->disp,
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->ck, c->lx, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
                     c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
                     c->nl_table, c->nl_val, c->nl_oup, c->nl_ofin, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->nl_walk,
@@ -435,6 +436,7 @@ struct Bufs {
     float* vm1;
     float* acc;
     float* ck;
+    float* lx;
     int16_t* disp;
     int16_t* disp1;
     int16_t* disp_tmp;
@@ -458,6 +460,7 @@ Bufs at(const sm_ctx* c, int off) {
     b.vm1 = c->vm1 ? c->vm1 + o * nv : nullptr;
     b.acc = c->acc ? c->acc + o * nv : nullptr;
     b.ck = c->ck ? c->ck + o * c->ck_pair : nullptr;
+    b.lx = c->lx ? c->lx + o * nv : nullptr;
     b.disp = c->disp + o * np;
     b.disp1 = c->disp1 ? c->disp1 + o * np : nullptr;
     b.disp_tmp = c->disp_tmp ? c->disp_tmp + o * np : nullptr;
@@ -821,6 +824,32 @@ sm_status run_optimize(sm_ctx* c, int n, int view, const Bufs& B) {
                 if (s) return s;
             }
             first = 4;
+            if (B.lx) {
+                // 8 paths: the diagonal pair (4, 6) with L5 between them (sm_sgm.hip): pass A of
+                // path 4, path 5 as an SGM_FIRST sweep storing L5, pass B of path 6 reading acc and
+                // L5 (acc = ((acc + L4) + L5) + L6); path 7 follows as the last sweep
+                const double ckd = 4.0 / sm::sgm_ck_diag_seg();
+                a.rv = RV[4];
+                a.ru = RU[4];
+                a.dir = 4;
+                a.dir2 = 6;
+                sm_status s = timed(c, (std::string("sgm_ck_a46") + sfx).c_str(), nv * (4.0 + ckd),
+                                    [&] { sm::launch_sgm_ck(a, sm::CK_A, n, c->st); });
+                if (s) return s;
+                sm::SgmArgs a5 = a;
+                a5.rv = RV[5];
+                a5.ru = RU[5];
+                a5.dir = 5;
+                a5.acc = B.lx;   // SGM_FIRST stores 0 + L5 == L5 (path costs are never -0)
+                s = timed(c, (std::string("sgm_l5") + sfx).c_str(), nv * 8.0,
+                          [&] { sm::launch_sgm_path(a5, sm::SGM_FIRST, n, c->st); });
+                if (s) return s;
+                a.lx = B.lx;
+                s = timed(c, (std::string("sgm_ck_b46") + sfx).c_str(), nv * (16.0 + ckd),
+                          [&] { sm::launch_sgm_ck(a, sm::CK_B | sm::CK_MID | sm::CK_X, n, c->st); });
+                if (s) return s;
+                first = 7;
+            }
         }
         for (int i = first; i < p.sgm_paths; i++) {
             a.rv = RV[i];
@@ -1080,9 +1109,15 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if ((s = dalloc(c, &c->acc, cap * c->nvol + vpad))) return s;
     if (p->optimization == SM_OPT_SGM && sm::sgm_ck_ok(p->num_disparities, p->sgm_paths)) {
         const size_t S = (size_t)sm::sgm_ck_seg(p->num_disparities), H = (size_t)p->rows, W = (size_t)p->cols;
-        const size_t lines_x_segs = std::max(H * ((W + S - 1) / S), W * ((H + S - 1) / S));
+        size_t lines_x_segs = std::max(H * ((W + S - 1) / S), W * ((H + S - 1) / S));
+        const bool diag = sm::sgm_ck_diag_ok(p->num_disparities, p->sgm_paths);
+        if (diag) {   // the diagonal pair: W + H - 1 lines, slots strided by the longest diagonal
+            const size_t SD = (size_t)sm::sgm_ck_diag_seg();
+            lines_x_segs = std::max(lines_x_segs, (W + H - 1) * ((std::min(H, W) + SD - 1) / SD));
+        }
         c->ck_pair = lines_x_segs * (size_t)p->num_disparities;
         if ((s = dalloc(c, &c->ck, cap * c->ck_pair))) return s;
+        if (diag && (s = dalloc(c, &c->lx, cap * c->nvol + vpad))) return s;
     }
     if ((s = dalloc(c, &c->disp, cap * c->npix))) return s;
     if ((s = dalloc(c, &c->dummy, 64))) return s;

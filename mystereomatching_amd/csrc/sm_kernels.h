@@ -84,6 +84,7 @@ struct SgmArgs {
     // checkpointed path pairs (k_sgm_ck): the second path of the pair is the first one reversed
     float* ck;                  // [n][lines][segments][D]: the first path's L at segment ends
     int dir2;                   // direction index of the pair's second path
+    const float* lx;            // CK_X: [n][H][W][D] L of the path between the pair's two (8 paths: L5)
 };
 
 struct GfPix {                  // guided filter, p-independent terms of one pixel (sm_gf.hip)
@@ -190,9 +191,13 @@ void launch_sgm_path(const SgmArgs& a, int mode, int n, hipStream_t st);
 // segment by segment from those checkpoints, and writes L_first + L_second (CK_B), adds both to
 // the running sum (CK_B | CK_MID, 8 paths) or adds them, takes the WTA and writes the map
 // (CK_B | SGM_LAST [| SGM_KEEP]).
-enum { CK_A = 16, CK_B = 32, CK_MID = 64 };
+// CK_B | CK_MID | CK_X (8 paths, the diagonal pair (4, 6)): acc = ((acc + L4) + L5) + L6 with L5
+// read from SgmArgs::lx (a path-5 sweep in SGM_FIRST mode stored it there).
+enum { CK_A = 16, CK_B = 32, CK_MID = 64, CK_X = 128 };
 bool sgm_ck_ok(int D, int paths);
 int sgm_ck_seg(int D);
+bool sgm_ck_diag_ok(int D, int paths);   // 8 paths: the diagonal pair (4, 6) checkpointed as well
+int sgm_ck_diag_seg();
 void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st);
 void launch_wta(const float* vm, int16_t* disp, int n, int H, int W, int D, hipStream_t st);
 void launch_expf_range(uint32_t first, uint32_t n, float* out, hipStream_t st);

@@ -623,6 +623,13 @@ static int rows_kv(const SgmArgs& a, int mode) {
 // Layouts: D in (128, 256]: k_sgm<4, ..., VEC>'s, one line per wave, four consecutive
 // disparities per lane (dwordx4); D <= 128: k_sgm_rows's, four lines per wave, a DPP row of 16
 // lanes per line, 4 KV disparities per lane.  D % 4 == 0 throughout.
+// Diagonal pair (8 paths, one line per wave): paths 4 and 6 walk the anti-diagonals both ways,
+// but the sum puts L5 between them: (((acc + L4) + L5) + L6) + L7.  Path 5 (the other diagonal
+// family) therefore runs as an SGM_FIRST sweep that stores L5 itself (4 + 4 B), pass A walks path
+// 4 (4 B), pass B walks path 6 with L4 recomputed and reads acc and L5 (16 B), and the last path
+// stays a sweep (8 B): 32 B + checkpoints instead of the three sweeps' 12 + 12 + 12 + 8.  Lines
+// are k_sgm's diagonals of the first path (W + H - 1 of them, 1 .. min(H, W) steps; checkpoint
+// slots strided by the longest), segments of SM_SGM_CK_SD steps.
 // ---------------------------------------------------------------------------------------
 #ifndef SM_SGM_CK
 #define SM_SGM_CK 1
@@ -634,9 +641,18 @@ static int rows_kv(const SgmArgs& a, int mode) {
 #define SM_SGM_CK_S2 4       // segment steps with 8 disparities per lane (D in (64, 128])
 #endif
 
+#ifndef SM_SGM_CK_DIAG
+#define SM_SGM_CK_DIAG 1     // 8 paths, 128 < D <= 256: the diagonal pair (4, 6) checkpointed too
+#endif
+#ifndef SM_SGM_CK_SD
+#define SM_SGM_CK_SD 4       // segment steps of the diagonal pair (its pass B also holds L5's segment)
+#endif
+
 bool sgm_ck_ok(int D, int paths) { return SM_SGM_CK && (paths == 4 || paths == 8) && D <= 256 && D % 4 == 0; }
 static int ck_kv(int D) { return D > SM_SGM_VEC_MIN_D ? 0 : ((D + 15) / 16 + 3) / 4; }   // 0: one line per wave
 int sgm_ck_seg(int D) { return ck_kv(D) == 2 ? SM_SGM_CK_S2 : SM_SGM_CK_S; }
+bool sgm_ck_diag_ok(int D, int paths) { return SM_SGM_CK_DIAG && paths == 8 && sgm_ck_ok(D, paths) && ck_kv(D) == 0; }
+int sgm_ck_diag_seg() { return SM_SGM_CK_SD; }
 
 template <int KV, bool ROWS, bool FULL, bool SG>
 struct CkStep {
@@ -691,12 +707,13 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
     constexpr bool SG = (MODE & SGM_SIGNED) != 0;
     constexpr bool LAST = (MODE & SGM_LAST) != 0;
     constexpr bool ACC_IN = LAST || (MODE & CK_MID) != 0;
+    constexpr bool LX = (MODE & CK_X) != 0;   // L5 between the pair's paths (diagonal pair)
     const int lane = threadIdx.x & 63;
     const int row = ROWS ? lane >> 4 : 0, ll = ROWS ? lane & 15 : lane;
     const int H = a.H, W = a.W, D = a.D;
-    const bool horiz = a.rv == 0;             // straight directions only
-    const int nl = horiz ? H : W;
-    const int steps = horiz ? W : H;
+    const bool diag = !ROWS && a.rv != 0 && a.ru != 0;   // the diagonal pair: one line per wave only
+    const bool horiz = a.rv == 0;
+    const int nl = diag ? W + H - 1 : (horiz ? H : W);
     const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256 + threadIdx.x) >> 6));
     int b, line;
     bool line_ok;
@@ -713,8 +730,22 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
         line = wave;
         line_ok = true;
     }
-    const int v0 = horiz ? line : (a.rv > 0 ? H - 1 : 0);
-    const int u0 = horiz ? (a.ru > 0 ? W - 1 : 0) : line;
+    int v0, u0, steps;
+    if (!diag) {
+        v0 = horiz ? line : (a.rv > 0 ? H - 1 : 0);
+        u0 = horiz ? (a.ru > 0 ? W - 1 : 0) : line;
+        steps = horiz ? W : H;
+    } else {   // k_sgm's diagonal lines of the first path: W from the edge row, then H - 1 from the edge column
+        if (line < W) {
+            v0 = a.rv > 0 ? H - 1 : 0;
+            u0 = line;
+        } else {
+            const int k = line - W;
+            v0 = a.rv > 0 ? k : k + 1;
+            u0 = a.ru > 0 ? W - 1 : 0;
+        }
+        steps = min(a.rv > 0 ? v0 + 1 : H - v0, a.ru > 0 ? u0 + 1 : W - u0);
+    }
     const int pstep = -a.rv * W - a.ru;       // pixel delta per step of the pair's FIRST path
     const size_t npix = (size_t)H * W;
     const size_t p0 = (size_t)v0 * W + u0;
@@ -738,7 +769,9 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
     const uint8_t* flbase = a.flags + (size_t)b * npix + p0;
     int16_t* dbase = a.disp + (size_t)b * npix + p0;
     const int nseg = (steps + S - 1) / S;     // segments of the line (= its checkpoint slots)
-    float* ckl = a.ck + ((size_t)b * nl + line) * (size_t)nseg * D;
+    const int nslot = diag ? (min(H, W) + S - 1) / S : nseg;   // slot stride per line
+    float* ckl = a.ck + ((size_t)b * nl + line) * (size_t)nslot * D;
+    const float* xld = LX ? a.lx + ((size_t)b * npix + p0) * D : nullptr;
     const int dirA = a.dir, dirB = a.dir2;
     auto clampj = [&](int j) { return j < 0 ? 0 : (j >= steps ? steps - 1 : j); };
     auto pen = [&](uint32_t fl, int s, int dir) {
@@ -814,6 +847,7 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
         struct Sg {
             float c[S][K];
             float acc[ACC_IN ? S : 1][K];   // the running sum (pair (2, 3))
+            float lx[LX ? S : 1][K];        // L5 (diagonal pair)
             float ck[K];                    // the first path's L at step aj0 - 1
             uint32_t fl;
         };
@@ -824,6 +858,7 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
                 const long off = (long)clampj(aj0 + s) * vstep;
                 ldK(g.c[s], cld, off);
                 if (ACC_IN) ldK(g.acc[s], ald, off);
+                if (LX) ldK(g.lx[s], xld, off);
             }
             ldK(g.ck, ckl, (long)(k < nseg - 1 ? k : 0) * D);
             // chunks past D: checkpoints are only stored inside D, and those lanes must hold
@@ -839,7 +874,8 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
         auto emit = [&](const Sg& g, int s, int j, const float (&LA)[K], const float (&LB)[K]) {
             float f[K];
 #pragma unroll
-            for (int q = 0; q < K; q++) f[q] = ACC_IN ? (g.acc[s][q] + LA[q]) + LB[q] : LA[q] + LB[q];
+            for (int q = 0; q < K; q++)
+                f[q] = LX ? ((g.acc[s][q] + LA[q]) + g.lx[s][q]) + LB[q] : (ACC_IN ? (g.acc[s][q] + LA[q]) + LB[q] : LA[q] + LB[q]);
             if (!LAST) {
                 stK(ast, (long)j * vstep, f);
                 return;
@@ -920,7 +956,7 @@ __global__ __launch_bounds__(256) void k_sgm_ck(const SgmArgs a) {
 
 template <int S, int MODE, int KV, bool ROWS, bool FULL>
 static void launch_ck_one(const SgmArgs& a, hipStream_t st) {
-    const int nl = a.rv == 0 ? a.H : a.W;
+    const int nl = (a.rv != 0 && a.ru != 0) ? a.W + a.H - 1 : (a.rv == 0 ? a.H : a.W);
     if (ROWS) {
         const int waves = (nl + 3) / 4 * a.n;
         hipLaunchKernelGGL((k_sgm_ck<S, MODE, KV, ROWS, FULL>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
@@ -934,6 +970,9 @@ static void launch_ck_f(const SgmArgs& a, int mode, hipStream_t st) {
         case CK_A: return launch_ck_one<S, SGN | CK_A, KV, ROWS, FULL>(a, st);
         case CK_B: return launch_ck_one<S, SGN | CK_B, KV, ROWS, FULL>(a, st);
         case CK_B | CK_MID: return launch_ck_one<S, SGN | CK_B | CK_MID, KV, ROWS, FULL>(a, st);
+        case CK_B | CK_MID | CK_X:
+            if constexpr (!ROWS) return launch_ck_one<S, SGN | CK_B | CK_MID | CK_X, KV, ROWS, FULL>(a, st);
+            return;
         case CK_B | SGM_LAST: return launch_ck_one<S, SGN | CK_B | SGM_LAST, KV, ROWS, FULL>(a, st);
         default: return launch_ck_one<S, SGN | CK_B | SGM_LAST | SGM_KEEP, KV, ROWS, FULL>(a, st);
     }
@@ -951,6 +990,10 @@ void launch_sgm_ck(const SgmArgs& a, int mode, int n, hipStream_t st) {
     SgmArgs b = a;
     b.n = n;
     if ((mode & SGM_LAST) && a.keep_final) mode |= SGM_KEEP;
+    if (a.rv != 0 && a.ru != 0) {   // the diagonal pair (sgm_ck_diag_ok: one line per wave)
+        if (a.D == 256) return launch_ck_s<SM_SGM_CK_SD, 1, false, true>(b, mode, st);
+        return launch_ck_s<SM_SGM_CK_SD, 1, false, false>(b, mode, st);
+    }
     switch (ck_kv(a.D)) {
         case 0:
             if (a.D == 256) return launch_ck_s<SM_SGM_CK_S, 1, false, true>(b, mode, st);

@@ -104,7 +104,8 @@ def test_gf_modes_volume_bits(oracle, mode, H, W, md, idx):
 @pytest.mark.parametrize("agg", ["GF", "NL"])
 @pytest.mark.parametrize("H,W,md,paths,cost", [(48, 64, 31, 4, "censusGrad"), (37, 70, 15, 8, "Census"),
                                                (30, 44, 127, 4, "censusGrad"),
-                                               (21, 30, 199, 4, "censusGrad")])   # checkpointed SGM pairs (GF: signed)
+                                               (21, 30, 199, 4, "censusGrad"),    # checkpointed SGM pairs (GF: signed)
+                                               (19, 26, 159, 8, "censusGrad")])   # + the diagonal pair (4, 6)
 def test_batch_maps_match_oracle(oracle, agg, H, W, md, paths, cost):
     n = 3
     batch = S.make_batch(n, H, W, md + 1, first_index=510)

@@ -335,14 +335,18 @@ def test_shapes_and_edge_cases(oracle, H, W, md, paths):
                                            (16, 24, 131, 4), (17, 33, 255, 4), (23, 7, 199, 4), (40, 41, 255, 4),
                                            (9, 17, 63, 4), (17, 10, 127, 4), (8, 8, 99, 4), (16, 9, 59, 4),
                                            (5, 13, 3, 4), (12, 19, 255, 8), (10, 11, 63, 8), (9, 9, 119, 8),
-                                           (24, 32, 15, 4), (29, 41, 15, 4), (41, 67, 23, 4), (20, 90, 191, 8)])
+                                           (24, 32, 15, 4), (29, 41, 15, 4), (41, 67, 23, 4), (20, 90, 191, 8),
+                                           (2, 2, 131, 8), (9, 17, 255, 8), (23, 7, 199, 8), (40, 41, 255, 8),
+                                           (17, 33, 135, 8), (64, 5, 143, 8)])
 def test_sgm_checkpointed_pairs(oracle, H, W, md, paths):
     """SGM with D % 4 == 0 runs paths 0 / 1 and 2 / 3 as checkpointed pairs (k_sgm_ck: segments of
     8 steps, 4 with 8 disparities per lane): one line per wave for 128 < D <= 256, four lines
     per wave below; lines shorter than, equal to and one longer than a segment, ragged tails, D
     below the layout's full width (lanes past D must enter every segment with FLT_MAX: the
     d + 1 neighbour of the last disparity — the shapes D = 16, 24 found that), 8 paths (the
-    second pair adds into the running sum, paths 4 .. 7 follow as sweeps).  The summed volume (keep_final) and the map bit-exact, and the map
+    second pair adds into the running sum; with D > 128 the diagonal pair (4, 6) is checkpointed
+    too, L5 stored between them: diagonals of 1 .. min(H, W) steps, H < W and H > W, the last
+    path a sweep).  The summed volume (keep_final) and the map bit-exact, and the map
     again through the batch path (no final volume)."""
     pair = S.make_pair(H, W, md + 1, 50 + H + W)
     cfg = oracle.config(H, W, md, sgm_paths=paths)

@@ -49,8 +49,6 @@ struct sm_ctx {
     uint8_t* bgr = nullptr;     // [cap][2][npix][3]
     uint8_t* gray = nullptr;    // [cap][2][npix]
     ulonglong2* code = nullptr; // [cap][2][npix]
-    float* gx = nullptr;        // [cap][2][npix]
-    float* gy = nullptr;
     uint8_t* arms = nullptr;    // [cap][2 views][2 planes][npix] u32: (L | R<<16), (U | D<<16)
     uint8_t* arms_alloc = nullptr;  // arms - front pad of 2 * lag rows (CBCA V sweeps read there)
     size_t arms_bytes = 0;
@@ -368,7 +366,7 @@ sm_status dalloc(sm_ctx* c, T** ptr, size_t count) {
 }
 
 void free_all(sm_ctx* c) {
-    void* ptrs[] = {c->bgr, c->gray, c->code, c->gx, c->gy, c->arms_alloc, c->vm0, c->vm1, c->acc, c->ck, c->lx, c->disp,
+    void* ptrs[] = {c->bgr, c->gray, c->code, c->arms_alloc, c->vm0, c->vm1, c->acc, c->ck, c->lx, c->disp,
                     c->disp1, c->disp_tmp, c->dummy, c->flags, c->flags1, c->px, c->so_trace, c->so_cidx,
                     c->gf_s, c->gf_planes, c->gf_pix, c->gfc_rs, c->gfc_ab, c->gfc_img, c->gfc_pix, c->nl_med, c->nl_ew, c->nl_ints, c->nl_rec,
                     c->nl_table, c->nl_val, c->nl_oup, c->nl_ofin, c->nl_par, c->nl_best, c->nl_mst, c->nl_adj, c->nl_walk,
@@ -429,8 +427,6 @@ struct Bufs {
     uint8_t* bgr;
     uint8_t* gray;
     ulonglong2* code;
-    float* gx;
-    float* gy;
     uint8_t* arms;
     float* vm0;
     float* vm1;
@@ -453,8 +449,6 @@ Bufs at(const sm_ctx* c, int off) {
     b.bgr = c->bgr + o * 2 * np * 3;
     b.gray = c->gray + o * 2 * np;
     b.code = c->code + o * 2 * np;
-    b.gx = c->gx + o * 2 * np;
-    b.gy = c->gy + o * 2 * np;
     b.arms = c->arms + o * 2 * 2 * np * 4;
     b.vm0 = c->vm0 + o * nv;
     b.vm1 = c->vm1 ? c->vm1 + o * nv : nullptr;
@@ -475,7 +469,7 @@ Bufs at(const sm_ctx* c, int off) {
 sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
     const sm_params& p = c->p;
     const int H = p.rows, W = p.cols;
-    const bool census = needs_census(p), grad = p.cost_method == SM_COST_CENSUS_GRAD, arms = needs_arms(p);
+    const bool census = needs_census(p), arms = needs_arms(p);
     const bool flags = p.optimization == SM_OPT_SGM;
     {
         sm::PrepArgs a{};
@@ -485,8 +479,6 @@ sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
         a.pxh = B.pxh;
         a.pxv = B.pxv;
         a.code = B.code;
-        a.gx = B.gx;
-        a.gy = B.gy;
         a.arms = B.arms;
         a.flags = B.flags;
         a.flags1 = flags && p.do_refine ? B.flags1 : nullptr;
@@ -502,12 +494,11 @@ sm_status run_prep(sm_ctx* c, int n, const Bufs& B) {
         a.minL = p.arm_min_l;
         a.cor_thres = p.sgm_cor_dif_thres;
         a.do_census = census;
-        a.do_grad = grad;
         a.do_arms = arms;
         a.do_flags = flags;
         // the packed BGR plane's later readers: the GF image planes, so, refine's properIpol
         a.pack_px = p.aggregation == SM_AGG_GF || p.optimization == SM_OPT_SO || p.do_refine;
-        return timed(c, "prep", (double)n * 2 * c->npix * (1 + 3 + (census ? 16 : 0) + (grad ? 8 : 0) + (arms ? 8 : 0)) +
+        return timed(c, "prep", (double)n * 2 * c->npix * (1 + 3 + (census ? 16 : 0) + (arms ? 8 : 0)) +
                                     (flags ? (double)n * c->npix * n_views(p) : 0),
                      [&] { sm::launch_prep(a, n, c->st); });
     }
@@ -518,8 +509,7 @@ sm_status run_cost(sm_ctx* c, int n, int view, const Bufs& B) {
     sm::CostArgs a{};
     a.vm = view == 0 ? B.vm0 : B.vm1;
     a.code = B.code;
-    a.gx = B.gx;
-    a.gy = B.gy;
+    a.gray = B.gray;
     a.arms = B.arms;
     a.bgr = B.bgr;
     a.H = p.rows;
@@ -1083,8 +1073,6 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     if ((s = dalloc(c, &c->bgr, cap * 2 * c->npix * 3 + 16))) return s;   // tail pad: prep's dword quads (load_quad_bgr)
     if ((s = dalloc(c, &c->gray, cap * 2 * c->npix))) return s;
     if ((s = dalloc(c, &c->code, cap * 2 * c->npix))) return s;
-    if ((s = dalloc(c, &c->gx, cap * 2 * c->npix))) return s;
-    if ((s = dalloc(c, &c->gy, cap * 2 * c->npix))) return s;
     {
         // front pad: V sweeps read rows i - lag >= -2 lag; tail pad: the fast V sweep's arm loads
         // run up to lag + T rows past the last plane's end (sm_cbca.hip NsV clamps later tiles)
@@ -1179,8 +1167,8 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
         if (!(p->aggregation == SM_AGG_CBCA || p->aggregation == SM_AGG_NONE)) c->place_trials = 0;   // (GF / NL scratch not moved)
     }
     if (getenv("SM_TRACE_ALLOC"))   // diagnostics: where the large buffers landed
-        fprintf(stderr, "[alloc] vm0 %p vm1 %p acc %p arms %p code %p gx %p px %p\n", (void*)c->vm0, (void*)c->vm1,
-                (void*)c->acc, (void*)c->arms, (void*)c->code, (void*)c->gx, (void*)c->px);
+        fprintf(stderr, "[alloc] vm0 %p vm1 %p acc %p arms %p code %p px %p\n", (void*)c->vm0, (void*)c->vm1,
+                (void*)c->acc, (void*)c->arms, (void*)c->code, (void*)c->px);
     build_luts(c);
     {
         // auto: the generic fused sweep wins where a pair's volume is large (full resolution:

@@ -19,14 +19,12 @@ struct PrepArgs {
     uint32_t* pxh;              // [n][2][H][W] arm-walk words, horizontal flags (k_pack_arms)
     uint32_t* pxv;              // [n][2][H][W] arm-walk words, vertical flags
     ulonglong2* code;           // [n][2][H][W]
-    float* gx;
-    float* gy;
     uint8_t* arms;              // [n][view][plane][H][W] u32: plane 0 = L | R<<16, plane 1 = U | D<<16
     uint8_t* flags;             // [n][H][W] left image
     uint8_t* flags1;            // [n][H][W] right image (nullptr: not needed)
     int H, W, rv, ru, ring;
     int L, L_out, C_D, C_D_out, minL, cor_thres;
-    int do_census, do_grad, do_arms, do_flags;
+    int do_census, do_arms, do_flags;
     int pack_px;                // the packed-BGR plane px is read later (GF, so, refine)
 };
 
@@ -34,8 +32,7 @@ struct CostArgs {
     float* vm;                  // [n][H][W][D] destination (view's volume)
     int seg;                    // pixels of a row per block (set by launch_cost: <= the LDS capacity)
     const ulonglong2* code;     // [n][2][H][W]
-    const float* gx;            // [n][2][H][W]
-    const float* gy;
+    const uint8_t* gray;        // [n][2][H][W] (censusGrad: the gradients, grad_at)
     const uint8_t* arms;        // [n][view][plane][H][W] u32: plane 0 = L | R<<16, plane 1 = U | D<<16
     const uint8_t* bgr;         // [n][2][H][W][3]
     int H, W, D, view, nwords;

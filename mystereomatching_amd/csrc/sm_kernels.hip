@@ -3,7 +3,7 @@
 // Layout in HBM (per pair b, all packed):
 //   bgr   [b][view][H][W][3] u8  gray [b][view][H][W] u8   (view 0 = left, 1 = right)
 //   code  [b][view][H][W] ulonglong2   (census words 0,1; genCensusCode_NC_Sur h:867-934)
-//   gx,gy [b][view][H][W] f32    (calGrad / calGrad_y cpp:271-386)
+//   (gradients, calGrad / calGrad_y cpp:271-386: recomputed from gray by the cost kernel)
 //   arms  [b][view][plane][H][W] u32 (L | R<<16, U | D<<16; calHorVerDis cpp:2959-3050)
 //   vm    [b][H][W][D] f32       (d innermost, as the reference's CV_32FC(D), cpp:2080)
 //   acc   [b][H][W][D] f32       (SGM path sum in path order, gen_sgm_vm cpp:2031-2056)
@@ -223,25 +223,32 @@ __device__ __forceinline__ void prep_census_grad(const PrepArgs& a, const uint8_
         if (step > 0) w[dep & 1] = cs;
         a.code[o] = make_ulonglong2(w[0], w[1]);
     }
-    // gradients (calGrad / calGrad_y single-channel, cpp:271-350); the one-sided border
-    // differences only touch interior rows/cols, so the reflected halo never enters them
-    if (a.do_grad) {
-        float gxv, gyv;
-        if (u == 0)
-            gxv = (float)(g[1] - g[0]);
-        else if (u == W - 1)
-            gxv = (float)(g[0] - g[-1]);
-        else
-            gxv = 0.5f * (float)(g[1] - g[-1]);
-        if (v == 0)
-            gyv = (float)(g[gw] - g[0]);
-        else if (v == H - 1)
-            gyv = (float)(g[0] - g[-gw]);
-        else
-            gyv = 0.5f * (float)(g[gw] - g[-gw]);
-        a.gx[o] = gxv;
-        a.gy[o] = gyv;
-    }
+}
+
+// gradients of image pixel (v, u) (calGrad / calGrad_y single-channel, cpp:271-350): half the
+// central difference inside, the one-sided difference on the border rows / columns (a 1-pixel
+// wide image has 0, as the prep halo's reflection gave).  The cost kernel evaluates them from the
+// gray plane when it stages a row, so no gradient plane goes through HBM.
+__device__ __forceinline__ float2 grad_at(const uint8_t* G, int v, int u, int H, int W) {
+    const uint8_t* row = G + (size_t)v * W;
+    float gxv, gyv;
+    if (W == 1)
+        gxv = 0.f;
+    else if (u == 0)
+        gxv = (float)((int)row[1] - (int)row[0]);
+    else if (u == W - 1)
+        gxv = (float)((int)row[u] - (int)row[u - 1]);
+    else
+        gxv = 0.5f * (float)((int)row[u + 1] - (int)row[u - 1]);
+    if (H == 1)
+        gyv = 0.f;
+    else if (v == 0)
+        gyv = (float)((int)row[W + u] - (int)row[u]);
+    else if (v == H - 1)
+        gyv = (float)((int)row[u] - (int)row[u - W]);
+    else
+        gyv = 0.5f * (float)((int)row[W + u] - (int)row[u - W]);
+    return make_float2(gxv, gyv);
 }
 
 // One arm walk over an LDS strip of arm-walk words (calHorVerDis, cpp:2959-3050): sp = the centre
@@ -374,7 +381,7 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
             }
         }
     };
-    if (a.do_census || a.do_grad)
+    if (a.do_census)
         fill(gt, gw * gh, [&](int i) -> uint32_t {
             const int ty = i / gw, tx = i - ty * gw;
             const int vv = reflect101(v0 - hv + ty, H), uu = reflect101(u0 - hu + tx, W);
@@ -457,21 +464,22 @@ __global__ __launch_bounds__(256) void k_prep(const PrepArgs a) {
 // Split prep (SM_PREP_SPLIT): two kernels that make the arm-walk words in LDS from the colour
 // bytes, so no packed plane (px / pxh / pxv) goes through HBM, and whose tiles are long along
 // their walk axis, so the walk halo is re-read 1.3-2.1 times instead of the 16-row tile's 5.3:
-//   k_prep_h  tiles of 256 columns x 4 rows: census, gradients, the SGM penalty flags and the
+//   k_prep_h  tiles of 256 columns x 8 rows: census, the SGM penalty flags and the
 //             L / R arms (arm plane 0), from a gray tile and a strip of packed pixels (rows
 //             v0 - 1 .. v0 + 4, columns u0 - Lo - 1 .. u0 + 256 + Lo);
-//   k_prep_v  tiles of 64 columns x 64 rows: the U / D arms (arm plane 1) from a strip of rows
-//             v0 - Lo - 1 .. v0 + 64 + Lo.
+//   k_prep_v  tiles of 64 columns x 128 rows: the U / D arms (arm plane 1) from a strip of rows
+//             v0 - Lo - 1 .. v0 + 128 + Lo.
 // The packed-BGR plane is made (k_pack_bgr) only for the kernels that read it (GF, so, refine).
 // ---------------------------------------------------------------------------------------
 #ifndef SM_PREP_SPLIT
 #define SM_PREP_SPLIT 1
 #endif
 #ifndef SM_PREP_HTH
-#define SM_PREP_HTH 4    // k_prep_h tile rows
+#define SM_PREP_HTH 8    // k_prep_h tile rows (4 -> 8: gray / colour halo re-reads 2.5 / 1.5 -> 1.75 / 1.25)
 #endif
 #ifndef SM_PREP_VTH
-#define SM_PREP_VTH 64   // k_prep_v tile rows
+#define SM_PREP_VTH 128  // k_prep_v tile rows (64 -> 128: colour strip re-read 2.1 -> 1.55; prep
+                         // 0.772 -> 0.736 ms at full resolution, profiles/r6/prep)
 #endif
 constexpr int PH_TW = 256, PH_TH = SM_PREP_HTH, PV_TW = 64, PV_TH = SM_PREP_VTH;
 #ifndef SM_PREP_QUAD
@@ -588,7 +596,7 @@ __global__ __launch_bounds__(256) void k_prep_h(const PrepArgs a) {
     uint8_t* gt = prep_raw;
     const bool words = a.do_arms;
     const bool flags = a.do_flags && (view == 0 || a.flags1);
-    if (a.do_census || a.do_grad) {
+    if (a.do_census) {
         const uint8_t* G = a.gray + img * npix;
         prep_fill(gt, gw * gh, [&](int i) -> uint32_t {
             const int ty = i / gw, tx = i - ty * gw;
@@ -987,8 +995,9 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
         const int u = u0 + i;
         if (CEN) fcode[i] = a.code[frow + u];
         if (GRAD) {
-            fgx[i] = a.gx[frow + u];
-            fgy[i] = a.gy[frow + u];
+            const float2 gr = grad_at(a.gray + frow - (size_t)v * W, v, u, H, W);
+            fgx[i] = gr.x;
+            fgy[i] = gr.y;
             float wa = 1.f, wb = 1.f;
             if (a.grad_adaptive) {
                 const uint32_t* planes = (const uint32_t*)a.arms + ((size_t)b * 2 + fview) * 2 * npix + (size_t)v * W + u;
@@ -1015,8 +1024,9 @@ __global__ __launch_bounds__(256) void k_cost(const CostArgs a) {
         if (q >= 0 && q < W) {
             if (CEN) c = a.code[mrow + q];
             if (GRAD) {
-                w2 = __float_as_uint(a.gx[mrow + q]);
-                w3 = __float_as_uint(a.gy[mrow + q]);
+                const float2 gr = grad_at(a.gray + mrow - (size_t)v * W, v, q, H, W);
+                w2 = __float_as_uint(gr.x);
+                w3 = __float_as_uint(gr.y);
             }
             if (ADM) {
                 const uint8_t* p = a.bgr + (mrow + q) * 3;

@@ -124,6 +124,8 @@ struct sm_ctx {
     int dl_slot = 0;            // ev_dl slot of the next async download
     int dl_count = 0;
     hipEvent_t ev_up[2] = {};   // an async upload's copies done: main stream, side stream
+    hipEvent_t ev_in[2] = {};   // a pipelined run's group k has read its input images (after the cost volume)
+    hipStream_t ust = nullptr;  // copy stream of an async upload that overlaps the groups' sweeps
     bool up_split = false;      // the async upload's second group went on the side stream
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
     hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
@@ -401,7 +403,12 @@ void free_all(sm_ctx* c) {
         hipStreamDestroy(c->cst);
         c->cst = nullptr;
     }
-    for (hipEvent_t* ev : {&c->ev_dl[0], &c->ev_dl[1], &c->ev_up[0], &c->ev_up[1]})
+    if (c->ust) {
+        hipStreamSynchronize(c->ust);
+        hipStreamDestroy(c->ust);
+        c->ust = nullptr;
+    }
+    for (hipEvent_t* ev : {&c->ev_dl[0], &c->ev_dl[1], &c->ev_up[0], &c->ev_up[1], &c->ev_in[0], &c->ev_in[1]})
         if (*ev) {
             hipEventDestroy(*ev);
             *ev = nullptr;
@@ -1496,6 +1503,9 @@ sm_status sm_upload_batch(sm_ctx* c, int32_t n, const uint8_t* lbgr, const uint8
 #ifndef SM_STAGGER_STAGE
 #define SM_STAGGER_STAGE 1   // 0: CBCA groups also start after the previous group's whole CBCA (A/B)
 #endif
+#ifndef SM_UP_EARLY
+#define SM_UP_EARLY 1   // async uploads into a pipelined context wait for the inputs' last reader, not the group's end
+#endif
 static sm_status place_volumes(sm_ctx* c, int k, int n, float reg_lambda);
 
 sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
@@ -1562,6 +1572,18 @@ sm_status sm_run(sm_ctx* c, int32_t n, float reg_lambda, int16_t* disp_out) {
             if ((s_out = run_cost(c, m2, 0, B))) break;
             if (right_view(c->p) && (s_out = run_cost(c, m2, 1, B))) break;
             if ((s_out = run_other_agg(c, m2, B, SM_FUSE_SOLVE_ALL, w))) break;   // SolveAll fused into GF / NL
+        }
+        // the group's input images are read by prep and the cost volume only (CBCA + SGM, no
+        // refinement: the pipelined form): the next call's async upload may overwrite them now
+        if (piped && SM_UP_EARLY) {
+            if (!c->ev_in[k] && (e = hipEventCreateWithFlags(&c->ev_in[k], hipEventDisableTiming)) != hipSuccess) {
+                s_out = hip_fail(c, e, "hipEventCreate (inputs read)");
+                break;
+            }
+            if ((e = hipEventRecord(c->ev_in[k], c->st)) != hipSuccess) {
+                s_out = hip_fail(c, e, "hipEventRecord (inputs read)");
+                break;
+            }
         }
         if (ns > 1 && early) c->stagger_ev = c->xev[1 + k % 8];
         for (int v = 0; v < n_views(c->p) && !s_out && !pipe; v++) {
@@ -1769,19 +1791,34 @@ sm_status sm_upload_batch_async(sm_ctx* c, int32_t n, const uint8_t* lbgr, const
         if (!c->ev_up[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_up[i], hipEventDisableTiming));
     const sm_params& p = c->p;
     const size_t H = p.rows, W = p.cols, crow = W * 3;
+    // early: the copies go on their own stream as soon as each group's previous inputs are read
+    // (ev_in, recorded after its cost volume), so they overlap that group's CBCA and SGM; the
+    // group's next kernels wait for its copies (ev_up)
+    const bool early = split && SM_UP_EARLY && c->ev_in[0] && c->ev_in[1];
+    if (early && !c->ust) HIP_TRY(c, hipStreamCreateWithFlags(&c->ust, hipStreamNonBlocking));
+    for (int grp = 0; grp < (early ? 2 : 1); grp++) {
+        if (early) HIP_TRY(c, hipStreamWaitEvent(c->ust, c->ev_in[grp], 0));
+        const int b0 = early ? grp * g : 0, b1 = early ? std::min(n, (grp + 1) * g) : n;
     for (int view = 0; view < 2; view++) {
         const uint8_t* src = view == 0 ? lbgr : rbgr;
         const uint8_t* gsrc = view == 0 ? lgray : rgray;
-        for (int b = 0; b < n; b++) {
-            hipStream_t st = (split && b >= g) ? c->xst[0] : c->st;
+        for (int b = b0; b < b1; b++) {
+            hipStream_t st = early ? c->ust : (split && b >= g) ? c->xst[0] : c->st;
             uint8_t* dst = c->bgr + ((size_t)b * 2 + view) * c->npix * 3;
             HIP_TRY(c, hipMemcpy2DAsync(dst, crow, src + (size_t)b * H * crow, crow, crow, H, hipMemcpyDefault, st));
             uint8_t* gdst = c->gray + ((size_t)b * 2 + view) * c->npix;
             HIP_TRY(c, hipMemcpy2DAsync(gdst, W, gsrc + (size_t)b * H * W, W, W, H, hipMemcpyDefault, st));
         }
     }
-    HIP_TRY(c, hipEventRecord(c->ev_up[0], c->st));
-    if (split) HIP_TRY(c, hipEventRecord(c->ev_up[1], c->xst[0]));
+        if (early) {
+            HIP_TRY(c, hipEventRecord(c->ev_up[grp], c->ust));
+            HIP_TRY(c, hipStreamWaitEvent(grp == 0 ? c->st : c->xst[0], c->ev_up[grp], 0));
+        }
+    }
+    if (!early) {
+        HIP_TRY(c, hipEventRecord(c->ev_up[0], c->st));
+        if (split) HIP_TRY(c, hipEventRecord(c->ev_up[1], c->xst[0]));
+    }
     c->up_split = split;
     c->n_loaded = n;
     c->stage = 1;

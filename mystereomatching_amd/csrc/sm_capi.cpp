@@ -1071,7 +1071,14 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     HIP_TRY(c, hipGetDeviceCount(&ndev));
     if (hip_device < 0 || hip_device >= ndev) return fail(c, SM_EINVAL, "hip_device out of range");
     HIP_TRY(c, hipSetDevice(hip_device));
+    // the main, side, download and upload streams back to back, so that the runtime's round-robin
+    // over its GPU_MAX_HW_QUEUES (4) hardware queues gives each its own: an upload or map copy that
+    // shared a group's queue would wait behind that group's kernels (in-order queue), whatever
+    // events it was meant to wait for
     HIP_TRY(c, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[0], hipStreamNonBlocking));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->ust, hipStreamNonBlocking));
     c->cap = p->batch_capacity;
     c->npix = (size_t)p->rows * p->cols;
     c->nvol = c->npix * (size_t)p->num_disparities;
@@ -1722,11 +1729,9 @@ sm_status sm_download_disp_async(sm_ctx* c, int32_t n, int16_t* disp_out) {
     if (s) return s;
     if (!disp_out || n < 1 || n > c->cap) return fail(c, SM_EINVAL, "bad arguments");
     if (c->stage < 4) return fail(c, SM_ESTATE, "no disparity map yet");
-    if (!c->cst) {
-        HIP_TRY(c, hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_run, hipEventDisableTiming));
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
-    }
+    if (!c->cst) HIP_TRY(c, hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
+    if (!c->ev_run) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_run, hipEventDisableTiming));
+    if (!c->ev_copy) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
     if (!c->ev_copy2) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_copy2, hipEventDisableTiming));
     HIP_TRY(c, hipEventRecord(c->ev_run, c->st));
     HIP_TRY(c, hipStreamWaitEvent(c->cst, c->ev_run, 0));

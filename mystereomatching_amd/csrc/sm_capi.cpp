@@ -23,6 +23,10 @@
 
 #include "sm_kernels.h"
 
+#ifndef SM_EAGER_CST
+#define SM_EAGER_CST 0   // 1: the map-copy stream is created with the others at sm_create (A/B)
+#endif
+
 namespace {
 
 struct ProfRec {
@@ -1071,14 +1075,17 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     HIP_TRY(c, hipGetDeviceCount(&ndev));
     if (hip_device < 0 || hip_device >= ndev) return fail(c, SM_EINVAL, "hip_device out of range");
     HIP_TRY(c, hipSetDevice(hip_device));
-    // the main, side, download and upload streams back to back, so that the runtime's round-robin
-    // over its GPU_MAX_HW_QUEUES (4) hardware queues gives each its own: an upload or map copy that
-    // shared a group's queue would wait behind that group's kernels (in-order queue), whatever
-    // events it was meant to wait for
+    // the main, side and upload streams back to back, so that the runtime's round-robin over its
+    // GPU_MAX_HW_QUEUES (4) hardware queues gives each its own: an upload that shared a group's
+    // queue would wait behind that group's kernels (in-order queue), whatever events it was meant
+    // to wait for.  (The map-copy stream stays lazy: created with the others, SM_EAGER_CST, the
+    // Teddy x16 timed loop measured 2.30-2.53 against 2.22-2.44 ms, profiles/r6/e2e_streams/cst_ab.)
     HIP_TRY(c, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[0], hipStreamNonBlocking));
-    HIP_TRY(c, hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
     HIP_TRY(c, hipStreamCreateWithFlags(&c->ust, hipStreamNonBlocking));
+#if SM_EAGER_CST
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
+#endif
     c->cap = p->batch_capacity;
     c->npix = (size_t)p->rows * p->cols;
     c->nvol = c->npix * (size_t)p->num_disparities;

@@ -23,9 +23,6 @@
 
 #include "sm_kernels.h"
 
-#ifndef SM_EAGER_CST
-#define SM_EAGER_CST 0   // 1: the map-copy stream is created with the others at sm_create (A/B)
-#endif
 
 namespace {
 
@@ -129,7 +126,11 @@ struct sm_ctx {
     int dl_count = 0;
     hipEvent_t ev_up[2] = {};   // an async upload's copies done: main stream, side stream
     hipEvent_t ev_in[2] = {};   // a pipelined run's group k has read its input images (after the cost volume)
-    hipStream_t ust = nullptr;  // copy stream of an async upload that overlaps the groups' sweeps
+    // (an early async upload goes on the null stream: the runtime spreads streams round-robin over
+    // GPU_MAX_HW_QUEUES (4) in-order hardware queues, and a fifth stream of the context shared one
+    // with a group or the map copies, whose kernels / copies the upload then waited behind; the
+    // null stream's queue carries nothing else on the hot path, and the context's streams are
+    // non-blocking, so it implies no synchronisation with them)
     bool up_split = false;      // the async upload's second group went on the side stream
     hipStream_t xst[3] = {nullptr, nullptr, nullptr};  // extra streams when nstreams > 1
     hipStream_t cst = nullptr;  // copy stream of sm_download_disp_async
@@ -406,11 +407,6 @@ void free_all(sm_ctx* c) {
         hipStreamSynchronize(c->cst);
         hipStreamDestroy(c->cst);
         c->cst = nullptr;
-    }
-    if (c->ust) {
-        hipStreamSynchronize(c->ust);
-        hipStreamDestroy(c->ust);
-        c->ust = nullptr;
     }
     for (hipEvent_t* ev : {&c->ev_dl[0], &c->ev_dl[1], &c->ev_up[0], &c->ev_up[1], &c->ev_in[0], &c->ev_in[1]})
         if (*ev) {
@@ -1075,17 +1071,7 @@ sm_status sm_create(sm_ctx** out, const sm_params* p, int32_t hip_device) {
     HIP_TRY(c, hipGetDeviceCount(&ndev));
     if (hip_device < 0 || hip_device >= ndev) return fail(c, SM_EINVAL, "hip_device out of range");
     HIP_TRY(c, hipSetDevice(hip_device));
-    // the main, side and upload streams back to back, so that the runtime's round-robin over its
-    // GPU_MAX_HW_QUEUES (4) hardware queues gives each its own: an upload that shared a group's
-    // queue would wait behind that group's kernels (in-order queue), whatever events it was meant
-    // to wait for.  (The map-copy stream stays lazy: created with the others, SM_EAGER_CST, the
-    // Teddy x16 timed loop measured 2.30-2.53 against 2.22-2.44 ms, profiles/r6/e2e_streams/cst_ab.)
     HIP_TRY(c, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    HIP_TRY(c, hipStreamCreateWithFlags(&c->xst[0], hipStreamNonBlocking));
-    HIP_TRY(c, hipStreamCreateWithFlags(&c->ust, hipStreamNonBlocking));
-#if SM_EAGER_CST
-    HIP_TRY(c, hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
-#endif
     c->cap = p->batch_capacity;
     c->npix = (size_t)p->rows * p->cols;
     c->nvol = c->npix * (size_t)p->num_disparities;
@@ -1807,15 +1793,15 @@ sm_status sm_upload_batch_async(sm_ctx* c, int32_t n, const uint8_t* lbgr, const
     // (ev_in, recorded after its cost volume), so they overlap that group's CBCA and SGM; the
     // group's next kernels wait for its copies (ev_up)
     const bool early = split && SM_UP_EARLY && c->ev_in[0] && c->ev_in[1];
-    if (early && !c->ust) HIP_TRY(c, hipStreamCreateWithFlags(&c->ust, hipStreamNonBlocking));
+    const hipStream_t ust = nullptr;
     for (int grp = 0; grp < (early ? 2 : 1); grp++) {
-        if (early) HIP_TRY(c, hipStreamWaitEvent(c->ust, c->ev_in[grp], 0));
+        if (early) HIP_TRY(c, hipStreamWaitEvent(ust, c->ev_in[grp], 0));
         const int b0 = early ? grp * g : 0, b1 = early ? std::min(n, (grp + 1) * g) : n;
     for (int view = 0; view < 2; view++) {
         const uint8_t* src = view == 0 ? lbgr : rbgr;
         const uint8_t* gsrc = view == 0 ? lgray : rgray;
         for (int b = b0; b < b1; b++) {
-            hipStream_t st = early ? c->ust : (split && b >= g) ? c->xst[0] : c->st;
+            hipStream_t st = early ? ust : (split && b >= g) ? c->xst[0] : c->st;
             uint8_t* dst = c->bgr + ((size_t)b * 2 + view) * c->npix * 3;
             HIP_TRY(c, hipMemcpy2DAsync(dst, crow, src + (size_t)b * H * crow, crow, crow, H, hipMemcpyDefault, st));
             uint8_t* gdst = c->gray + ((size_t)b * 2 + view) * c->npix;
@@ -1823,7 +1809,7 @@ sm_status sm_upload_batch_async(sm_ctx* c, int32_t n, const uint8_t* lbgr, const
         }
     }
         if (early) {
-            HIP_TRY(c, hipEventRecord(c->ev_up[grp], c->ust));
+            HIP_TRY(c, hipEventRecord(c->ev_up[grp], ust));
             HIP_TRY(c, hipStreamWaitEvent(grp == 0 ? c->st : c->xst[0], c->ev_up[grp], 0));
         }
     }
